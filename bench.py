@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Headline benchmark: FlashAttention forward TFLOP/s + HBM GB/s at
+(B,H,N,d) = (8,16,4096,64) bf16 per GPU (BASELINE.json metric, configs[2]).
+
+    python bench.py --gpus N --steps K --warmup W
+
+One "step" = one pass of the hot path (the bf16 MFMA forward kernel) over one
+(8,16,4096,64) batch of synthetic Q/K/V already resident in HBM. Multi-GPU: one
+process per GPU (torch.distributed.run); the batch x heads axis is sharded, each
+rank owns its own (8,16,4096,64) slice of a global (8N,16,4096,64) problem
+(weak scaling, no collective inside the timed region). An RCCL all-gather of the
+output shards over xGMI (BASELINE config 4's exchange step) is timed separately
+and reported under "allgather".
+
+rank 0 prints ONE JSON line with the contract fields plus:
+  roofline     : achieved TFLOP/s of the forward kernel (algorithmic flops / mean
+                 kernel duration from HIP events on the launch stream) vs the dense
+                 bf16 MFMA peak; "traffic" = HBM bytes per launch from the committed
+                 rocprofv3 PMC capture (profiles/), or null.
+  cpu_baseline : the C restatement of the reference's CPU fast_ops attention
+                 (oracle/attn_ref.c), timed on a bounded sample of heads of the same
+                 workload on this host (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "llmsys-project-flashattn_amd"))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 flop/clk x 2.4 GHz (MI355X_MICROARCH.md, dense)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBPS = 8000.0
+WORKLOAD = (8, 16, 4096, 64)
+
+
+def fwd_flops(B, H, N, d, causal=False):
+    f = 4.0 * B * H * N * N * d
+    return f / 2 if causal else f
+
+
+def fwd_bytes(B, H, N, d, esize=2):
+    # read Q, K, V + write O, plus the fp32 row statistics m and l
+    return 4.0 * B * H * N * d * esize + 2.0 * B * H * N * 4
+
+
+def make_inputs(torch, shape, dtype, seed, rank):
+    """Synthetic N(0,1) inputs; shard r of the global tensor = global batch rows
+    [r*B, (r+1)*B), generated from (seed, global batch index)."""
+    B, H, N, d = shape
+    out = torch.empty(shape, dtype=dtype, device="cuda")
+    g = torch.Generator(device="cuda")
+    for b in range(B):
+        g.manual_seed(seed * 1000003 + rank * B + b)
+        out[b].copy_(torch.randn((H, N, d), generator=g, device="cuda", dtype=torch.float32))
+    return out
+
+
+def time_kernel(torch, fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(steps):
+        fn()
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps  # ms per launch
+
+
+def cpu_baseline(shape, seconds=10.0):
+    """Time the C oracle on a bounded sample of (b,h) heads at full N and d."""
+    import numpy as np
+    from oracle import cref
+    B, H, N, d = shape
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = min(threads or avail, avail, 16)
+    rng = np.random.default_rng(0)
+    one = [rng.standard_normal((1, N, d)).astype(np.float32) for _ in range(3)]
+    t0 = time.perf_counter()
+    cref.attn_fwd(*one, causal=False, nthreads=threads)
+    t_one = time.perf_counter() - t0
+    heads = max(threads, min(B * H, int(seconds / max(t_one, 1e-6))))
+    heads = max(1, (heads // threads) * threads)
+    qkv = [rng.standard_normal((heads, N, d)).astype(np.float32) for _ in range(3)]
+    t0 = time.perf_counter()
+    cref.attn_fwd(*qkv, causal=False, nthreads=threads)
+    dt = time.perf_counter() - t0
+    flops = fwd_flops(1, heads, N, d)
+    return {
+        "value": round(flops / dt / 1e12, 6),
+        "unit": "TFLOP/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{heads} of {B*H} (b,h) heads at N={N}, d={d}, fp32 (C restatement of the "
+                  f"reference fast_ops attention, oracle/attn_ref.c), {dt:.1f} s",
+        "seconds": round(dt, 2),
+    }
+
+
+def load_pmc_traffic(tag):
+    path = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        with open(path) as f:
+            j = json.load(f)
+        return j.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    except Exception:
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--causal", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-extra", action="store_true", help="skip the extra (bwd, fp32) legs")
+    ap.add_argument("--policy", type=int, default=0, help="0 auto, 1 generic kernels only")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from minitorch import _hip
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes",
+                  file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    _hip.lib().mt_flash_set_kernel_policy(args.policy)
+
+    B, H, N, d = WORKLOAD
+    q, k, v = (make_inputs(torch, WORKLOAD, torch.bfloat16, s, rank) for s in (1, 2, 3))
+    o = torch.empty_like(q)
+    m = torch.empty((B, H, N), dtype=torch.float32, device="cuda")
+    l = torch.empty_like(m)
+
+    def step():
+        _hip.flash_fwd(q, k, v, args.causal, out=o, m=m, l=l)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(st)
+    for _ in range(args.steps):
+        step()
+    ev1.record(st)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        t = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+
+    flops_rank = fwd_flops(B, H, N, d, args.causal)
+    total_flops = flops_rank * world * args.steps
+    value = total_flops / wall / 1e12
+    ms_per_step = wall * 1e3 / args.steps
+    achieved = flops_rank / (kern_ms * 1e-3) / 1e12
+    alg_bytes = fwd_bytes(B, H, N, d)
+    traffic, traffic_src = load_pmc_traffic("fwd_bf16_c3" + ("_causal" if args.causal else ""))
+
+    result = {
+        "metric": "FlashAttn fwd TFLOP/s (+ HBM GB/s) at (B,H,N,d)=(8,16,4096,64) per GPU",
+        "value": round(value, 3),
+        "unit": "TFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic N(0,1) Q/K/V, resident in HBM",
+        "config": {"workload": "flash_attention_fwd", "B": B * world, "H": H, "N": N, "d": d,
+                   "per_gpu_shape": [B, H, N, d], "causal": bool(args.causal),
+                   "parallelism": f"bh-shard x{world}"},
+        "hbm_gbps": round(alg_bytes * world * args.steps / wall / 1e9, 2),
+        "roofline": {
+            "bound": "mfma",
+            "achieved": round(achieved, 2),
+            "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes": alg_bytes,
+            "algorithmic_flops": flops_rank,
+            "kernel_ms": round(kern_ms, 5),
+        },
+    }
+
+    # RCCL all-gather of the output shards (BASELINE config 4's exchange step).
+    if world > 1:
+        gathered = torch.empty((world,) + tuple(o.shape), dtype=o.dtype, device="cuda")
+
+        def step_gather():
+            step()
+            dist.all_gather_into_tensor(gathered, o)
+
+        for _ in range(3):
+            step_gather()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_gather()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+        tg = float(tg[0])
+        result["allgather"] = {
+            "ms_per_step_fwd_plus_allgather": round(tg * 1e3 / args.steps, 4),
+            "tflops_fwd_plus_allgather": round(total_flops / tg / 1e12, 3),
+            "gathered_bytes_per_rank": int(o.numel() * o.element_size() * world),
+        }
+
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra = {}
+        # causal forward, same workload
+        extra["fwd_causal_tflops"] = round(
+            fwd_flops(B, H, N, d, True) / (time_kernel(
+                torch, lambda: _hip.flash_fwd(q, k, v, True, out=o, m=m, l=l), 20, 3) * 1e-3) / 1e12, 2)
+        # backward (bf16), FA-2 flop convention 2.5 x fwd
+        do = make_inputs(torch, WORKLOAD, torch.bfloat16, 4, rank)
+        _hip.flash_fwd(q, k, v, False, out=o, m=m, l=l)
+        ws = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(B, H, N, d) // 4,
+                         dtype=torch.float32, device="cuda")
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
+        bwd_ms = time_kernel(torch, lambda: _hip.flash_bwd(q, k, v, o, do, m, l, False, dq=dq, dk=dk,
+                                                          dv=dv, workspace=ws), 10, 2)
+        extra["bwd_ms"] = round(bwd_ms, 4)
+        extra["bwd_tflops"] = round(2.5 * fwd_flops(B, H, N, d) / (bwd_ms * 1e-3) / 1e12, 2)
+        del do, dq, dk, dv, ws
+        # config 2: (8,16,1024,64) fp32 forward
+        c2 = (8, 16, 1024, 64)
+        q2, k2, v2 = (make_inputs(torch, c2, torch.float32, s, 0) for s in (5, 6, 7))
+        c2_ms = time_kernel(torch, lambda: _hip.flash_fwd(q2, k2, v2, False), 20, 3)
+        extra["c2_fp32_fwd_ms"] = round(c2_ms, 4)
+        extra["c2_fp32_fwd_tflops"] = round(fwd_flops(*c2) / (c2_ms * 1e-3) / 1e12, 2)
+        extra["c2_fp32_frac_of_f32_peak"] = round(extra["c2_fp32_fwd_tflops"] / PEAK_F32_TFLOPS, 4)
+        result["extra"] = extra
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(WORKLOAD)
+        cpu["gpu_over_cpu"] = round(value / cpu["value"], 1) if cpu["value"] > 0 else None
+        result["cpu_baseline"] = cpu
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,221 @@
+// C ABI for the FlashAttention kernels (include/minitorch_hip.h).
+//
+// Device-pointer entry points (mt_flash_attn_*) plus host-pointer wrappers with the
+// exact names and argument order of the reference launchers
+// (src/flashattention_kernel.cu:259, :352, :694, :761), so the reference's ctypes
+// binding (minitorch/cuda_kernel_ops.py:605-892) can load this library unchanged.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/minitorch_hip.h"
+#include "fa_common.h"
+
+namespace mt {
+hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
+                              hipStream_t st);
+hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, hipStream_t st, bool* handled);
+hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
+                              hipStream_t st);
+
+static thread_local char g_err[512] = "";
+static int g_kernel_policy = 0;  // 0: auto (fast bf16 kernel when eligible), 1: generic only
+
+int set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return 1;
+}
+int check_hip(hipError_t e, const char* where) {
+  if (e == hipSuccess) return 0;
+  return set_error("%s: %s", where, hipGetErrorString(e));
+}
+
+static void fill_strides(int64_t dst[3], const int64_t* src, int64_t H, int64_t N, int64_t d) {
+  if (src) {
+    dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
+  } else {
+    dst[0] = H * N * d; dst[1] = N * d; dst[2] = d;
+  }
+}
+
+// 16-B vector path allowed: d and every row/batch/head stride a multiple of the
+// 16-B element count, and every base pointer 16-B aligned.
+static bool vec_ok(int64_t d, int esize, std::initializer_list<const int64_t*> strides,
+                   std::initializer_list<const void*> ptrs) {
+  const int64_t epc = 16 / esize;
+  if (d % epc) return false;
+  for (const int64_t* s : strides)
+    for (int i = 0; i < 3; ++i)
+      if (s[i] % epc) return false;
+  for (const void* p : ptrs)
+    if (p && ((uintptr_t)p & 15)) return false;
+  return true;
+}
+
+static int check_sizes(int dtype, int64_t B, int64_t H, int64_t N, int64_t d) {
+  if (dtype != MT_F32 && dtype != MT_BF16) return set_error("unsupported dtype %d", dtype);
+  if (B <= 0 || H <= 0 || N <= 0 || d <= 0)
+    return set_error("bad sizes B=%lld H=%lld N=%lld d=%lld", (long long)B, (long long)H,
+                     (long long)N, (long long)d);
+  if (N > (1 << 30) || B * H > (1ll << 31) - 1 || d > 4096)
+    return set_error("sizes out of range (N=%lld, B*H=%lld, d=%lld; d <= 4096)", (long long)N,
+                     (long long)(B * H), (long long)d);
+  return 0;
+}
+
+}  // namespace mt
+
+using namespace mt;
+
+extern "C" {
+
+const char* mt_last_error(void) { return g_err; }
+void mt_flash_set_kernel_policy(int policy) { g_kernel_policy = policy; }
+int mt_abi_version(void) { return 1; }
+
+int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const void* v,
+                      void* o, float* m, float* l, int64_t B, int64_t H, int64_t N, int64_t d,
+                      const int64_t* q_strides, const int64_t* k_strides,
+                      const int64_t* v_strides, const int64_t* o_strides, void* stream) {
+  if (check_sizes(dtype, B, H, N, d)) return 1;
+  if (!q || !k || !v || !o) return set_error("mt_flash_attn_fwd: null tensor pointer");
+  AttnArgs a;
+  memset(&a, 0, sizeof(a));
+  a.q = q; a.k = k; a.v = v; a.out = o; a.m = m; a.l = l;
+  fill_strides(a.sq, q_strides, H, N, d);
+  fill_strides(a.sk, k_strides, H, N, d);
+  fill_strides(a.sv, v_strides, H, N, d);
+  fill_strides(a.so, o_strides, H, N, d);
+  a.B = (int)B; a.H = (int)H; a.N = (int)N; a.d = (int)d;
+  a.scale = (float)(1.0 / sqrt((double)d));
+  a.scale_log2 = (float)(1.4426950408889634 / sqrt((double)d));
+  const int es = dtype == MT_BF16 ? 2 : 4;
+  const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so}, {q, k, v, o});
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MT_BF16 && vec && g_kernel_policy == 0) {
+    bool handled = false;
+    hipError_t e = launch_fwd_fast(a, causal != 0, st, &handled);
+    if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");
+  }
+  return check_hip(launch_fwd_generic(a, dtype == MT_BF16, vec, causal != 0, st),
+                   "mt_flash_attn_fwd");
+}
+
+int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t d) {
+  (void)d;
+  return 2 * B * H * N * (int64_t)sizeof(float);
+}
+
+int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const void* v,
+                      const void* o, const void* dout, const float* m, const float* l,
+                      void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
+                      int64_t d, const int64_t* strides, void* workspace, void* stream) {
+  if (check_sizes(dtype, B, H, N, d)) return 1;
+  if (!q || !k || !v || !o || !dout || !m || !l || !dq || !dk || !dv || !workspace)
+    return set_error("mt_flash_attn_bwd: null pointer argument");
+  AttnArgs a;
+  memset(&a, 0, sizeof(a));
+  a.q = q; a.k = k; a.v = v; a.o = o; a.dout = dout;
+  a.dq = dq; a.dk = dk; a.dv = dv;
+  a.m = (float*)m; a.l = (float*)l;
+  a.lse2 = (float*)workspace;
+  a.delta = a.lse2 + B * H * N;
+  int64_t* dst[8] = {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv};
+  for (int i = 0; i < 8; ++i) fill_strides(dst[i], strides ? strides + 3 * i : nullptr, H, N, d);
+  a.B = (int)B; a.H = (int)H; a.N = (int)N; a.d = (int)d;
+  a.scale = (float)(1.0 / sqrt((double)d));
+  a.scale_log2 = (float)(1.4426950408889634 / sqrt((double)d));
+  const int es = dtype == MT_BF16 ? 2 : 4;
+  const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv},
+                          {q, k, v, o, dout, dq, dk, dv});
+  return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream),
+                   "mt_flash_attn_bwd");
+}
+
+// ---- reference-compatible host-pointer wrappers ---------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+static int host_fwd(float* Q, float* K, float* V, float* O, float* l, float* m, int B, int nh,
+                    int N, int d, int causal, const char* name) {
+  const size_t n = (size_t)B * nh * N * d, r = (size_t)B * nh * N;
+  DevBuf dq, dk, dv, dof, dm, dl;
+  if (check_hip(hipMalloc(&dq.p, n * 4), name) || check_hip(hipMalloc(&dk.p, n * 4), name) ||
+      check_hip(hipMalloc(&dv.p, n * 4), name) || check_hip(hipMalloc(&dof.p, n * 4), name) ||
+      check_hip(hipMalloc(&dm.p, r * 4), name) || check_hip(hipMalloc(&dl.p, r * 4), name))
+    goto fail;
+  if (check_hip(hipMemcpy(dq.p, Q, n * 4, hipMemcpyHostToDevice), name) ||
+      check_hip(hipMemcpy(dk.p, K, n * 4, hipMemcpyHostToDevice), name) ||
+      check_hip(hipMemcpy(dv.p, V, n * 4, hipMemcpyHostToDevice), name))
+    goto fail;
+  if (mt_flash_attn_fwd(MT_F32, causal, dq.p, dk.p, dv.p, dof.p, (float*)dm.p, (float*)dl.p, B, nh,
+                        N, d, nullptr, nullptr, nullptr, nullptr, nullptr))
+    goto fail;
+  if (check_hip(hipDeviceSynchronize(), name) ||
+      check_hip(hipMemcpy(O, dof.p, n * 4, hipMemcpyDeviceToHost), name) ||
+      check_hip(hipMemcpy(m, dm.p, r * 4, hipMemcpyDeviceToHost), name) ||
+      check_hip(hipMemcpy(l, dl.p, r * 4, hipMemcpyDeviceToHost), name))
+    goto fail;
+  return 0;
+fail:
+  fprintf(stderr, "%s failed: %s\n", name, g_err);
+  return 1;
+}
+
+static int host_bwd(float* Q, float* K, float* V, float* O, float* dQ, float* dK, float* dV,
+                    float* dO, float* l, float* m, int B, int nh, int N, int d, int causal,
+                    const char* name) {
+  const size_t n = (size_t)B * nh * N * d, r = (size_t)B * nh * N;
+  DevBuf bufs[11];
+  float* hin[5] = {Q, K, V, O, dO};
+  for (int i = 0; i < 8; ++i)
+    if (check_hip(hipMalloc(&bufs[i].p, n * 4), name)) goto fail;
+  if (check_hip(hipMalloc(&bufs[8].p, r * 4), name) || check_hip(hipMalloc(&bufs[9].p, r * 4), name) ||
+      check_hip(hipMalloc(&bufs[10].p, (size_t)mt_flash_attn_bwd_workspace_bytes(B, nh, N, d)), name))
+    goto fail;
+  for (int i = 0; i < 5; ++i)
+    if (check_hip(hipMemcpy(bufs[i].p, hin[i], n * 4, hipMemcpyHostToDevice), name)) goto fail;
+  if (check_hip(hipMemcpy(bufs[8].p, m, r * 4, hipMemcpyHostToDevice), name) ||
+      check_hip(hipMemcpy(bufs[9].p, l, r * 4, hipMemcpyHostToDevice), name))
+    goto fail;
+  if (mt_flash_attn_bwd(MT_F32, causal, bufs[0].p, bufs[1].p, bufs[2].p, bufs[3].p, bufs[4].p,
+                        (const float*)bufs[8].p, (const float*)bufs[9].p, bufs[5].p, bufs[6].p,
+                        bufs[7].p, B, nh, N, d, nullptr, bufs[10].p, nullptr))
+    goto fail;
+  if (check_hip(hipDeviceSynchronize(), name) ||
+      check_hip(hipMemcpy(dQ, bufs[5].p, n * 4, hipMemcpyDeviceToHost), name) ||
+      check_hip(hipMemcpy(dK, bufs[6].p, n * 4, hipMemcpyDeviceToHost), name) ||
+      check_hip(hipMemcpy(dV, bufs[7].p, n * 4, hipMemcpyDeviceToHost), name))
+    goto fail;
+  return 0;
+fail:
+  fprintf(stderr, "%s failed: %s\n", name, g_err);
+  return 1;
+}
+
+void launch_flashattention_forward(float* Q, float* K, float* V, float* O, float* l, float* m,
+                                   int B, int nh, int N, int d) {
+  host_fwd(Q, K, V, O, l, m, B, nh, N, d, 0, "launch_flashattention_forward");
+}
+void launch_flashattention_forward_causal(float* Q, float* K, float* V, float* O, float* l,
+                                          float* m, int B, int nh, int N, int d) {
+  host_fwd(Q, K, V, O, l, m, B, nh, N, d, 1, "launch_flashattention_forward_causal");
+}
+void launch_flashattention_backward(float* Q, float* K, float* V, float* O, float* dQ,
+                                    float* dK, float* dV, float* dO, float* l, float* m, int B,
+                                    int nh, int N, int d) {
+  host_bwd(Q, K, V, O, dQ, dK, dV, dO, l, m, B, nh, N, d, 0, "launch_flashattention_backward");
+}
+void launch_flashattention_backward_causal(float* Q, float* K, float* V, float* O, float* dQ,
+                                           float* dK, float* dV, float* dO, float* l,
+                                           float* m, int B, int nh, int N, int d) {
+  host_bwd(Q, K, V, O, dQ, dK, dV, dO, l, m, B, nh, N, d, 1,
+           "launch_flashattention_backward_causal");
+}
+
+}  // extern "C"

@@ -1,0 +1,360 @@
+// FlashAttention backward, generic tiled kernels (fp32 and bf16, any head dim).
+//
+// Replaces the reference backward_kernel / backward_kernel_causal
+// (src/flashattention_kernel.cu:115-255, :547-690): given Q, K, V, O, dO and the
+// forward's (m, l), produce dQ, dK, dV of O = softmax(QKᵀ/√d) V. The reference's
+// dV term is wrong (:202/:637 use dO row t instead of y) and racy (:241/:676); this
+// computes the exact gradient:
+//     P = exp(s − m)/l,  dV = Pᵀ dO,  dP = dO Vᵀ,  δ = rowsum(dO ∘ O),
+//     dS = P ∘ (dP − δ),  dQ = dS K/√d,  dK = dSᵀ Q/√d.
+//
+// MI355X design, three deterministic launches (no atomics, no HBM read-modify-write):
+//  1. fa_bwd_prep : δ and lse2 = m·log2e + log2(l) per row (one wave per row).
+//  2. fa_bwd_dkv  : "key on the lane" — a workgroup owns 128 keys (32 per wave) and
+//                   sweeps all query tiles; S and dP come out of MFMA with the key on
+//                   the lane, so they are directly the B operands of dVᵀ += dOᵀ·P and
+//                   dKᵀ += Qᵀ·dS (dOᵀ/Qᵀ read with ds_read_b64_tr_b16).
+//  3. fa_bwd_dq   : "query on the lane" — a workgroup owns 128 queries and sweeps the
+//                   key tiles; dQᵀ += Kᵀ·dSᵀ.
+// The dQ pass recomputes S and dP (7 MFMA products instead of 5) in exchange for
+// no cross-workgroup reduction of dQ.
+#include "fa_common.h"
+
+namespace mt {
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void fa_bwd_prep(AttnArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t rows = (int64_t)p.B * p.H * p.N;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int n = (int)(row % p.N);
+  const int64_t bh = row / p.N;
+  const int b = (int)(bh / p.H), hh = (int)(bh % p.H);
+  const T* O = (const T*)p.o + b * p.so[0] + hh * p.so[1] + (int64_t)n * p.so[2];
+  const T* dO = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + (int64_t)n * p.sdo[2];
+  float acc = 0.f;
+  for (int c = lane; c < p.d; c += 64) acc += to_f32(O[c]) * to_f32(dO[c]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) {
+    p.delta[row] = acc;
+    p.lse2[row] = p.m[row] * kLog2e + log2f(p.l[row]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dK, dV: grid (ceil(N/128), B*H, ceil(d/DT)).
+template <typename T, int DT, int QB, bool VEC, bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
+  constexpr int BKV = 128, BQ = 32 * QB;
+  constexpr int PAD = 16 / sizeof(T);
+  constexpr int LD = DT + PAD;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* sK = (T*)smem;
+  T* sV = sK + BKV * LD;
+  T* sQ = sV + BKV * LD;
+  T* sO = sQ + BQ * LD;  // dO tile
+  float* sLse = (float*)(sO + BQ * LD);
+  float* sDel = sLse + BQ;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N, d = p.d;
+  const int k0 = blockIdx.x * BKV;
+  const int bh = blockIdx.y, b = bh / p.H, hh = bh % p.H;
+  const int oc = blockIdx.z * DT;
+  const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const T* dOg = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const float* lse2 = p.lse2 + (int64_t)bh * N;
+  const float* delta = p.delta + (int64_t)bh * N;
+  const int dpad = (d + 15) & ~15;
+  const int nch = (dpad + DT - 1) / DT;
+  const int my_k = k0 + wave * 32 + c32;  // this lane's key
+  const int wave_kmin = k0 + wave * 32;
+
+  f32x16 dK[DT / 32], dV[DT / 32];
+#pragma unroll
+  for (int i = 0; i < DT / 32; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
+
+  if (nch == 1) {
+    stage_tile<T, BKV, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, 0, d);
+    stage_tile<T, BKV, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, 0, d);
+  }
+  const int qstart = CAUSAL ? (k0 / BQ) * BQ : 0;
+  for (int qt = qstart; qt < N; qt += BQ) {
+    const bool active = !(CAUSAL && qt + BQ - 1 < wave_kmin);
+    f32x16 S[QB], dP[QB];
+#pragma unroll
+    for (int i = 0; i < QB; ++i) { S[i] = f32x16{}; dP[i] = f32x16{}; }
+    for (int c = 0; c < nch; ++c) {
+      __syncthreads();
+      if (nch > 1) {
+        stage_tile<T, BKV, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
+        stage_tile<T, BKV, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, c * DT, d);
+      }
+      stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], qt, N, c * DT, d);
+      stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], qt, N, c * DT, d);
+      if (c == 0 && tid < BQ) {
+        const int q = qt + tid;
+        sLse[tid] = q < N ? lse2[q] : 0.f;
+        sDel[tid] = q < N ? delta[q] : 0.f;
+      }
+      __syncthreads();
+      const int ksteps = min(DT, dpad - c * DT) / 16;
+      if (active) {
+        for (int ks = 0; ks < ksteps; ++ks) {
+          const int col = ks * 16 + 8 * hf;
+          Frag<T> bk = row_frag<T>(sK + (wave * 32 + c32) * LD + col);
+          Frag<T> bv = row_frag<T>(sV + (wave * 32 + c32) * LD + col);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) {
+            Frag<T> aq = row_frag<T>(sQ + (qb * 32 + c32) * LD + col);
+            Frag<T> ao = row_frag<T>(sO + (qb * 32 + c32) * LD + col);
+            mma(S[qb], aq, bk);
+            mma(dP[qb], ao, bv);
+          }
+        }
+      }
+    }
+    // Row c32-lane holds S[q][my_k] for q = qt + qb*32 + acc_row(r, hf).
+    if (active) {
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = qb * 32 + acc_row(r, hf);
+          const int q = qt + ql;
+          float pv = exp2f(S[qb][r] * p.scale_log2 - sLse[ql]);
+          if (q >= N || my_k >= N || (CAUSAL && my_k > q)) pv = 0.f;
+          S[qb][r] = pv;
+          dP[qb][r] = pv * (dP[qb][r] - sDel[ql]);
+        }
+    }
+    if (nch > 1 && oc != (nch - 1) * DT) {
+      // The Q/dO tiles hold the last d-chunk; restage the output chunk.
+      __syncthreads();
+      stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], qt, N, oc, d);
+      stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], qt, N, oc, d);
+      __syncthreads();
+    }
+    if (active) {
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          Frag<T> bp = acc_frag<T>(S[qb], s);
+          Frag<T> bs = acc_frag<T>(dP[qb], s);
+#pragma unroll
+          for (int db = 0; db < DT / 32; ++db) {
+            Frag<T> ao = col_frag<T>(sO, LD, qb * 32 + 16 * s + 4 * hf, db * 32, lane);
+            Frag<T> aq = col_frag<T>(sQ, LD, qb * 32 + 16 * s + 4 * hf, db * 32, lane);
+            mma(dV[db], ao, bp);
+            mma(dK[db], aq, bs);
+          }
+        }
+    }
+  }
+
+  if (my_k < N) {
+    T* dKg = (T*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
+    T* dVg = (T*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
+#pragma unroll
+    for (int db = 0; db < DT / 32; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = oc + db * 32 + 8 * g + 4 * hf;
+        const float ak[4] = {dK[db][4 * g] * p.scale, dK[db][4 * g + 1] * p.scale,
+                             dK[db][4 * g + 2] * p.scale, dK[db][4 * g + 3] * p.scale};
+        const float av[4] = {dV[db][4 * g], dV[db][4 * g + 1], dV[db][4 * g + 2], dV[db][4 * g + 3]};
+        if (VEC && col + 3 < d) {
+          store4(dKg + col, ak[0], ak[1], ak[2], ak[3], true);
+          store4(dVg + col, av[0], av[1], av[2], av[3], true);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < d) {
+              dKg[col + e] = from_f32<T>(ak[e]);
+              dVg[col + e] = from_f32<T>(av[e]);
+            }
+        }
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dQ: grid (ceil(N/128), B*H, ceil(d/DT)).
+template <typename T, int DT, int KB, bool VEC, bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
+  constexpr int BQ = 128, BK = 32 * KB;
+  constexpr int PAD = 16 / sizeof(T);
+  constexpr int LD = DT + PAD;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* sQ = (T*)smem;
+  T* sO = sQ + BQ * LD;  // dO
+  T* sK = sO + BQ * LD;
+  T* sV = sK + BK * LD;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N, d = p.d;
+  const int q0 = blockIdx.x * BQ;
+  const int bh = blockIdx.y, b = bh / p.H, hh = bh % p.H;
+  const int oc = blockIdx.z * DT;
+  const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const T* dOg = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int dpad = (d + 15) & ~15;
+  const int nch = (dpad + DT - 1) / DT;
+  const int my_q = q0 + wave * 32 + c32;
+  const int wave_qmax = q0 + wave * 32 + 31;
+  const float lse_q = my_q < N ? p.lse2[(int64_t)bh * N + my_q] : 0.f;
+  const float del_q = my_q < N ? p.delta[(int64_t)bh * N + my_q] : 0.f;
+
+  f32x16 dQ[DT / 32];
+#pragma unroll
+  for (int i = 0; i < DT / 32; ++i) dQ[i] = f32x16{};
+
+  if (nch == 1) {
+    stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, 0, d);
+    stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], q0, N, 0, d);
+  }
+  const int kend = CAUSAL ? min(N, q0 + BQ) : N;
+  for (int k0 = 0; k0 < kend; k0 += BK) {
+    const bool active = !(CAUSAL && k0 > wave_qmax);
+    f32x16 S[KB], dP[KB];
+#pragma unroll
+    for (int i = 0; i < KB; ++i) { S[i] = f32x16{}; dP[i] = f32x16{}; }
+    for (int c = 0; c < nch; ++c) {
+      __syncthreads();
+      if (nch > 1) {
+        stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, c * DT, d);
+        stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], q0, N, c * DT, d);
+      }
+      stage_tile<T, BK, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
+      stage_tile<T, BK, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, c * DT, d);
+      __syncthreads();
+      const int ksteps = min(DT, dpad - c * DT) / 16;
+      if (active) {
+        for (int ks = 0; ks < ksteps; ++ks) {
+          const int col = ks * 16 + 8 * hf;
+          Frag<T> bq = row_frag<T>(sQ + (wave * 32 + c32) * LD + col);
+          Frag<T> bo = row_frag<T>(sO + (wave * 32 + c32) * LD + col);
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            Frag<T> ak = row_frag<T>(sK + (kb * 32 + c32) * LD + col);
+            Frag<T> av = row_frag<T>(sV + (kb * 32 + c32) * LD + col);
+            mma(S[kb], ak, bq);
+            mma(dP[kb], av, bo);
+          }
+        }
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + kb * 32 + acc_row(r, hf);
+          float pv = exp2f(S[kb][r] * p.scale_log2 - lse_q);
+          if (key >= N || (CAUSAL && key > my_q)) pv = 0.f;
+          dP[kb][r] = pv * (dP[kb][r] - del_q);
+        }
+    }
+    if (nch > 1 && oc != (nch - 1) * DT) {
+      __syncthreads();
+      stage_tile<T, BK, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, oc, d);
+      __syncthreads();
+    }
+    if (active) {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          Frag<T> bs = acc_frag<T>(dP[kb], s);
+#pragma unroll
+          for (int db = 0; db < DT / 32; ++db) {
+            Frag<T> ak = col_frag<T>(sK, LD, kb * 32 + 16 * s + 4 * hf, db * 32, lane);
+            mma(dQ[db], ak, bs);
+          }
+        }
+    }
+  }
+
+  if (my_q < N) {
+    T* dQg = (T*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)my_q * p.sdq[2];
+#pragma unroll
+    for (int db = 0; db < DT / 32; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = oc + db * 32 + 8 * g + 4 * hf;
+        const float a[4] = {dQ[db][4 * g] * p.scale, dQ[db][4 * g + 1] * p.scale,
+                            dQ[db][4 * g + 2] * p.scale, dQ[db][4 * g + 3] * p.scale};
+        if (VEC && col + 3 < d) {
+          store4(dQg + col, a[0], a[1], a[2], a[3], true);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < d) dQg[col + e] = from_f32<T>(a[e]);
+        }
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <typename T, int DT, int QB, int KB, bool VEC, bool CAUSAL>
+static hipError_t launch_bwd_t(const AttnArgs& a, hipStream_t st) {
+  constexpr int LD = DT + 16 / sizeof(T);
+  const int nz = (a.d + DT - 1) / DT;
+  const int nblk = (a.N + 127) / 128;
+  {
+    const int64_t rows = (int64_t)a.B * a.H * a.N;
+    hipLaunchKernelGGL(fa_bwd_prep<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  {
+    const size_t smem = sizeof(T) * (size_t)LD * (2 * 128 + 2 * 32 * QB) + 2 * sizeof(float) * 32 * QB;
+    auto kfn = fa_bwd_dkv<T, DT, QB, VEC, CAUSAL>;
+    hipError_t e = hipFuncSetAttribute((const void*)kfn,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kfn, dim3(nblk, a.B * a.H, nz), dim3(256), smem, st, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  {
+    const size_t smem = sizeof(T) * (size_t)LD * (2 * 128 + 2 * 32 * KB);
+    auto kfn = fa_bwd_dq<T, DT, KB, VEC, CAUSAL>;
+    hipError_t e = hipFuncSetAttribute((const void*)kfn,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kfn, dim3(nblk, a.B * a.H, nz), dim3(256), smem, st, a);
+    return hipGetLastError();
+  }
+}
+
+template <typename T, int DT, int QB, int KB>
+static hipError_t dispatch_bwd(const AttnArgs& a, bool vec, bool causal, hipStream_t st) {
+  if (vec)
+    return causal ? launch_bwd_t<T, DT, QB, KB, true, true>(a, st)
+                  : launch_bwd_t<T, DT, QB, KB, true, false>(a, st);
+  return causal ? launch_bwd_t<T, DT, QB, KB, false, true>(a, st)
+                : launch_bwd_t<T, DT, QB, KB, false, false>(a, st);
+}
+
+hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
+                              hipStream_t st) {
+  if (bf16_io) {
+    if (a.d <= 64) return dispatch_bwd<bf16, 64, 2, 2>(a, vec, causal, st);
+    return dispatch_bwd<bf16, 128, 1, 1>(a, vec, causal, st);
+  }
+  // fp32 keeps 64-column chunks: a 128-column fp32 K+V pair would not fit the LDS.
+  return dispatch_bwd<float, 64, 1, 1>(a, vec, causal, st);
+}
+
+}  // namespace mt

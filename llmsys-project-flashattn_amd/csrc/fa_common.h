@@ -1,0 +1,170 @@
+// Shared CDNA4 (gfx950) primitives for the FlashAttention kernels.
+//
+// Every attention product in this library is expressed on one MFMA shape, the
+// 32x32 output tile with a 16-deep k step:
+//   bf16 : one  v_mfma_f32_32x32x16_bf16
+//   fp32 : eight v_mfma_f32_32x32x2_f32  (exact fp32 fma chain, no xf32 on gfx950)
+// In both cases lane l (c = l&31, h = l>>5) supplies 8 elements of row c of A
+// and column c of B, for the k indices {8h .. 8h+7} of the step ("Frag<T>"),
+// and receives the C/D tile with column c on the lane and rows
+//   row(r, h) = (r&3) + 8*(r>>2) + 4*h ,   r = 0..15            (f32x16 "Acc").
+// An accumulator is reused as the B operand of the next product by taking
+// registers 8s..8s+7 as k-step s; element j of lane half h then stands for
+// k = 16s + 8(j>>2) + 4h + (j&3), so the A operand of that product must be
+// gathered with the same k order (col_frag below).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mt {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __bf16 bf16;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+template <typename T> struct FragT;
+template <> struct FragT<bf16> { typedef bf16x8 type; };
+template <> struct FragT<float> { typedef f32x8 type; };
+template <typename T> using Frag = typename FragT<T>::type;
+
+__device__ __forceinline__ void mma(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mma(f32x16& acc, const f32x8& a, const f32x8& b) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// 8 contiguous elements of one LDS row (row fragment). p must be 16-B aligned.
+__device__ __forceinline__ bf16x8 row_frag(const bf16* p, bf16x8*) { return *(const bf16x8*)p; }
+__device__ __forceinline__ f32x8 row_frag(const float* p, f32x8*) {
+  f32x8 r;
+  float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w; r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+  return r;
+}
+template <typename T> __device__ __forceinline__ Frag<T> row_frag(const T* p) {
+  return row_frag(p, (Frag<T>*)nullptr);
+}
+
+// Column ("transposed") fragment of an LDS tile with row stride ld (elements):
+// element j = tile[(k0 + 8(j>>2) + (j&3)) * ld + col], where the caller passes
+// k0 = base + 16s + 4h and col = cbase + (lane&31). bf16 uses the gfx950
+// ds_read_b64_tr_b16 transpose read (two per fragment); EXEC must be full.
+__device__ __forceinline__ bf16x8 col_frag(const bf16* tile, int ld, int k0, int cbase, int lane,
+                                           bf16x8*) {
+  const int i = lane & 15, g = (lane >> 4) & 1;
+  const bf16* a = tile + (k0 + (i >> 2)) * ld + cbase + 16 * g + 4 * (i & 3);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 8 * ld));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+__device__ __forceinline__ f32x8 col_frag(const float* tile, int ld, int k0, int cbase, int lane,
+                                          f32x8*) {
+  const float* a = tile + k0 * ld + cbase + (lane & 31);
+  f32x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = a[(8 * (j >> 2) + (j & 3)) * ld];
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ Frag<T> col_frag(const T* tile, int ld, int k0, int cbase, int lane) {
+  return col_frag(tile, ld, k0, cbase, lane, (Frag<T>*)nullptr);
+}
+
+// Accumulator registers 8s..8s+7 as a B-operand fragment.
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s, bf16x8*) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+__device__ __forceinline__ f32x8 acc_frag(const f32x16& a, int s, f32x8*) {
+  f32x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = a[8 * s + j];
+  return r;
+}
+template <typename T> __device__ __forceinline__ Frag<T> acc_frag(const f32x16& a, int s) {
+  return acc_frag(a, s, (Frag<T>*)nullptr);
+}
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// Store 4 consecutive fp32 accumulator values (one row group) as T.
+__device__ __forceinline__ void store4(float* p, float a, float b, float c, float d, bool vec) {
+  if (vec) {
+    *(float4*)p = make_float4(a, b, c, d);
+  } else {
+    p[0] = a; p[1] = b; p[2] = c; p[3] = d;
+  }
+}
+__device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float d, bool vec) {
+  if (vec) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+    *(bf16x4*)p = v;
+  } else {
+    p[0] = (bf16)a; p[1] = (bf16)b; p[2] = (bf16)c; p[3] = (bf16)d;
+  }
+}
+
+// Cooperative global -> LDS staging of a ROWS x COLS tile (COLS a multiple of
+// 16 B worth of T). Row r of the tile is global row row0 + r (stride gstride
+// elements), columns col0 .. col0+COLS-1; rows >= nrows or columns >= ncols are
+// zero-filled. VEC: every 16-B chunk is either fully inside ncols and aligned
+// (host-checked), so it is moved with one 16-B load.
+template <typename T, int ROWS, int COLS, int NTHREADS, bool VEC>
+__device__ __forceinline__ void stage_tile(T* lds, int ld, const T* g, int64_t gstride, int row0,
+                                           int nrows, int col0, int ncols) {
+  constexpr int EPC = 16 / sizeof(T);          // elements per 16-B chunk
+  constexpr int CPR = COLS / EPC;              // chunks per row
+  constexpr int NCH = ROWS * CPR;
+  for (int c = threadIdx.x; c < NCH; c += NTHREADS) {
+    const int r = c / CPR, cc = (c % CPR) * EPC;
+    const int gr = row0 + r, gc = col0 + cc;
+    T* dst = lds + r * ld + cc;
+    if (VEC) {
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (gr < nrows && gc < ncols) val = *(const uint4*)(g + (int64_t)gr * gstride + gc);
+      *(uint4*)dst = val;
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        T val = from_f32<T>(0.f);
+        if (gr < nrows && gc + e < ncols) val = g[(int64_t)gr * gstride + gc + e];
+        dst[e] = val;
+      }
+    }
+  }
+}
+
+// Parameters shared by the forward / backward launches (all strides in elements;
+// the head dimension d is always unit-stride).
+struct AttnArgs {
+  const void* q; const void* k; const void* v; const void* o; const void* dout;
+  void* out;   // O (fwd)
+  void* dq; void* dk; void* dv;
+  float* m; float* l;              // fwd outputs / bwd inputs, [B*H*N]
+  float* lse2; float* delta;       // bwd workspace, [B*H*N]
+  int64_t sq[3], sk[3], sv[3], so[3], sdo[3], sdq[3], sdk[3], sdv[3];  // (b, h, n)
+  int B, H, N, d;
+  float scale;       // 1/sqrt(d)
+  float scale_log2;  // log2(e)/sqrt(d)
+};
+
+}  // namespace mt

@@ -1,0 +1,196 @@
+// FlashAttention forward, generic tiled kernel (fp32 and bf16, any head dim).
+//
+// Replaces the reference forward_kernel / forward_kernel_causal
+// (src/flashattention_kernel.cu:9-112, :438-545). Same contract: O = softmax(QKᵀ/√d) V
+// per (b, h) slice, plus the row statistics m (max of the scaled logits) and
+// l = Σ exp(s − m), so that P = exp(s − m)/l (:194). Causal masks key > query.
+//
+// MI355X design (not the reference's FA-1 loop order):
+//  * Q-tile outer loop; a 256-thread workgroup (4 waves) owns BQ = 128 queries,
+//    32 per wave, and streams K/V tiles of BK keys through LDS.
+//  * "Query on the lane": Sᵀ = K·Qᵀ on MFMA puts one query per lane column, so the
+//    online softmax (row max / row sum / rescale) is lane-local except for one
+//    cross-half shuffle, and Sᵀ feeds Oᵀ = Vᵀ·Pᵀ directly as the MFMA B operand
+//    (no LDS round trip for P). V is read transposed with ds_read_b64_tr_b16.
+//  * exp2 with log2(e)/√d folded into one scale; m, l kept in registers; O written
+//    once (the reference read-modify-writes O in HBM for every K tile, :92-104).
+//  * Head dims above the tile DT are handled by a d-chunked QKᵀ and a grid.z split
+//    of the O columns (each z-slice recomputes S; exact, only slower).
+//  * int64 addressing throughout (the reference overflows at 2^31 elements).
+#include "fa_common.h"
+
+namespace mt {
+
+template <typename T, int DT, int KB, bool VEC, bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_fwd_generic(AttnArgs p) {
+  constexpr int BQ = 128, BK = 32 * KB;
+  constexpr int PAD = 16 / sizeof(T);
+  constexpr int LD = DT + PAD;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* sQ = (T*)smem;
+  T* sK = sQ + BQ * LD;
+  T* sV = sK + BK * LD;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N, d = p.d;
+  const int q0 = blockIdx.x * BQ;
+  const int bh = blockIdx.y, b = bh / p.H, hh = bh % p.H;
+  const int oc = blockIdx.z * DT;  // first output column of this slice
+  const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const int dpad = (d + 15) & ~15;
+  const int nch = (dpad + DT - 1) / DT;
+  const int my_q = q0 + wave * 32 + c32;
+  const int wave_qmax = q0 + wave * 32 + 31;
+
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x16 O[DT / 32];
+#pragma unroll
+  for (int i = 0; i < DT / 32; ++i) O[i] = f32x16{};
+
+  const int kend = CAUSAL ? min(N, q0 + BQ) : N;
+  const int ntiles = (kend + BK - 1) / BK;
+
+  if (nch == 1) stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, 0, d);
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * BK;
+    const bool active = !(CAUSAL && k0 > wave_qmax);
+    f32x16 S[KB];
+#pragma unroll
+    for (int i = 0; i < KB; ++i) S[i] = f32x16{};
+    for (int c = 0; c < nch; ++c) {
+      __syncthreads();
+      if (nch > 1) stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, c * DT, d);
+      stage_tile<T, BK, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
+      __syncthreads();
+      const int ksteps = min(DT, dpad - c * DT) / 16;
+      if (active) {
+        for (int ks = 0; ks < ksteps; ++ks) {
+          Frag<T> bq = row_frag<T>(sQ + (wave * 32 + c32) * LD + ks * 16 + 8 * hf);
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            Frag<T> ak = row_frag<T>(sK + (kb * 32 + c32) * LD + ks * 16 + 8 * hf);
+            mma(S[kb], ak, bq);
+          }
+        }
+      }
+    }
+    // V rows k0.., output columns oc..oc+DT (sV is not read by the QKᵀ phase).
+    stage_tile<T, BK, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, oc, d);
+
+    if (active) {
+      // Online softmax in the log2 domain; lane (c32, hf) holds 16*KB keys of query my_q.
+      float smax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + kb * 32 + acc_row(r, hf);
+          float x = S[kb][r] * p.scale_log2;
+          if (key >= N || (CAUSAL && key > my_q)) x = -INFINITY;
+          S[kb][r] = x;
+          smax = fmaxf(smax, x);
+        }
+      smax = fmaxf(smax, __shfl_xor(smax, 32));
+      const float m_new = fmaxf(m_run, smax);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run - m_use);
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = exp2f(S[kb][r] - m_use);
+          S[kb][r] = e;
+          rs += e;
+        }
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < DT / 32; ++i) O[i] *= alpha;
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          Frag<T> bp = acc_frag<T>(S[kb], s);
+#pragma unroll
+          for (int db = 0; db < DT / 32; ++db) {
+            Frag<T> av = col_frag<T>(sV, LD, kb * 32 + 16 * s + 4 * hf, db * 32, lane);
+            mma(O[db], av, bp);
+          }
+        }
+    }
+  }
+
+  // Epilogue: combine the two lane halves' partial row sums, normalise, store.
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  const float inv_l = 1.f / l_tot;
+  if (my_q < N) {
+    T* Og = (T*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+#pragma unroll
+    for (int db = 0; db < DT / 32; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = oc + db * 32 + 8 * g + 4 * hf;
+        const float a[4] = {O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
+                            O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l};
+        if (VEC && col + 3 < d) {
+          store4(Og + col, a[0], a[1], a[2], a[3], true);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < d) Og[col + e] = from_f32<T>(a[e]);
+        }
+      }
+    if (blockIdx.z == 0 && hf == 0) {
+      const int64_t row = (int64_t)bh * N + my_q;
+      if (p.m) p.m[row] = m_run * kLn2;
+      if (p.l) p.l[row] = l_tot;
+    }
+  }
+}
+
+template <typename T, int DT, int KB>
+static size_t fwd_generic_smem() {
+  constexpr int LD = DT + 16 / sizeof(T);
+  return sizeof(T) * (size_t)LD * (128 + 2 * 32 * KB);
+}
+
+template <typename T, int DT, int KB, bool VEC, bool CAUSAL>
+static hipError_t launch_fwd_generic_t(const AttnArgs& a, hipStream_t st) {
+  const size_t smem = fwd_generic_smem<T, DT, KB>();
+  auto kfn = fa_fwd_generic<T, DT, KB, VEC, CAUSAL>;
+  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)smem);
+  if (e != hipSuccess) return e;
+  dim3 grid((a.N + 127) / 128, a.B * a.H, (a.d + DT - 1) / DT);
+  hipLaunchKernelGGL(kfn, grid, dim3(256), smem, st, a);
+  return hipGetLastError();
+}
+
+template <typename T, int DT, int KB>
+static hipError_t dispatch_fwd_generic(const AttnArgs& a, bool vec, bool causal, hipStream_t st) {
+  if (vec)
+    return causal ? launch_fwd_generic_t<T, DT, KB, true, true>(a, st)
+                  : launch_fwd_generic_t<T, DT, KB, true, false>(a, st);
+  return causal ? launch_fwd_generic_t<T, DT, KB, false, true>(a, st)
+                : launch_fwd_generic_t<T, DT, KB, false, false>(a, st);
+}
+
+hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
+                              hipStream_t st) {
+  if (bf16_io) {
+    if (a.d <= 64) return dispatch_fwd_generic<bf16, 64, 2>(a, vec, causal, st);
+    return dispatch_fwd_generic<bf16, 128, 2>(a, vec, causal, st);
+  }
+  if (a.d <= 64) return dispatch_fwd_generic<float, 64, 2>(a, vec, causal, st);
+  return dispatch_fwd_generic<float, 128, 1>(a, vec, causal, st);
+}
+
+}  // namespace mt

@@ -1,0 +1,167 @@
+"""ctypes binding of ``libminitorch_hip.so`` (C ABI declared in ``include/minitorch_hip.h``).
+
+This is the MI355X counterpart of the reference's ctypes loading block
+(reference ``minitorch/cuda_kernel_ops.py:25-29``): one library, located next to
+this file rather than relative to the CWD, with every ``argtypes`` declared once.
+There is no fallback: if the library is missing the first call raises.
+
+Device buffers are torch tensors (PyTorch-ROCm is used for memory, streams and
+``torch.distributed`` only); every computation goes through the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libminitorch_hip.so")
+
+MT_F32 = 0
+MT_BF16 = 1
+
+_lib = None
+
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_vp = ctypes.c_void_p
+_fp = ctypes.POINTER(ctypes.c_float)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+
+# name -> (restype, argtypes); mirrors include/minitorch_hip.h
+_PROTOS = {
+    "mt_last_error": (ctypes.c_char_p, []),
+    "mt_abi_version": (_int, []),
+    "mt_flash_set_kernel_policy": (None, [_int]),
+    "mt_flash_attn_fwd": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,
+                                 _i64p, _i64p, _i64p, _i64p, _vp]),
+    "mt_flash_attn_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
+    "mt_flash_attn_bwd": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                 _i64, _i64, _i64, _i64, _i64p, _vp, _vp]),
+    "launch_flashattention_forward": (None, [_fp] * 6 + [_int] * 4),
+    "launch_flashattention_backward": (None, [_fp] * 10 + [_int] * 4),
+    "launch_flashattention_forward_causal": (None, [_fp] * 6 + [_int] * 4),
+    "launch_flashattention_backward_causal": (None, [_fp] * 10 + [_int] * 4),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `make -C {os.path.dirname(_HERE)}` "
+                "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def register(name: str, restype, argtypes) -> None:
+    """Declare an additional export (used by the companion-kernel modules)."""
+    _PROTOS[name] = (restype, argtypes)
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = lib().mt_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed: {msg}")
+
+
+# ---- torch plumbing -------------------------------------------------------------
+def _torch():
+    import torch
+    return torch
+
+
+def stream_ptr(device=None) -> int:
+    torch = _torch()
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(t) -> int:
+    torch = _torch()
+    if t.dtype == torch.float32:
+        return MT_F32
+    if t.dtype == torch.bfloat16:
+        return MT_BF16
+    raise TypeError(f"unsupported dtype {t.dtype} (float32 or bfloat16)")
+
+
+def strides3(t) -> ctypes.Array:
+    """(batch, head, seq) element strides of a [B, H, N, d] tensor with unit-stride d."""
+    if t.dim() != 4:
+        raise ValueError(f"expected a 4-D [B,H,N,d] tensor, got shape {tuple(t.shape)}")
+    if t.stride(3) != 1 and t.shape[3] != 1:
+        raise ValueError("the head dimension must be unit-stride")
+    return (ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(2))
+
+
+def _check_dev(*ts) -> None:
+    for t in ts:
+        if not t.is_cuda:
+            raise ValueError("HIP flash attention needs device (cuda) tensors")
+
+
+def flash_fwd(q, k, v, causal: bool = False, out=None, m=None, l=None, stream: Optional[int] = None):
+    """Device-pointer forward on torch tensors [B,H,N,d] (fp32 or bf16, any strides
+    with unit-stride d). Returns (O, m, l); O has q's dtype, m/l are fp32 [B,H,N]."""
+    torch = _torch()
+    _check_dev(q, k, v)
+    B, H, N, d = q.shape
+    if k.shape != q.shape or v.shape != q.shape:
+        raise ValueError(f"q/k/v shapes differ: {tuple(q.shape)} {tuple(k.shape)} {tuple(v.shape)}")
+    if not (q.dtype == k.dtype == v.dtype):
+        raise TypeError("q/k/v dtypes differ")
+    if out is None:
+        out = torch.empty_like(q, memory_format=torch.contiguous_format)
+    if m is None:
+        m = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
+    if l is None:
+        l = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
+    st = stream_ptr(q.device) if stream is None else stream
+    check(lib().mt_flash_attn_fwd(dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(), v.data_ptr(),
+                                  out.data_ptr(), m.data_ptr(), l.data_ptr(), B, H, N, d,
+                                  strides3(q), strides3(k), strides3(v), strides3(out), st),
+          "mt_flash_attn_fwd")
+    return out, m, l
+
+
+def flash_bwd(q, k, v, o, do, m, l, causal: bool = False, dq=None, dk=None, dv=None,
+              workspace=None, stream: Optional[int] = None):
+    """Device-pointer backward. Returns (dQ, dK, dV) in q's dtype."""
+    torch = _torch()
+    _check_dev(q, k, v, o, do, m, l)
+    B, H, N, d = q.shape
+    dq = torch.empty_like(q, memory_format=torch.contiguous_format) if dq is None else dq
+    dk = torch.empty_like(k, memory_format=torch.contiguous_format) if dk is None else dk
+    dv = torch.empty_like(v, memory_format=torch.contiguous_format) if dv is None else dv
+    if workspace is None:
+        nbytes = lib().mt_flash_attn_bwd_workspace_bytes(B, H, N, d)
+        workspace = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
+    m = m.contiguous().float()
+    l = l.contiguous().float()
+    strides = (ctypes.c_int64 * 24)()
+    for i, t in enumerate((q, k, v, o, do, dq, dk, dv)):
+        s = strides3(t)
+        strides[3 * i:3 * i + 3] = list(s)
+    st = stream_ptr(q.device) if stream is None else stream
+    check(lib().mt_flash_attn_bwd(dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(), v.data_ptr(),
+                                  o.data_ptr(), do.data_ptr(), m.data_ptr(), l.data_ptr(),
+                                  dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, N, d,
+                                  strides, workspace.data_ptr(), st),
+          "mt_flash_attn_bwd")
+    return dq, dk, dv
+
+
+def exported_symbols() -> Sequence[str]:
+    return tuple(_PROTOS)

@@ -1,0 +1,146 @@
+/*
+ * CPU ORACLE (C restatement) -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Used by tests/ (large-size parity checks) and by bench.py's cpu_baseline leg.
+ * The shipped HIP path never links or calls this file.
+ *
+ * Restates the reference's CPU ("fast_ops") attention, unfused and in the
+ * reference's op order:
+ *   S   = fp32( sum_k fp64(q_ik * k_jk) )            fast_ops.py:291-350 (fp64 acc, :339-345)
+ *   S   = fp32( S * inv(sqrt(d)) )                     tensor.py:169-170  (Mul(Inv))
+ *   S  += causal ? -FLT_MAX (j > i) : 0                modules_transfomer.py:63-71
+ *   mx  = max_j S;  e_j = fp32(exp(S_j - mx))          nn.py:120 (Max, Exp)
+ *   sum = fp32 sum_j e_j;  P_j = e_j * fp32(1/sum)     nn.py:121-122 (Sum, Inv, Mul)
+ *   O   = fp32( sum_j fp64(P_j * v_jk) )
+ * m = mx and l = sum are returned with the reference flash contract's meaning
+ * (P = exp(S - m) / l, src/flashattention_kernel.cu:194).
+ *
+ * One N-float score row per (bh, i), OpenMP over (bh, i) like numba's prange.
+ * The backward is the exact gradient, fp64 accumulation, one N x N fp32 P slice
+ * per (bh) and thread; OpenMP over bh.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static void score_row(const float* q, const float* k, int64_t N, int64_t d, int64_t i,
+                      int causal, float inv_sqrt_d, float* s) {
+  for (int64_t j = 0; j < N; ++j) {
+    double acc = 0.0;
+    const float* kj = k + j * d;
+    for (int64_t t = 0; t < d; ++t) acc += (double)(q[t] * kj[t]);
+    float v = (float)acc;
+    v = v * inv_sqrt_d;
+    if (causal && j > i) v = v + (-FLT_MAX);
+    s[j] = v;
+  }
+}
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+/* q,k,v,o: [BH, N, d] contiguous fp32; m,l: [BH, N] (may be NULL). */
+void oracle_attn_fwd(const float* q, const float* k, const float* v, float* o, float* m,
+                     float* l, int64_t BH, int64_t N, int64_t d, int causal, int nthreads) {
+  const float inv_sqrt_d = (float)(1.0 / (double)(float)sqrt((double)d));
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel
+  {
+    float* s = (float*)malloc(sizeof(float) * (size_t)N);
+    double* acc = (double*)malloc(sizeof(double) * (size_t)d);
+#pragma omp for schedule(static) collapse(2)
+    for (int64_t bh = 0; bh < BH; ++bh) {
+      for (int64_t i = 0; i < N; ++i) {
+        const int64_t base = bh * N * d;
+        score_row(q + base + i * d, k + base, N, d, i, causal, inv_sqrt_d, s);
+        float mx = -INFINITY;
+        for (int64_t j = 0; j < N; ++j) mx = s[j] > mx ? s[j] : mx;
+        float sum = 0.0f;
+        for (int64_t j = 0; j < N; ++j) {
+          s[j] = (float)exp((double)(s[j] - mx));
+          sum += s[j];
+        }
+        const float inv = (float)(1.0 / (double)sum);
+        for (int64_t t = 0; t < d; ++t) acc[t] = 0.0;
+        for (int64_t j = 0; j < N; ++j) {
+          const float p = s[j] * inv;
+          const float* vj = v + base + j * d;
+          for (int64_t t = 0; t < d; ++t) acc[t] += (double)(p * vj[t]);
+        }
+        float* oi = o + base + i * d;
+        for (int64_t t = 0; t < d; ++t) oi[t] = (float)acc[t];
+        if (m) m[bh * N + i] = mx;
+        if (l) l[bh * N + i] = sum;
+      }
+    }
+    free(s);
+    free(acc);
+  }
+}
+
+/* Exact gradients. dq, dk, dv: [BH, N, d] outputs (overwritten). */
+void oracle_attn_bwd(const float* q, const float* k, const float* v, const float* dout,
+                     const float* m, const float* l, float* dq, float* dk, float* dv,
+                     int64_t BH, int64_t N, int64_t d, int causal, int nthreads) {
+  const float inv_sqrt_d = (float)(1.0 / (double)(float)sqrt((double)d));
+  const double scale = 1.0 / sqrt((double)d);
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel
+  {
+    double* p = (double*)malloc(sizeof(double) * (size_t)(N * N));
+    double* ds = (double*)malloc(sizeof(double) * (size_t)(N * N));
+    float* s = (float*)malloc(sizeof(float) * (size_t)N);
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t bh = 0; bh < BH; ++bh) {
+      const int64_t base = bh * N * d;
+      const float *Q = q + base, *K = k + base, *V = v + base, *dO = dout + base;
+      for (int64_t i = 0; i < N; ++i) {
+        score_row(Q + i * d, K, N, d, i, causal, inv_sqrt_d, s);
+        const double mi = m[bh * N + i], li = l[bh * N + i];
+        double delta = 0.0;
+        for (int64_t j = 0; j < N; ++j) {
+          const double pij = exp((double)s[j] - mi) / li;
+          double dp = 0.0;
+          for (int64_t t = 0; t < d; ++t) dp += (double)dO[i * d + t] * (double)V[j * d + t];
+          p[i * N + j] = pij;
+          ds[i * N + j] = dp;
+          delta += dp * pij;
+        }
+        for (int64_t j = 0; j < N; ++j) ds[i * N + j] = p[i * N + j] * (ds[i * N + j] - delta);
+      }
+      for (int64_t i = 0; i < N; ++i)
+        for (int64_t t = 0; t < d; ++t) {
+          double a = 0.0;
+          for (int64_t j = 0; j < N; ++j) a += ds[i * N + j] * (double)K[j * d + t];
+          dq[base + i * d + t] = (float)(a * scale);
+        }
+      for (int64_t j = 0; j < N; ++j)
+        for (int64_t t = 0; t < d; ++t) {
+          double a = 0.0, b = 0.0;
+          for (int64_t i = 0; i < N; ++i) {
+            a += ds[i * N + j] * (double)Q[i * d + t];
+            b += p[i * N + j] * (double)dO[i * d + t];
+          }
+          dk[base + j * d + t] = (float)(a * scale);
+          dv[base + j * d + t] = (float)b;
+        }
+    }
+    free(p);
+    free(ds);
+    free(s);
+  }
+}
