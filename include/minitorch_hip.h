@@ -36,8 +36,9 @@ enum { MT_F32 = 0, MT_BF16 = 1 };
 /* ---- status ------------------------------------------------------------- */
 const char* mt_last_error(void);
 int mt_abi_version(void);
-/* 0 (default): use the bf16 MFMA kernel specialised for d in {64, 128} when the
- * layout allows it; 1: always use the generic tiled kernels (A/B testing). */
+/* Forward kernel selection (A/B testing). 0 (default): the bf16 MFMA kernel specialised
+ * for d in {64, 128} when the layout allows it, else the generic kernel; 1: always the
+ * generic tiled kernels; 2, 4, 5, 6: alternative bf16 schedules (see fa_fwd_fast.hip). */
 void mt_flash_set_kernel_policy(int policy);
 
 /* ---- FlashAttention, device pointers ------------------------------------- */

@@ -14,12 +14,14 @@
 namespace mt {
 hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
-hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, hipStream_t st, bool* handled);
+hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStream_t st,
+                           bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
 
 static thread_local char g_err[512] = "";
-static int g_kernel_policy = 0;  // 0: auto (fast bf16 kernel when eligible), 1: generic only
+static int g_kernel_policy = 0;  // 0: default bf16 MFMA kernel, 1: generic kernels only,
+                                 // other values: A/B variants (fa_fwd_fast.hip)
 
 int set_error(const char* fmt, ...) {
   va_list ap;
@@ -95,9 +97,9 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
   const int es = dtype == MT_BF16 ? 2 : 4;
   const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so}, {q, k, v, o});
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MT_BF16 && vec && g_kernel_policy == 0) {
+  if (dtype == MT_BF16 && vec && g_kernel_policy != 1) {
     bool handled = false;
-    hipError_t e = launch_fwd_fast(a, causal != 0, st, &handled);
+    hipError_t e = launch_fwd_fast(a, causal != 0, g_kernel_policy, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");
   }
   return check_hip(launch_fwd_generic(a, dtype == MT_BF16, vec, causal != 0, st),

@@ -1,0 +1,25 @@
+"""Interleaved in-process A/B timing of forward-kernel policies (diagnostics)."""
+import os, sys, json
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "llmsys-project-flashattn_amd"))
+import torch
+from minitorch import _hip
+pols = [int(x) for x in sys.argv[1].split(",")]
+causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
+B, H, N, d = 8, 16, 4096, 64
+g = torch.Generator(device="cuda").manual_seed(0)
+q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
+o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
+res = {p: [] for p in pols}
+flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
+for rnd in range(5):
+    for p in pols:
+        _hip.lib().mt_flash_set_kernel_policy(p)
+        for _ in range(3): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(); e0.record()
+        for _ in range(10): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
+        e1.record(); torch.cuda.synchronize()
+        res[p].append(e0.elapsed_time(e1) / 10)
+for p in pols:
+    t = sorted(res[p]); med = t[len(t) // 2]
+    print(f"policy {p:3d}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s")

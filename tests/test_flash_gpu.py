@@ -26,6 +26,19 @@ def torch_dev():
     return torch
 
 
+def _check_ml(m, l, m_ref, l_ref, exact):
+    """(m, l) contract: P = exp(s - m)/l, i.e. m + ln(l) is the row log-sum-exp. The
+    generic kernels return the true row max; the bf16 MFMA kernels may return a max
+    that lags by up to 8·ln2 (deferred rescale), which the contract allows."""
+    lse, lse_ref = m + np.log(l), m_ref + np.log(l_ref)
+    np.testing.assert_allclose(lse, lse_ref, atol=2e-3 if not exact else 1e-5, rtol=1e-5)
+    if exact:
+        np.testing.assert_allclose(m, m_ref, atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(l, l_ref, rtol=1e-5)
+    else:
+        assert np.all(m <= m_ref + 1e-3) and np.all(m >= m_ref - 8 * np.log(2) - 1e-3)
+
+
 def _dev(torch, a, dtype=None):
     dtype = dtype or torch.float32
     return torch.from_numpy(np.ascontiguousarray(a)).to("cuda").to(dtype)
@@ -92,8 +105,7 @@ def test_random_fwd_bwd(torch_dev, B, H, N, d, causal, dtype):
     else:  # bf16 I/O: outputs rounded to 8 significant bits, P rounded before PV
         atol = {"o": 2e-2, "g": 6e-2}
     np.testing.assert_allclose(_np(o), o_ref, atol=atol["o"], rtol=0)
-    np.testing.assert_allclose(_np(m), m_ref, atol=1e-4, rtol=1e-5)
-    np.testing.assert_allclose(_np(l), l_ref, rtol=1e-3)
+    _check_ml(_np(m), _np(l), m_ref, l_ref, exact=(dtype == "fp32"))
     scale = max(1.0, float(np.abs(dq_ref).max()), float(np.abs(dk_ref).max()), float(np.abs(dv_ref).max()))
     for got, ref, name in ((dq, dq_ref, "dq"), (dk, dk_ref, "dk"), (dv, dv_ref, "dv")):
         np.testing.assert_allclose(_np(got), ref, atol=atol["g"] * scale, rtol=0, err_msg=name)
@@ -144,18 +156,22 @@ def test_host_pointer_abi():
             np.testing.assert_allclose(got, ref, atol=2e-5)
 
 
-def _subset_check_fwd(torch, q, k, v, o, causal, heads, atol, rtol=0.0):
+def _subset_check_fwd(torch, q, k, v, o, causal, heads, atol, pv_rel=0.0):
     """Exact check of a subset of (b,h) slices at full N against the C oracle:
-    |O - O_ref| <= atol + rtol * |O_ref| elementwise."""
+    |O - O_ref| <= atol + pv_rel * (P|V|) elementwise, where P|V| = softmax(QKᵀ/√d)|V|
+    bounds what rounding P to bf16 (relative 2^-9 per element) can move O."""
     B, H, N, d = q.shape
     for (b, h) in heads:
         qs, ks, vs = (_np(t[b, h]) for t in (q, k, v))
         o_ref, _, _ = cref.attn_fwd(qs[None], ks[None], vs[None], causal)
         err = np.abs(_np(o[b, h]) - o_ref[0])
-        bound = atol + rtol * np.abs(o_ref[0])
+        bound = atol
+        if pv_rel:
+            pabs, _, _ = cref.attn_fwd(qs[None], ks[None], np.abs(vs)[None], causal)
+            bound = atol + pv_rel * pabs[0]
         worst = float((err - bound).max())
         assert worst <= 0, (f"(b,h)=({b},{h}) max-abs {float(err.max()):.3e} exceeds "
-                            f"{atol} + {rtol}*|ref|")
+                            f"{atol} + {pv_rel}*P|V|")
 
 
 def test_config2_fp32_full_size(torch_dev):
@@ -174,7 +190,8 @@ def test_config3_bf16_full_size(torch_dev, causal):
     """BASELINE config 3: (8,16,4096,64) bf16 fwd + bwd vs the CPU reference fed the
     same bf16 inputs. Non-causal: ≤1e-3 max-abs on O (the north_star bound). Causal:
     the first rows average only a few V rows, so |O| reaches ~2.5 and the bf16 output's
-    own half-ulp (2^-9 relative) exceeds 1e-3 there -> bound 1e-3 + 2^-7·|O_ref|.
+    rounding of P to bf16 (2^-9 relative per weight) moves O by up to 2^-9·(P|V|), which
+    exceeds 1e-3 there -> bound 1e-3 + 2^-8·(P|V|) elementwise.
     Gradients on 2 slices at 2% of their max magnitude."""
     from minitorch import _hip
     torch = torch_dev
@@ -186,7 +203,7 @@ def test_config3_bf16_full_size(torch_dev, causal):
     torch.cuda.synchronize()
     assert torch.isfinite(o.float()).all()
     _subset_check_fwd(torch, q, k, v, o, causal, [(0, 0), (5, 9)], 1e-3,
-                      2.0 ** -7 if causal else 0.0)
+                      2.0 ** -8 if causal else 0.0)
     for (b, h) in [(0, 1), (7, 15)]:
         qs, ks, vs, dos = (_np(t[b, h])[None] for t in (q, k, v, do))
         o_ref, m_ref, l_ref = cref.attn_fwd(qs, ks, vs, causal)
@@ -211,3 +228,49 @@ def test_deterministic(torch_dev):
     torch.cuda.synchronize()
     for a, b in zip(r1 + g1, r2 + g2):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [64, 128])
+def test_kernel_variants_agree(torch_dev, causal, d):
+    """The ping-pong bf16 kernel (default), the single-phase bf16 kernel and the generic
+    tiled kernel compute the same attention (A/B switch mt_flash_set_kernel_policy)."""
+    from minitorch import _hip
+    torch = torch_dev
+    g = torch.Generator(device="cuda").manual_seed(11)
+    q, k, v = (torch.randn((2, 3, 1000, d), device="cuda", generator=g).to(torch.bfloat16)
+               for _ in range(3))
+    outs = []
+    try:
+        for pol in (0, 2, 4, 5, 6, 1):
+            _hip.lib().mt_flash_set_kernel_policy(pol)
+            o, m, l = _hip.flash_fwd(q, k, v, causal)
+            torch.cuda.synchronize()
+            outs.append((o.float(), (m + torch.log(l))))
+    finally:
+        _hip.lib().mt_flash_set_kernel_policy(0)
+    for o, lse in outs[1:]:
+        assert float((o - outs[0][0]).abs().max()) < 2e-2
+        assert float((lse - outs[0][1]).abs().max()) < 2e-3
+
+
+def test_spiked_rescale(torch_dev):
+    """Force the deferred-rescale branch (rule: a rare data-dependent branch needs its own
+    test): one key row aligned with one query row makes that row's max jump past the
+    2^8 threshold at a chosen tile, after several tiles at a low max."""
+    from minitorch import _hip
+    torch = torch_dev
+    B, H, N, d = 1, 2, 700, 64
+    rng = np.random.default_rng(21)
+    q = rng.standard_normal((B, H, N, d)).astype(np.float32) * 0.3
+    k = rng.standard_normal((B, H, N, d)).astype(np.float32) * 0.3
+    v = rng.standard_normal((B, H, N, d)).astype(np.float32)
+    for row, key in ((5, 600), (300, 130), (699, 450)):
+        k[:, :, key] = q[:, :, row] * 12.0
+    q, k, v = (A.bf16_round(x) for x in (q, k, v))
+    for causal in (False, True):
+        o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
+        o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), causal)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(_np(o), o_ref, atol=2e-2)
+        _check_ml(_np(m), _np(l), m_ref, l_ref, exact=False)
