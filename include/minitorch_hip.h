@@ -76,6 +76,82 @@ void launch_flashattention_backward_causal(float* Q, float* K, float* V, float* 
                                            float* dK, float* dV, float* dO, float* l,
                                            float* m, int B, int nh, int N, int d);
 
+
+/* ---- companion kernels, device pointers (fp32) ---------------------------- */
+/* Row softmax over [B, nh, from, to]: out = exp(x + mask - max) / (sum + 1e-8); out may
+ * alias inp. mask: NULL or any tensor broadcastable to [B, nh, from, to] given by 4
+ * element strides (b, h, row, col; 0 = broadcast). mask_future masks col > row.
+ * (reference src/softmax_kernel.cu:35-224) */
+int mt_attn_softmax_fw(float* out, const float* inp, const float* mask, int64_t B, int64_t nh,
+                       int64_t from_len, int64_t to_len, const int64_t* mask_strides,
+                       int mask_future, void* stream);
+/* dinp = soft * (dout - rowsum(dout * soft)); dinp may alias dout. (:308-341) */
+int mt_attn_softmax_bw(float* dinp, const float* dout, const float* soft, int64_t rows,
+                       int64_t softmax_len, void* stream);
+/* LayerNorm over the last dim of [rows, hidden]; var is stored with +1e-8.
+ * (reference src/layernorm_kernel.cu:36-98) */
+int mt_layernorm_fw(float* ln_res, float* var, float* mean, const float* inp, const float* gamma,
+                    const float* beta, int64_t rows, int64_t hidden, void* stream);
+int64_t mt_layernorm_bw_workspace_bytes(int64_t rows, int64_t hidden);
+/* (reference src/layernorm_kernel.cu:192-368) */
+int mt_layernorm_bw(float* gamma_grad, float* beta_grad, float* inp_grad, const float* out_grad,
+                    const float* inp, const float* gamma, const float* beta, const float* var,
+                    const float* mean, int64_t rows, int64_t hidden, void* workspace,
+                    void* stream);
+
+/* ---- generic strided tensor ops, device pointers (fp32) ------------------- */
+/* fn ids as the reference's combine.cu:12-29 (1 add, 2 mul, 3 id, 4 neg, 5 lt, 6 eq,
+ * 7 sigmoid, 8 relu, 9 relu_back, 10 log, 11 log_back, 12 exp, 13 inv, 14 inv_back,
+ * 15 is_close, 16 max, 17 pow, 18 tanh). Shapes broadcast right-aligned; rank <= 8. */
+int mt_tensor_map(int fn, float* out, const int64_t* out_shape, const int64_t* out_strides,
+                  int out_dims, const float* in, const int64_t* in_shape,
+                  const int64_t* in_strides, int in_dims, void* stream);
+int mt_tensor_zip(int fn, float* out, const int64_t* out_shape, const int64_t* out_strides,
+                  int out_dims, const float* a, const int64_t* a_shape, const int64_t* a_strides,
+                  int a_dims, const float* b, const int64_t* b_shape, const int64_t* b_strides,
+                  int b_dims, void* stream);
+/* out has a's shape with shape[reduce_dim] = 1; out = fn(start, fn-fold of the axis). */
+int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t* out_strides,
+                     const float* a, const int64_t* a_shape, const int64_t* a_strides, int dims,
+                     int reduce_dim, float start, void* stream);
+/* c[b] = a[b] @ b[b]; strides are (batch, row, col) triples, batch stride 0 broadcasts. */
+int mt_matmul_f32(float* c, const float* a, const float* b, int64_t batch, int64_t M, int64_t N,
+                  int64_t K, const int64_t* a_strides, const int64_t* b_strides,
+                  const int64_t* c_strides, void* stream);
+
+/* ---- reference-compatible host-pointer wrappers (companion + combine) ----- */
+/* reference src/softmax_kernel.cu:233 (stream: hipStream_t) */
+void launch_attn_softmax(float* inp, const float* attn_mask, int batch_size, int nhead,
+                         int from_len, int to_len, bool mask_future, void* stream);
+/* reference src/softmax_kernel.cu:345 */
+void launch_attn_softmax_bw(float* out_grad, const float* soft_inp, int rows, int softmax_len,
+                            void* stream);
+/* reference src/layernorm_kernel.cu:101 */
+void launch_layernorm(float* ln_res, float* vars, float* means, const float* inp,
+                      const float* scale, const float* bias, int batch_size, int hidden_dim,
+                      void* stream);
+/* reference src/layernorm_kernel.cu:370 */
+void launch_layernorm_bw(float* gamma_grad, float* betta_grad, float* inp_grad,
+                         const float* out_grad, const float* inp, const float* gamma,
+                         const float* betta, const float* vars, const float* means,
+                         int batch_size, int hidden_dim, void* stream_1, void* stream_2);
+/* reference src/combine.cu:385 */
+void tensorMap(float* out, int* out_shape, int* out_strides, int out_size, float* in_storage,
+               int* in_shape, int* in_strides, int in_size, int shape_size, int fn_id);
+/* reference src/combine.cu:443 */
+void tensorZip(float* out, int* out_shape, int* out_strides, int out_size, int out_shape_size,
+               float* a_storage, int* a_shape, int* a_strides, int a_size, int a_shape_size,
+               float* b_storage, int* b_shape, int* b_strides, int b_size, int b_shape_size,
+               int fn_id);
+/* reference src/combine.cu:523 */
+void tensorReduce(float* out, int* out_shape, int* out_strides, int out_size, float* a_storage,
+                  int* a_shape, int* a_strides, int reduce_dim, float reduce_value,
+                  int shape_size, int fn_id);
+/* reference src/combine.cu:315 */
+void MatrixMultiply(float* out, int* out_shape, int* out_strides, float* a_storage, int* a_shape,
+                    int* a_strides, float* b_storage, int* b_shape, int* b_strides, int batch,
+                    int m, int p);
+
 #ifdef __cplusplus
 }
 #endif

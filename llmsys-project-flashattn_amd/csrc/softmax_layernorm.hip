@@ -1,0 +1,377 @@
+// Companion kernels named in the north star: attention softmax (fwd/bwd) and LayerNorm
+// (fwd/bwd), fp32, device pointers.
+//
+// Contracts (reference file:line):
+//  * softmax fwd, src/softmax_kernel.cu:35-224: y = exp(x + mask − max) / (Σ + 1e-8) per
+//    row of [B, nh, from, to]; masked entries (mask_future: col > row) take −1e8
+//    (REDUCE_FLOAT_INF_NEG, includes/block_reduce.h:13) so a fully masked row stays finite.
+//    The reference kernel reads an additive [B, to] mask (:26-33, :53); here the mask is
+//    any tensor broadcastable to [B, nh, from, to] given by element strides, which covers
+//    [B, to] and also the [B, nh, T, T] / [1, 1, T, T] masks the reference MHA passes
+//    (modules_transfomer.py:140-150, defect A.9 in SURVEY.md).
+//  * softmax bwd, :308-341: dx = y ∘ (dy − Σ dy∘y).
+//  * LayerNorm fwd, src/layernorm_kernel.cu:36-98: μ = E[x], var = E[x²] − μ² + 1e-8
+//    (stored with eps), y = γ (x − μ)/√var + β.
+//  * LayerNorm bwd, :192-368: dβ = Σ dy, dγ = Σ dy·x̂,
+//    dx = (dy·γ − mean(dy·γ) − x̂·mean(dy·γ·x̂)) / √var. (The reference adds eps a
+//    second time inside the backward, :229/:310; this is the exact gradient of the forward.)
+//
+// MI355X design: one wave64 per row with butterfly reductions (no cub/cooperative-group
+// dependency), grid-stride over rows, 16-B vector loads when the row length allows, and a
+// deterministic two-stage column reduction for dγ/dβ (per-block partials in a caller-given
+// workspace, then one pass) instead of atomics.
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/minitorch_hip.h"
+#include "fa_common.h"
+
+namespace mt {
+
+int set_error(const char* fmt, ...);
+int check_hip(hipError_t e, const char* where);
+
+constexpr float kSoftmaxEps = 1e-8f;
+constexpr float kMaskedLogit = -100000000.f;
+constexpr float kLnEps = 1e-8f;
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
+}
+
+static unsigned row_grid(int64_t rows) {
+  int64_t g = (rows + 3) / 4;
+  if (g > 256 * 32) g = 256 * 32;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+// ---------------------------------------------------------------------------- softmax
+struct SoftmaxArgs {
+  float* out; const float* inp; const float* mask;
+  int64_t B, nh, from, to;
+  int64_t ms[4];  // mask strides (b, h, row, col)
+  int mask_future;
+};
+
+__global__ __launch_bounds__(256) void softmax_fw_kernel(SoftmaxArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t rows = a.B * a.nh * a.from;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    const int64_t i = r % a.from, bh = r / a.from, h = bh % a.nh, b = bh / a.nh;
+    const float* x = a.inp + r * a.to;
+    float* y = a.out + r * a.to;
+    const float* mrow = a.mask ? a.mask + b * a.ms[0] + h * a.ms[1] + i * a.ms[2] : nullptr;
+    auto logit = [&](int64_t j) {
+      if (a.mask_future && j > i) return kMaskedLogit;
+      float v = x[j];
+      if (mrow) v += mrow[j * a.ms[3]];
+      return v;
+    };
+    float mx = kMaskedLogit;
+    for (int64_t j = lane; j < a.to; j += 64) mx = fmaxf(mx, logit(j));
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int64_t j = lane; j < a.to; j += 64) s += __expf(logit(j) - mx);
+    s = wave_sum(s);
+    const float inv = 1.f / (s + kSoftmaxEps);
+    for (int64_t j = lane; j < a.to; j += 64) y[j] = __expf(logit(j) - mx) * inv;
+  }
+}
+
+__global__ __launch_bounds__(256) void softmax_bw_kernel(float* dinp, const float* dout,
+                                                         const float* soft, int64_t rows,
+                                                         int64_t len) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    const float* dy = dout + r * len;
+    const float* y = soft + r * len;
+    float s = 0.f;
+    for (int64_t j = lane; j < len; j += 64) s += dy[j] * y[j];
+    s = wave_sum(s);
+    float* dx = dinp + r * len;
+    for (int64_t j = lane; j < len; j += 64) dx[j] = y[j] * (dy[j] - s);
+  }
+}
+
+// -------------------------------------------------------------------------- layernorm
+__global__ __launch_bounds__(256) void ln_fw_kernel(float* ln, float* var_out, float* mean_out,
+                                                    const float* inp, const float* gamma,
+                                                    const float* beta, int64_t rows, int64_t H) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const bool vec = (H % 4) == 0;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    const float* x = inp + r * H;
+    float s = 0.f, ss = 0.f;
+    if (vec) {
+      for (int64_t j = lane * 4; j < H; j += 256) {
+        const float4 v = *(const float4*)(x + j);
+        s += v.x + v.y + v.z + v.w;
+        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      }
+    } else {
+      for (int64_t j = lane; j < H; j += 64) { s += x[j]; ss += x[j] * x[j]; }
+    }
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+    const float mean = s / (float)H;
+    const float var = ss / (float)H - mean * mean + kLnEps;
+    const float rsd = 1.f / sqrtf(var);
+    if (lane == 0) { mean_out[r] = mean; var_out[r] = var; }
+    float* y = ln + r * H;
+    if (vec) {
+      for (int64_t j = lane * 4; j < H; j += 256) {
+        const float4 v = *(const float4*)(x + j);
+        const float4 g = *(const float4*)(gamma + j), bb = *(const float4*)(beta + j);
+        *(float4*)(y + j) = make_float4(g.x * ((v.x - mean) * rsd) + bb.x,
+                                        g.y * ((v.y - mean) * rsd) + bb.y,
+                                        g.z * ((v.z - mean) * rsd) + bb.z,
+                                        g.w * ((v.w - mean) * rsd) + bb.w);
+      }
+    } else {
+      for (int64_t j = lane; j < H; j += 64) y[j] = gamma[j] * ((x[j] - mean) * rsd) + beta[j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bw_dinp_kernel(float* dinp, const float* dout,
+                                                         const float* inp, const float* gamma,
+                                                         const float* var, const float* mean,
+                                                         int64_t rows, int64_t H) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    const float* x = inp + r * H;
+    const float* dy = dout + r * H;
+    const float mu = mean[r], rsd = 1.f / sqrtf(var[r]);
+    float s1 = 0.f, s2 = 0.f;
+    for (int64_t j = lane; j < H; j += 64) {
+      const float g = dy[j] * gamma[j];
+      s1 += g;
+      s2 += g * (x[j] - mu) * rsd;
+    }
+    s1 = wave_sum(s1) / (float)H;
+    s2 = wave_sum(s2) / (float)H;
+    float* dx = dinp + r * H;
+    for (int64_t j = lane; j < H; j += 64) {
+      const float xh = (x[j] - mu) * rsd;
+      dx[j] = (dy[j] * gamma[j] - s1 - xh * s2) * rsd;
+    }
+  }
+}
+
+// Stage 1: block (x = 64-column group, y = row chunk) writes per-chunk partial sums
+// of dβ and dγ into ws[2][chunks][H]. Stage 2 sums the chunks.
+constexpr int kLnRowsPerChunk = 256;
+
+__global__ __launch_bounds__(256) void ln_bw_dgb_partial(float* ws, const float* dout,
+                                                         const float* inp, const float* var,
+                                                         const float* mean, int64_t rows,
+                                                         int64_t H, int64_t chunks) {
+  __shared__ float sb[4][64], sg[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.y * kLnRowsPerChunk;
+  const int64_t r1 = min(rows, r0 + kLnRowsPerChunk);
+  float db = 0.f, dg = 0.f;
+  if (col < H) {
+    for (int64_t r = r0 + wave; r < r1; r += 4) {
+      const float dy = dout[r * H + col];
+      db += dy;
+      dg += dy * (inp[r * H + col] - mean[r]) / sqrtf(var[r]);
+    }
+  }
+  sb[wave][lane] = db;
+  sg[wave][lane] = dg;
+  __syncthreads();
+  if (wave == 0 && col < H) {
+    ws[blockIdx.y * H + col] = sb[0][lane] + sb[1][lane] + sb[2][lane] + sb[3][lane];
+    ws[(chunks + blockIdx.y) * H + col] = sg[0][lane] + sg[1][lane] + sg[2][lane] + sg[3][lane];
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bw_dgb_final(float* dgamma, float* dbeta,
+                                                       const float* ws, int64_t H,
+                                                       int64_t chunks) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= H) return;
+  float db = 0.f, dg = 0.f;
+  for (int64_t c = 0; c < chunks; ++c) {
+    db += ws[c * H + col];
+    dg += ws[(chunks + c) * H + col];
+  }
+  dbeta[col] = db;
+  dgamma[col] = dg;
+}
+
+static int64_t ln_chunks(int64_t rows) { return (rows + kLnRowsPerChunk - 1) / kLnRowsPerChunk; }
+
+}  // namespace mt
+
+using namespace mt;
+
+extern "C" {
+
+int mt_attn_softmax_fw(float* out, const float* inp, const float* mask, int64_t B, int64_t nh,
+                       int64_t from_len, int64_t to_len, const int64_t* mask_strides,
+                       int mask_future, void* stream) {
+  if (B <= 0 || nh <= 0 || from_len <= 0 || to_len <= 0)
+    return set_error("mt_attn_softmax_fw: bad sizes");
+  if (mask && !mask_strides) return set_error("mt_attn_softmax_fw: mask without strides");
+  SoftmaxArgs a;
+  memset(&a, 0, sizeof(a));
+  a.out = out; a.inp = inp; a.mask = mask;
+  a.B = B; a.nh = nh; a.from = from_len; a.to = to_len;
+  if (mask)
+    for (int i = 0; i < 4; ++i) a.ms[i] = mask_strides[i];
+  a.mask_future = mask_future;
+  hipLaunchKernelGGL(softmax_fw_kernel, dim3(row_grid(B * nh * from_len)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_hip(hipGetLastError(), "mt_attn_softmax_fw");
+}
+
+int mt_attn_softmax_bw(float* dinp, const float* dout, const float* soft, int64_t rows,
+                       int64_t softmax_len, void* stream) {
+  if (rows <= 0 || softmax_len <= 0) return set_error("mt_attn_softmax_bw: bad sizes");
+  hipLaunchKernelGGL(softmax_bw_kernel, dim3(row_grid(rows)), dim3(256), 0, (hipStream_t)stream,
+                     dinp, dout, soft, rows, softmax_len);
+  return check_hip(hipGetLastError(), "mt_attn_softmax_bw");
+}
+
+int mt_layernorm_fw(float* ln_res, float* var, float* mean, const float* inp, const float* gamma,
+                    const float* beta, int64_t rows, int64_t hidden, void* stream) {
+  if (rows <= 0 || hidden <= 0) return set_error("mt_layernorm_fw: bad sizes");
+  hipLaunchKernelGGL(ln_fw_kernel, dim3(row_grid(rows)), dim3(256), 0, (hipStream_t)stream,
+                     ln_res, var, mean, inp, gamma, beta, rows, hidden);
+  return check_hip(hipGetLastError(), "mt_layernorm_fw");
+}
+
+int64_t mt_layernorm_bw_workspace_bytes(int64_t rows, int64_t hidden) {
+  return 2 * ln_chunks(rows) * hidden * (int64_t)sizeof(float);
+}
+
+int mt_layernorm_bw(float* gamma_grad, float* beta_grad, float* inp_grad, const float* out_grad,
+                    const float* inp, const float* gamma, const float* beta, const float* var,
+                    const float* mean, int64_t rows, int64_t hidden, void* workspace,
+                    void* stream) {
+  (void)beta;
+  if (rows <= 0 || hidden <= 0) return set_error("mt_layernorm_bw: bad sizes");
+  if (!workspace) return set_error("mt_layernorm_bw: null workspace");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t chunks = ln_chunks(rows);
+  if (chunks > 65535) return set_error("mt_layernorm_bw: too many rows");
+  hipLaunchKernelGGL(ln_bw_dgb_partial, dim3((unsigned)((hidden + 63) / 64), (unsigned)chunks),
+                     dim3(256), 0, st, (float*)workspace, out_grad, inp, var, mean, rows, hidden,
+                     chunks);
+  if (check_hip(hipGetLastError(), "mt_layernorm_bw(partial)")) return 1;
+  hipLaunchKernelGGL(ln_bw_dgb_final, dim3((unsigned)((hidden + 255) / 256)), dim3(256), 0, st,
+                     gamma_grad, beta_grad, (const float*)workspace, hidden, chunks);
+  if (check_hip(hipGetLastError(), "mt_layernorm_bw(final)")) return 1;
+  hipLaunchKernelGGL(ln_bw_dinp_kernel, dim3(row_grid(rows)), dim3(256), 0, st, inp_grad,
+                     out_grad, inp, gamma, var, mean, rows, hidden);
+  return check_hip(hipGetLastError(), "mt_layernorm_bw(dinp)");
+}
+
+// ---- reference-compatible host-pointer wrappers (copy in, run, copy out) -------------
+static int h2d(void** d, const void* h, size_t n, const char* w) {
+  if (check_hip(hipMalloc(d, n ? n : 4), w)) return 1;
+  return h ? check_hip(hipMemcpy(*d, h, n, hipMemcpyHostToDevice), w) : 0;
+}
+
+/* reference src/softmax_kernel.cu:233 — attn_mask is [batch, to_len] (or NULL). */
+void launch_attn_softmax(float* inp, const float* attn_mask, int batch_size, int nhead,
+                         int from_len, int to_len, bool mask_future, void* stream) {
+  const size_t n = (size_t)batch_size * nhead * from_len * to_len * 4;
+  const size_t mn = (size_t)batch_size * to_len * 4;
+  void *d_inp = nullptr, *d_mask = nullptr;
+  int64_t ms[4] = {to_len, 0, 0, 1};
+  int rc = h2d(&d_inp, inp, n, "launch_attn_softmax") ||
+           (attn_mask && h2d(&d_mask, attn_mask, mn, "launch_attn_softmax")) ||
+           mt_attn_softmax_fw((float*)d_inp, (const float*)d_inp, (const float*)d_mask,
+                              batch_size, nhead, from_len, to_len, attn_mask ? ms : nullptr,
+                              mask_future ? 1 : 0, stream) ||
+           check_hip(hipStreamSynchronize((hipStream_t)stream), "launch_attn_softmax") ||
+           check_hip(hipMemcpy(inp, d_inp, n, hipMemcpyDeviceToHost), "launch_attn_softmax");
+  if (rc) fprintf(stderr, "launch_attn_softmax failed: %s\n", mt_last_error());
+  if (d_inp) (void)hipFree(d_inp);
+  if (d_mask) (void)hipFree(d_mask);
+}
+
+/* reference src/softmax_kernel.cu:345 — in place on out_grad. */
+void launch_attn_softmax_bw(float* out_grad, const float* soft_inp, int rows, int softmax_len,
+                            void* stream) {
+  const size_t n = (size_t)rows * softmax_len * 4;
+  void *d_g = nullptr, *d_s = nullptr;
+  int rc = h2d(&d_g, out_grad, n, "launch_attn_softmax_bw") ||
+           h2d(&d_s, soft_inp, n, "launch_attn_softmax_bw") ||
+           mt_attn_softmax_bw((float*)d_g, (const float*)d_g, (const float*)d_s, rows, softmax_len,
+                              stream) ||
+           check_hip(hipStreamSynchronize((hipStream_t)stream), "launch_attn_softmax_bw") ||
+           check_hip(hipMemcpy(out_grad, d_g, n, hipMemcpyDeviceToHost), "launch_attn_softmax_bw");
+  if (rc) fprintf(stderr, "launch_attn_softmax_bw failed: %s\n", mt_last_error());
+  if (d_g) (void)hipFree(d_g);
+  if (d_s) (void)hipFree(d_s);
+}
+
+/* reference src/layernorm_kernel.cu:101 */
+void launch_layernorm(float* ln_res, float* vars, float* means, const float* inp,
+                      const float* scale, const float* bias, int batch_size, int hidden_dim,
+                      void* stream) {
+  const size_t n = (size_t)batch_size * hidden_dim * 4, h = (size_t)hidden_dim * 4,
+               r = (size_t)batch_size * 4;
+  void *d_ln = nullptr, *d_var = nullptr, *d_mean = nullptr, *d_inp = nullptr, *d_g = nullptr,
+       *d_b = nullptr;
+  const char* w = "launch_layernorm";
+  int rc = h2d(&d_ln, nullptr, n, w) || h2d(&d_var, nullptr, r, w) || h2d(&d_mean, nullptr, r, w) ||
+           h2d(&d_inp, inp, n, w) || h2d(&d_g, scale, h, w) || h2d(&d_b, bias, h, w) ||
+           mt_layernorm_fw((float*)d_ln, (float*)d_var, (float*)d_mean, (const float*)d_inp,
+                           (const float*)d_g, (const float*)d_b, batch_size, hidden_dim, stream) ||
+           check_hip(hipStreamSynchronize((hipStream_t)stream), w) ||
+           check_hip(hipMemcpy(ln_res, d_ln, n, hipMemcpyDeviceToHost), w) ||
+           check_hip(hipMemcpy(vars, d_var, r, hipMemcpyDeviceToHost), w) ||
+           check_hip(hipMemcpy(means, d_mean, r, hipMemcpyDeviceToHost), w);
+  if (rc) fprintf(stderr, "launch_layernorm failed: %s\n", mt_last_error());
+  void* bufs[6] = {d_ln, d_var, d_mean, d_inp, d_g, d_b};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+}
+
+/* reference src/layernorm_kernel.cu:370 (two streams there; one here). */
+void launch_layernorm_bw(float* gamma_grad, float* betta_grad, float* inp_grad,
+                         const float* out_grad, const float* inp, const float* gamma,
+                         const float* betta, const float* vars, const float* means,
+                         int batch_size, int hidden_dim, void* stream_1, void* stream_2) {
+  (void)stream_2;
+  const size_t n = (size_t)batch_size * hidden_dim * 4, h = (size_t)hidden_dim * 4,
+               r = (size_t)batch_size * 4;
+  const char* w = "launch_layernorm_bw";
+  void *d_dg = nullptr, *d_db = nullptr, *d_dx = nullptr, *d_dy = nullptr, *d_x = nullptr,
+       *d_g = nullptr, *d_b = nullptr, *d_v = nullptr, *d_m = nullptr, *d_ws = nullptr;
+  int rc = h2d(&d_dg, nullptr, h, w) || h2d(&d_db, nullptr, h, w) || h2d(&d_dx, nullptr, n, w) ||
+           h2d(&d_dy, out_grad, n, w) || h2d(&d_x, inp, n, w) || h2d(&d_g, gamma, h, w) ||
+           h2d(&d_b, betta, h, w) || h2d(&d_v, vars, r, w) || h2d(&d_m, means, r, w) ||
+           h2d(&d_ws, nullptr, (size_t)mt_layernorm_bw_workspace_bytes(batch_size, hidden_dim), w) ||
+           mt_layernorm_bw((float*)d_dg, (float*)d_db, (float*)d_dx, (const float*)d_dy,
+                           (const float*)d_x, (const float*)d_g, (const float*)d_b,
+                           (const float*)d_v, (const float*)d_m, batch_size, hidden_dim, d_ws,
+                           stream_1) ||
+           check_hip(hipStreamSynchronize((hipStream_t)stream_1), w) ||
+           check_hip(hipMemcpy(gamma_grad, d_dg, h, hipMemcpyDeviceToHost), w) ||
+           check_hip(hipMemcpy(betta_grad, d_db, h, hipMemcpyDeviceToHost), w) ||
+           check_hip(hipMemcpy(inp_grad, d_dx, n, hipMemcpyDeviceToHost), w);
+  if (rc) fprintf(stderr, "launch_layernorm_bw failed: %s\n", mt_last_error());
+  void* bufs[10] = {d_dg, d_db, d_dx, d_dy, d_x, d_g, d_b, d_v, d_m, d_ws};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+}
+
+}  // extern "C"

@@ -27,6 +27,7 @@ _int = ctypes.c_int
 _vp = ctypes.c_void_p
 _fp = ctypes.POINTER(ctypes.c_float)
 _i64p = ctypes.POINTER(ctypes.c_int64)
+_ip = ctypes.POINTER(ctypes.c_int)
 
 # name -> (restype, argtypes); mirrors include/minitorch_hip.h
 _PROTOS = {
@@ -38,6 +39,26 @@ _PROTOS = {
     "mt_flash_attn_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "mt_flash_attn_bwd": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _i64, _i64, _i64, _i64, _i64p, _vp, _vp]),
+    "mt_attn_softmax_fw": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _int, _vp]),
+    "mt_attn_softmax_bw": (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
+    "mt_layernorm_fw": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
+    "mt_layernorm_bw_workspace_bytes": (_i64, [_i64, _i64]),
+    "mt_layernorm_bw": (_int, [_vp] * 9 + [_i64, _i64, _vp, _vp]),
+    "mt_tensor_map": (_int, [_int, _vp, _i64p, _i64p, _int, _vp, _i64p, _i64p, _int, _vp]),
+    "mt_tensor_zip": (_int, [_int, _vp, _i64p, _i64p, _int, _vp, _i64p, _i64p, _int,
+                             _vp, _i64p, _i64p, _int, _vp]),
+    "mt_tensor_reduce": (_int, [_int, _vp, _i64p, _i64p, _vp, _i64p, _i64p, _int, _int,
+                                ctypes.c_float, _vp]),
+    "mt_matmul_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _i64p, _i64p, _vp]),
+    "launch_attn_softmax": (None, [_fp, _fp, _int, _int, _int, _int, ctypes.c_bool, _vp]),
+    "launch_attn_softmax_bw": (None, [_fp, _fp, _int, _int, _vp]),
+    "launch_layernorm": (None, [_fp] * 6 + [_int, _int, _vp]),
+    "launch_layernorm_bw": (None, [_fp] * 9 + [_int, _int, _vp, _vp]),
+    "tensorMap": (None, [_fp, _ip, _ip, _int, _fp, _ip, _ip, _int, _int, _int]),
+    "tensorZip": (None, [_fp, _ip, _ip, _int, _int, _fp, _ip, _ip, _int, _int,
+                         _fp, _ip, _ip, _int, _int, _int]),
+    "tensorReduce": (None, [_fp, _ip, _ip, _int, _fp, _ip, _ip, _int, ctypes.c_float, _int, _int]),
+    "MatrixMultiply": (None, [_fp, _ip, _ip, _fp, _ip, _ip, _fp, _ip, _ip, _int, _int, _int]),
     "launch_flashattention_forward": (None, [_fp] * 6 + [_int] * 4),
     "launch_flashattention_backward": (None, [_fp] * 10 + [_int] * 4),
     "launch_flashattention_forward_causal": (None, [_fp] * 6 + [_int] * 4),

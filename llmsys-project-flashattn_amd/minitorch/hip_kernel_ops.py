@@ -1,0 +1,268 @@
+"""``HipKernelOps``: the MI355X backend for ``TensorBackend`` (drop-in for the reference's
+``CudaKernelOps``, ``minitorch/cuda_kernel_ops.py``).
+
+Every storage is device-resident (``cuda = True``): tensors are uploaded once by
+``tensor_from_numpy`` and every operator -- map/zip/reduce/matmul and the fused softmax,
+LayerNorm and FlashAttention kernels -- runs as a stream-ordered HIP kernel from
+``libminitorch_hip.so`` on device pointers. The reference instead round-trips every
+operand host->device->host inside each launcher (flashattention_kernel.cu:284-324,
+combine.cu:345-382). There is no CPU fallback: a missing library raises.
+
+Fused-op contracts (reference cuda_kernel_ops.py:439-892):
+  attn_softmax_fw(inp, mask)              -> softmax(inp + mask) (new tensor)
+  attn_softmax_bw(out_grad, soft_inp)     -> (inp_grad, soft_inp)
+  layernorm_fw(inp, gamma, beta)          -> (ln_res, var, means)
+  layernorm_bw(dout, inp, gamma, beta, var, mean) -> (inp_grad, gamma_grad[1,H], beta_grad[1,H])
+  flash_attention[_causal]_fw(Q, K, V)    -> (O, m, l)      P = exp(s - m) / l
+  flash_attention[_causal]_bw(Q, K, V, O, dO, m, l) -> (dQ, dK, dV)
+Q/K/V may be strided views (e.g. the permuted projections of MultiHeadAttention): the
+kernels take (batch, head, seq) strides, so no ``.contiguous()`` copy is made.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, Optional
+
+import numpy as np
+
+from . import _hip
+from . import operators
+from .tensor import Tensor
+from .tensor_data import TensorData, shape_broadcast
+from .tensor_ops import MapProto, TensorOps
+
+
+def _i64(vals) -> ctypes.Array:
+    vals = [int(v) for v in vals]
+    return (ctypes.c_int64 * max(1, len(vals)))(*vals)
+
+
+def _dev(t: Tensor) -> Tensor:
+    if not t._tensor.on_device:
+        t._tensor.to_cuda_()
+    return t
+
+
+def _ptr(t: Tensor) -> int:
+    return _dev(t)._tensor.data_ptr()
+
+
+def _stream() -> int:
+    return _hip.stream_ptr()
+
+
+def _fn_id(fn: Callable) -> int:
+    try:
+        return operators.FN_IDS[fn]
+    except KeyError:
+        raise NotImplementedError(f"no device kernel for {getattr(fn, '__name__', fn)}") from None
+
+
+def _torch_view(t: Tensor):
+    """A torch view of a minitorch tensor's storage with its shape and strides (plumbing
+    for the flash entry points, which read strides from torch tensors)."""
+    import torch
+    st = _dev(t)._tensor._storage
+    return torch.as_strided(st, t.shape, t._tensor.strides)
+
+
+def _wrap(storage, shape, backend, strides=None) -> Tensor:
+    return Tensor(TensorData(storage, tuple(shape), strides), backend=backend)
+
+
+class HipKernelOps(TensorOps):
+    cuda = True
+
+    @staticmethod
+    def map(fn: Callable[[float], float]) -> MapProto:
+        fid = _fn_id(fn)
+
+        def ret(a: Tensor, out: Optional[Tensor] = None) -> Tensor:
+            if out is None:
+                out = a.zeros(a.shape)
+            _hip.check(_hip.lib().mt_tensor_map(
+                fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides), out.dims,
+                _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims, _stream()), "map")
+            return out
+
+        return ret
+
+    @staticmethod
+    def cmap(fn: Callable[[float], float]) -> Callable[[Tensor, Tensor], Tensor]:
+        fid = _fn_id(fn)
+
+        def ret(a: Tensor, out: Tensor) -> Tensor:
+            _hip.check(_hip.lib().mt_tensor_map(
+                fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides), out.dims,
+                _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims, _stream()), "cmap")
+            return out
+
+        return ret
+
+    @staticmethod
+    def zip(fn: Callable[[float, float], float]) -> Callable[[Tensor, Tensor], Tensor]:
+        fid = _fn_id(fn)
+
+        def ret(a: Tensor, b: Tensor) -> Tensor:
+            shape = shape_broadcast(a.shape, b.shape)
+            out = a.zeros(shape)
+            _hip.check(_hip.lib().mt_tensor_zip(
+                fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides), out.dims,
+                _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims,
+                _ptr(b), _i64(b.shape), _i64(b._tensor.strides), b.dims, _stream()), "zip")
+            return out
+
+        return ret
+
+    @staticmethod
+    def reduce(fn: Callable[[float, float], float], start: float = 0.0) -> Callable[[Tensor, int], Tensor]:
+        fid = _fn_id(fn)
+
+        def ret(a: Tensor, dim: int) -> Tensor:
+            shape = list(a.shape)
+            shape[dim] = 1
+            out = a.zeros(tuple(shape))
+            _hip.check(_hip.lib().mt_tensor_reduce(
+                fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides),
+                _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims, int(dim),
+                ctypes.c_float(start), _stream()), "reduce")
+            return out
+
+        return ret
+
+    @staticmethod
+    def matrix_multiply(a: Tensor, b: Tensor) -> Tensor:
+        """Batched a @ b over broadcast leading dims (reference cuda_kernel_ops.py:340-437
+        flattens to 3-D the same way)."""
+        both_2d = a.dims == 2 and b.dims == 2
+        if a.dims == 2:
+            a = a.view(1, *a.shape) if a._tensor.is_dense() else a.contiguous().view(1, *a.shape)
+        if b.dims == 2:
+            b = b.view(1, *b.shape) if b._tensor.is_dense() else b.contiguous().view(1, *b.shape)
+        lead = tuple(shape_broadcast(a.shape[:-2], b.shape[:-2]))
+        M, K = a.shape[-2], a.shape[-1]
+        K2, N = b.shape[-2], b.shape[-1]
+        assert K == K2, f"matmul shape mismatch {a.shape} @ {b.shape}"
+        batch = int(np.prod(lead)) if lead else 1
+
+        def batch_view(t: Tensor):
+            # (batch stride, row stride, col stride); a broadcast operand gets stride 0.
+            if t.dims == 3 and len(lead) == 1:
+                bs = 0 if t.shape[0] == 1 and batch > 1 else t._tensor.strides[0]
+                return t, (bs, t._tensor.strides[1], t._tensor.strides[2])
+            tl = t.shape[:-2]
+            if int(np.prod(tl)) == 1 and batch > 1:
+                return t, (0, t._tensor.strides[-2], t._tensor.strides[-1])
+            if tuple(tl) != lead:
+                raise NotImplementedError(f"partial batch broadcast {t.shape} vs {lead}")
+            if not t._tensor.is_dense():
+                t = t.contiguous()
+            s = t._tensor.strides
+            return t, (s[-3], s[-2], s[-1])
+
+        a, sa = batch_view(a)
+        b, sb = batch_view(b)
+        out = a.zeros(lead + (M, N))
+        so = (M * N, N, 1)
+        _hip.check(_hip.lib().mt_matmul_f32(_ptr(out), _ptr(a), _ptr(b), batch, M, N, K,
+                                            _i64(sa), _i64(sb), _i64(so), _stream()), "matmul")
+        if both_2d:
+            return out.view(M, N)
+        return out
+
+    # ---- fused kernels -------------------------------------------------------------------
+    @staticmethod
+    def attn_softmax_fw(inp: Tensor, mask: Optional[Tensor], mask_future: bool = False) -> Tensor:
+        B, nh, T_from, T_to = inp.shape
+        x = inp if inp._tensor.is_dense() else inp.contiguous()
+        out = x.zeros(x.shape)
+        mptr, ms = None, None
+        if mask is not None:
+            mshape = (1,) * (4 - mask.dims) + tuple(mask.shape)
+            mstr = (0,) * (4 - mask.dims) + tuple(mask._tensor.strides)
+            ms = _i64([0 if mshape[i] == 1 else mstr[i] for i in range(4)])
+            mptr = _ptr(mask)
+        _hip.check(_hip.lib().mt_attn_softmax_fw(_ptr(out), _ptr(x), mptr, B, nh, T_from, T_to, ms,
+                                                 int(mask_future), _stream()), "attn_softmax_fw")
+        return out
+
+    @staticmethod
+    def attn_softmax_bw(out_grad: Tensor, soft_inp: Tensor):
+        g = out_grad if out_grad._tensor.is_dense() else out_grad.contiguous()
+        y = soft_inp if soft_inp._tensor.is_dense() else soft_inp.contiguous()
+        rows = int(np.prod(y.shape[:-1]))
+        dinp = g.zeros(g.shape)
+        _hip.check(_hip.lib().mt_attn_softmax_bw(_ptr(dinp), _ptr(g), _ptr(y), rows, y.shape[-1],
+                                                 _stream()), "attn_softmax_bw")
+        return dinp, soft_inp
+
+    @staticmethod
+    def layernorm_fw(inp: Tensor, gamma: Tensor, beta: Tensor):
+        x = inp if inp._tensor.is_dense() else inp.contiguous()
+        rows, H = x.shape
+        ln = x.zeros(x.shape)
+        var = x.zeros((rows,))
+        mean = x.zeros((rows,))
+        _hip.check(_hip.lib().mt_layernorm_fw(_ptr(ln), _ptr(var), _ptr(mean), _ptr(x),
+                                              _ptr(gamma.contiguous()), _ptr(beta.contiguous()),
+                                              rows, H, _stream()), "layernorm_fw")
+        return ln, var, mean
+
+    @staticmethod
+    def layernorm_bw(out_grad: Tensor, inp: Tensor, gamma: Tensor, beta: Tensor, var: Tensor,
+                     mean: Tensor):
+        import torch
+        g = out_grad if out_grad._tensor.is_dense() else out_grad.contiguous()
+        x = inp if inp._tensor.is_dense() else inp.contiguous()
+        rows, H = x.shape
+        dx = x.zeros(x.shape)
+        dgamma = x.zeros((1, H))
+        dbeta = x.zeros((1, H))
+        ws = torch.empty(max(1, _hip.lib().mt_layernorm_bw_workspace_bytes(rows, H) // 4),
+                         dtype=torch.float32, device="cuda")
+        _hip.check(_hip.lib().mt_layernorm_bw(_ptr(dgamma), _ptr(dbeta), _ptr(dx), _ptr(g), _ptr(x),
+                                              _ptr(gamma.contiguous()), _ptr(beta.contiguous()),
+                                              _ptr(var), _ptr(mean), rows, H, ws.data_ptr(),
+                                              _stream()), "layernorm_bw")
+        return dx, dgamma, dbeta
+
+    @staticmethod
+    def _flash_fw(Q: Tensor, K: Tensor, V: Tensor, causal: bool):
+        import torch
+        B, H, N, d = Q.shape
+        backend = Q.backend
+        o = torch.empty(B * H * N * d, dtype=torch.float32, device="cuda")
+        m = torch.empty(B * H * N, dtype=torch.float32, device="cuda")
+        l = torch.empty(B * H * N, dtype=torch.float32, device="cuda")
+        _hip.flash_fwd(_torch_view(Q), _torch_view(K), _torch_view(V), causal,
+                       out=o.view(B, H, N, d), m=m.view(B, H, N), l=l.view(B, H, N))
+        return (_wrap(o, (B, H, N, d), backend), _wrap(m, (B, H, N), backend),
+                _wrap(l, (B, H, N), backend))
+
+    @staticmethod
+    def _flash_bw(Q, K, V, O, dO, m, l, causal: bool):
+        import torch
+        B, H, N, d = Q.shape
+        backend = Q.backend
+        bufs = [torch.empty(B * H * N * d, dtype=torch.float32, device="cuda") for _ in range(3)]
+        _hip.flash_bwd(_torch_view(Q), _torch_view(K), _torch_view(V), _torch_view(O),
+                       _torch_view(dO), _torch_view(m), _torch_view(l), causal,
+                       dq=bufs[0].view(B, H, N, d), dk=bufs[1].view(B, H, N, d),
+                       dv=bufs[2].view(B, H, N, d))
+        return tuple(_wrap(b, (B, H, N, d), backend) for b in bufs)
+
+    @staticmethod
+    def flash_attention_fw(Q: Tensor, K: Tensor, V: Tensor):
+        return HipKernelOps._flash_fw(Q, K, V, False)
+
+    @staticmethod
+    def flash_attention_bw(Q, K, V, O, dO, m, l):
+        return HipKernelOps._flash_bw(Q, K, V, O, dO, m, l, False)
+
+    @staticmethod
+    def flash_attention_causal_fw(Q: Tensor, K: Tensor, V: Tensor):
+        return HipKernelOps._flash_fw(Q, K, V, True)
+
+    @staticmethod
+    def flash_attention_causal_bw(Q, K, V, O, dO, m, l):
+        return HipKernelOps._flash_bw(Q, K, V, O, dO, m, l, True)

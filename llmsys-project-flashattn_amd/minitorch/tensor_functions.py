@@ -1,0 +1,454 @@
+"""Autodiff ``Function``s and tensor constructors (reference ``minitorch/tensor_functions.py``).
+
+The fused functions are the hot path of the north star:
+``FlashAttention`` / ``FlashAttentionCausal`` (reference :472-516) call
+``Q.f.flash_attention[_causal]_fw`` and save ``(Q, K, V, O, m, l)``; their backward calls
+``out_grad.f.flash_attention[_causal]_bw``. ``Attn_Softmax`` saves the softmax *output*
+(what its backward needs; the reference saves the input and then mis-unpacks it,
+:440/:447) and ``LayerNorm`` saves ``(inp, gamma, beta, var, mean)``.
+"""
+from __future__ import annotations
+
+import random
+from typing import Any, List, Optional, Tuple
+
+import numpy as np
+
+from . import operators
+from .autodiff import Context
+from .tensor_data import TensorData, UserShape, datatype, strides_from_shape
+
+
+def wrap_tuple(x: Any) -> tuple:
+    return x if isinstance(x, tuple) else (x,)
+
+
+class Function:
+    @classmethod
+    def _backward(cls, ctx: Context, grad_out) -> tuple:
+        return wrap_tuple(cls.backward(ctx, grad_out))
+
+    @classmethod
+    def _forward(cls, ctx: Context, *inps):
+        return cls.forward(ctx, *inps)
+
+    @classmethod
+    def apply(cls, *vals):
+        from .tensor import History, Tensor
+        raw_vals = []
+        need_grad = False
+        for v in vals:
+            if v.requires_grad():
+                need_grad = True
+            raw_vals.append(v.detach())
+        ctx = Context(not need_grad)
+        c = cls._forward(ctx, *raw_vals)
+        back = History(cls, ctx, vals) if need_grad else None
+        return Tensor(c._tensor, back, backend=c.backend)
+
+
+class Neg(Function):
+    @staticmethod
+    def forward(ctx, t1):
+        return t1.f.neg_map(t1)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return grad_output.f.neg_map(grad_output)
+
+
+class Inv(Function):
+    @staticmethod
+    def forward(ctx, t1):
+        ctx.save_for_backward(t1)
+        return t1.f.inv_map(t1)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (t1,) = ctx.saved_values
+        return grad_output.f.inv_back_zip(t1, grad_output)
+
+
+class Add(Function):
+    @staticmethod
+    def forward(ctx, t1, t2):
+        return t1.f.add_zip(t1, t2)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return grad_output, grad_output
+
+
+class Mul(Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return a.f.mul_zip(a, b)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        a, b = ctx.saved_values
+        return grad_output.f.mul_zip(b, grad_output), grad_output.f.mul_zip(a, grad_output)
+
+
+class PowerScalar(Function):
+    @staticmethod
+    def forward(ctx, a, scalar):
+        ctx.save_for_backward(a, scalar)
+        return a.f.pow_scalar_zip(a, scalar)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        a, scalar = ctx.saved_values
+        s = scalar.item()
+        # d/da a^s = s * a^(s-1)
+        da = grad_output.f.mul_zip(
+            grad_output,
+            a.f.mul_zip(a.f.pow_scalar_zip(a, a._ensure_tensor(s - 1.0)), a._ensure_tensor(s)))
+        return da, 0.0
+
+
+class Tanh(Function):
+    @staticmethod
+    def forward(ctx, a):
+        out = a.f.tanh_map(a)
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (out,) = ctx.saved_values
+        one_minus = out.f.add_zip(out._ensure_tensor(1.0), out.f.neg_map(out.f.mul_zip(out, out)))
+        return grad_output.f.mul_zip(grad_output, one_minus)
+
+
+class Sigmoid(Function):
+    @staticmethod
+    def forward(ctx, t1):
+        out = t1.f.sigmoid_map(t1)
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (s,) = ctx.saved_values
+        ds = s.f.mul_zip(s, s.f.add_zip(s._ensure_tensor(1.0), s.f.neg_map(s)))
+        return grad_output.f.mul_zip(grad_output, ds)
+
+
+class ReLU(Function):
+    @staticmethod
+    def forward(ctx, t1):
+        ctx.save_for_backward(t1)
+        return t1.f.relu_map(t1)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (t1,) = ctx.saved_values
+        return grad_output.f.relu_back_zip(t1, grad_output)
+
+
+class Log(Function):
+    @staticmethod
+    def forward(ctx, t1):
+        ctx.save_for_backward(t1)
+        return t1.f.log_map(t1)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (t1,) = ctx.saved_values
+        return grad_output.f.log_back_zip(t1, grad_output)
+
+
+class Exp(Function):
+    @staticmethod
+    def forward(ctx, t1):
+        out = t1.f.exp_map(t1)
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (out,) = ctx.saved_values
+        return grad_output.f.mul_zip(out, grad_output)
+
+
+class Sum(Function):
+    @staticmethod
+    def forward(ctx, a, dim):
+        ctx.save_for_backward(a.shape, dim)
+        return a.f.add_reduce(a, int(dim.item()))
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return grad_output, 0.0
+
+
+class All(Function):
+    @staticmethod
+    def forward(ctx, a, dim):
+        if dim is not None:
+            return a.f.mul_reduce(a, int(dim.item()))
+        return a.f.mul_reduce(a.contiguous().view(int(operators.prod(a.shape))), 0)
+
+
+class LT(Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a.shape, b.shape)
+        return a.f.lt_zip(a, b)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        a_shape, b_shape = ctx.saved_values
+        return grad_output.zeros(a_shape), grad_output.zeros(b_shape)
+
+
+class EQ(Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a.shape, b.shape)
+        return a.f.eq_zip(a, b)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        a_shape, b_shape = ctx.saved_values
+        return grad_output.zeros(a_shape), grad_output.zeros(b_shape)
+
+
+class IsClose(Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        return a.f.is_close_zip(a, b)
+
+
+class Permute(Function):
+    @staticmethod
+    def forward(ctx, a, order):
+        order_l = [int(order[i]) for i in range(order.size)]
+        ctx.save_for_backward(order_l)
+        return a._new(a._tensor.permute(*order_l))
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (order_l,) = ctx.saved_values
+        inv = [0] * len(order_l)
+        for i, o in enumerate(order_l):
+            inv[o] = i
+        return grad_output._new(grad_output._tensor.permute(*inv)), 0.0
+
+
+class View(Function):
+    @staticmethod
+    def forward(ctx, a, shape):
+        ctx.save_for_backward(a.shape)
+        if not a._tensor.is_dense():
+            raise AssertionError("Must be contiguous to view")
+        shape2 = [int(shape[i]) for i in range(shape.size)]
+        from .tensor import Tensor
+        return Tensor.make(a._tensor._storage, tuple(shape2), backend=a.backend)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        (original,) = ctx.saved_values
+        from .tensor import Tensor
+        g = grad_output if grad_output._tensor.is_dense() else grad_output.contiguous()
+        return Tensor.make(g._tensor._storage, original, backend=g.backend), 0.0
+
+
+class Copy(Function):
+    @staticmethod
+    def forward(ctx, a):
+        return a.f.id_map(a)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return grad_output
+
+
+class MatMul(Function):
+    @staticmethod
+    def forward(ctx, t1, t2):
+        ctx.save_for_backward(t1, t2)
+        return t1.f.matrix_multiply(t1, t2)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        t1, t2 = ctx.saved_values
+
+        def transpose(a):
+            order = list(range(a.dims))
+            order[-2], order[-1] = order[-1], order[-2]
+            return a._new(a._tensor.permute(*order))
+
+        return (grad_output.f.matrix_multiply(grad_output, transpose(t2)),
+                grad_output.f.matrix_multiply(transpose(t1), grad_output))
+
+
+class Attn_Softmax(Function):  # noqa: N801 - reference name
+    @staticmethod
+    def forward(ctx, inp, mask):
+        out = inp.f.attn_softmax_fw(inp, mask)
+        ctx.save_for_backward(out, mask.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, out_grad):
+        out, mask_shape = ctx.saved_values
+        dinp, _ = out_grad.f.attn_softmax_bw(out_grad, out)
+        return dinp, out_grad.zeros(mask_shape)
+
+
+class Attn_Softmax_NoMask(Function):  # noqa: N801
+    """Row softmax without an additive mask; ``future`` (a host constant 0/1) masks
+    col > row inside the kernel (the decoder self-attention case)."""
+
+    @staticmethod
+    def forward(ctx, inp, future):
+        out = inp.f.attn_softmax_fw(inp, None, mask_future=bool(future.item()))
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, out_grad):
+        (out,) = ctx.saved_values
+        dinp, _ = out_grad.f.attn_softmax_bw(out_grad, out)
+        return dinp, 0.0
+
+
+class LayerNorm(Function):
+    @staticmethod
+    def forward(ctx, inp, gamma, beta):
+        ln_res, var, means = inp.f.layernorm_fw(inp, gamma, beta)
+        ctx.save_for_backward(inp, gamma, beta, var, means)
+        return ln_res
+
+    @staticmethod
+    def backward(ctx, out_grad):
+        inp, gamma, beta, var, means = ctx.saved_values
+        return out_grad.f.layernorm_bw(out_grad, inp, gamma, beta, var, means)
+
+
+class FlashAttention(Function):
+    @staticmethod
+    def forward(ctx, Q, K, V):  # noqa: N803 - reference names
+        O, m, l = Q.f.flash_attention_fw(Q, K, V)
+        ctx.save_for_backward(Q, K, V, O, m, l)
+        return O
+
+    @staticmethod
+    def backward(ctx, out_grad):
+        Q, K, V, O, m, l = ctx.saved_values
+        return out_grad.f.flash_attention_bw(Q, K, V, O, out_grad, m, l)
+
+
+class FlashAttentionCausal(Function):
+    @staticmethod
+    def forward(ctx, Q, K, V):  # noqa: N803
+        O, m, l = Q.f.flash_attention_causal_fw(Q, K, V)
+        ctx.save_for_backward(Q, K, V, O, m, l)
+        return O
+
+    @staticmethod
+    def backward(ctx, out_grad):
+        Q, K, V, O, m, l = ctx.saved_values
+        return out_grad.f.flash_attention_causal_bw(Q, K, V, O, out_grad, m, l)
+
+
+# ---- constructors --------------------------------------------------------------------
+def _backend_or_raise(backend):
+    if backend is None:
+        raise ValueError("a TensorBackend is required (e.g. TensorBackend(HipKernelOps))")
+    return backend
+
+
+def zeros(shape: UserShape, backend=None):
+    from .tensor import Tensor
+    backend = _backend_or_raise(backend)
+    shape = tuple(int(s) for s in shape)
+    if backend.cuda:
+        import torch
+        size = int(np.prod(shape)) if shape else 1
+        st = torch.zeros(size, dtype=torch.float32, device="cuda")
+        return Tensor(TensorData(st, shape), backend=backend)
+    t = Tensor.make(np.zeros(int(np.prod(shape)) if shape else 1, dtype=datatype), shape, backend=backend)
+    return t
+
+
+def ones(shape: UserShape, backend=None):
+    from .tensor import Tensor
+    backend = _backend_or_raise(backend)
+    shape = tuple(int(s) for s in shape)
+    t = Tensor.make(np.ones(int(np.prod(shape)) if shape else 1, dtype=datatype), shape, backend=backend)
+    t._type_(backend)
+    return t
+
+
+def rand(shape: UserShape, backend=None, requires_grad: bool = False):
+    from .tensor import Tensor
+    backend = _backend_or_raise(backend)
+    vals = np.array([random.random() for _ in range(int(np.prod(shape)))], dtype=datatype)
+    t = Tensor.make(vals, tuple(shape), backend=backend)
+    t._type_(backend)
+    t.requires_grad_(requires_grad)
+    return t
+
+
+def _tensor(ls, shape: UserShape, backend=None, requires_grad: bool = False):
+    from .tensor import Tensor
+    backend = _backend_or_raise(backend)
+    t = Tensor.make(np.array(ls, dtype=datatype), tuple(shape), backend=backend)
+    t._type_(backend)
+    t.requires_grad_(requires_grad)
+    return t
+
+
+def tensor(ls: Any, backend=None, requires_grad: bool = False):
+    arr = np.array(ls, dtype=datatype)
+    shape = arr.shape if arr.shape else (1,)
+    return _tensor(arr.reshape(-1).tolist(), shape, backend=backend, requires_grad=requires_grad)
+
+
+def tensor_from_numpy(ls: np.ndarray, backend=None, requires_grad: bool = False):
+    """Copy a NumPy array into a new tensor on ``backend`` (device-resident for HIP)."""
+    from .tensor import Tensor
+    backend = _backend_or_raise(backend)
+    arr = np.ascontiguousarray(ls, dtype=datatype)
+    shape = arr.shape if arr.shape else (1,)
+    t = Tensor(TensorData(arr.reshape(-1).copy(), shape, strides_from_shape(shape)), backend=backend)
+    t._type_(backend)
+    t.requires_grad_(requires_grad)
+    return t
+
+
+def zeros_tensor_from_numpy(shape, backend=None):
+    return zeros(shape, backend=backend)
+
+
+def ones_tensor_from_numpy(shape, backend=None):
+    return ones(shape, backend=backend)
+
+
+# ---- gradient checking ------------------------------------------------------------------
+def grad_central_difference(f: Any, *vals, arg: int = 0, epsilon: float = 1e-6, ind=None) -> float:
+    x = vals[arg]
+    up = np.zeros(x.shape, dtype=np.float64)
+    up[ind] = epsilon
+    vals1 = [x if j != arg else x + tensor_from_numpy(up, x.backend) for j, x in enumerate(vals)]
+    vals2 = [x if j != arg else x - tensor_from_numpy(up, x.backend) for j, x in enumerate(vals)]
+    delta = f(*vals1).sum() - f(*vals2).sum()
+    return delta[0] / (2.0 * epsilon)
+
+
+def grad_check(f: Any, *vals, tol: float = 1e-6) -> None:
+    for x in vals:
+        x.requires_grad_(True)
+        x.zero_grad_()
+    random.seed(10)
+    out = f(*vals)
+    out.sum().backward()
+    for i, x in enumerate(vals):
+        ind = x._tensor.sample()
+        check = grad_central_difference(f, *vals, arg=i, ind=ind)
+        assert x.grad is not None
+        np.testing.assert_allclose(x.grad[ind], check, 1e-2, 1e-2)

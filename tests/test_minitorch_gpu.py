@@ -1,0 +1,240 @@
+"""minitorch on the HIP backend (``TensorBackend(HipKernelOps)``), on an MI355X.
+
+Mirrors the reference's tests: MultiHeadAttention vs ``torch.nn.MultiheadAttention`` at
+atol = rtol = 1e-5 (reference tests/test_flash_attention.py:24-186, same weight
+injection recipe, same ``result.sum().backward()`` upstream), the companion kernels at
+the reference's kernel_tests tolerances (softmax fw 1e-3, bw 1e-2/1e-3; LayerNorm fw
+1e-2/1e-3, bw 1e-3/1e-2), plus the generic map/zip/reduce/matmul ops.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mt():
+    import torch
+    assert torch.cuda.is_available(), "needs an MI355X"
+    import minitorch
+    from minitorch import _hip
+    _hip.lib()  # fail loudly if the HIP library is missing
+    return minitorch, minitorch.TensorBackend(minitorch.HipKernelOps)
+
+
+def test_generic_ops(mt):
+    minitorch, B = mt
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((3, 4, 5)).astype(np.float32)
+    y = rng.standard_normal((4, 1)).astype(np.float32) + 3.0
+    a, b = minitorch.tensor_from_numpy(x, B), minitorch.tensor_from_numpy(y, B)
+    np.testing.assert_allclose((a + b).to_numpy(), x + y, rtol=1e-6)
+    np.testing.assert_allclose((a * b).to_numpy(), x * y, rtol=1e-6)
+    np.testing.assert_allclose((a / b).to_numpy(), x / y, rtol=1e-6)
+    np.testing.assert_allclose(a.exp().to_numpy(), np.exp(x), rtol=1e-6)
+    np.testing.assert_allclose(a.relu().to_numpy(), np.maximum(x, 0))
+    np.testing.assert_allclose((a < b).to_numpy(), (x < y).astype(np.float32))
+    np.testing.assert_allclose(a.sigmoid().to_numpy(), 1 / (1 + np.exp(-x)), rtol=1e-6)
+    np.testing.assert_allclose(a.tanh().to_numpy(), np.tanh(x), rtol=1e-5, atol=1e-6)
+    for dim in range(3):
+        np.testing.assert_allclose(a.sum(dim).to_numpy(), x.sum(dim, keepdims=True), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(minitorch.max(a, dim).to_numpy(), x.max(dim, keepdims=True))
+    big = rng.standard_normal((7, 1000)).astype(np.float32)  # wave-per-row reduce path
+    g = minitorch.tensor_from_numpy(big, B)
+    np.testing.assert_allclose(g.sum(1).to_numpy(), big.sum(1, keepdims=True), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(minitorch.max(g, 1).to_numpy(), big.max(1, keepdims=True))
+    p = a.permute(2, 0, 1)
+    np.testing.assert_allclose(p.contiguous().to_numpy(), x.transpose(2, 0, 1))
+
+
+@pytest.mark.parametrize("shapes", [((5, 7), (7, 3)), ((4, 33, 65), (4, 65, 70)),
+                                    ((2, 3, 17, 8), (2, 3, 8, 40)), ((1, 64, 96), (3, 96, 5))])
+def test_matmul(mt, shapes):
+    minitorch, B = mt
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal(shapes[0]).astype(np.float32)
+    w = rng.standard_normal(shapes[1]).astype(np.float32)
+    out = minitorch.tensor_from_numpy(x, B) @ minitorch.tensor_from_numpy(w, B)
+    ref = np.matmul(x.astype(np.float64), w.astype(np.float64))
+    np.testing.assert_allclose(out.to_numpy(), ref, rtol=1e-5, atol=1e-5)
+    # transposed (strided) operand
+    xt = minitorch.tensor_from_numpy(np.ascontiguousarray(np.swapaxes(x, -1, -2)), B)
+    order = list(range(xt.dims))
+    order[-1], order[-2] = order[-2], order[-1]
+    out2 = xt.permute(*order) @ minitorch.tensor_from_numpy(w, B)
+    np.testing.assert_allclose(out2.to_numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+def _mha_case(minitorch, backend, batch_size, queries_len, n_embd, num_heads, causal, use_flash,
+              use_fused=False):
+    import torch
+    np.random.seed(10)
+    torch.manual_seed(10)
+    data = np.random.rand(batch_size, queries_len, n_embd)
+    X = minitorch.tensor_from_numpy(data, backend, True)
+    X_ = torch.tensor(data, dtype=torch.float32, requires_grad=True, device="cuda")
+    layer_ = torch.nn.MultiheadAttention(n_embd, num_heads, 0.0, bias=False, batch_first=True,
+                                         dtype=torch.float32, device="cuda")
+    layer = minitorch.MultiHeadAttention(n_embd, num_heads, causal, 0.0, bias=False, backend=backend,
+                                         use_fused_kernel=use_fused, use_flash_attention=use_flash)
+    w_qkv = layer_.in_proj_weight.detach().cpu().numpy().T.copy()
+    for name, w in zip(("q_projection", "k_projection", "v_projection"), np.split(w_qkv, 3, -1)):
+        getattr(layer, name).weights.value = minitorch.tensor_from_numpy(w.copy(), backend, True)
+    layer.out_projection.weights.value = minitorch.tensor_from_numpy(
+        layer_.out_proj.weight.detach().cpu().numpy().T.copy(), backend, True)
+    M = torch.triu(-float("inf") * torch.ones(queries_len, queries_len, device="cuda"), 1) if causal else None
+    result = layer(X)
+    result_, _ = layer_(X_, X_, X_, attn_mask=M, need_weights=False)
+    np.testing.assert_allclose(result.to_numpy(), result_.detach().cpu().numpy(), atol=1e-5, rtol=1e-5)
+    result.sum().backward()
+    result_.sum().backward()
+    np.testing.assert_allclose(X.grad.to_numpy(), X_.grad.detach().cpu().numpy(), atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(layer.out_projection.weights.value.grad.to_numpy(),
+                               layer_.out_proj.weight.grad.detach().cpu().numpy().T, atol=1e-5, rtol=1e-5)
+    assert all(getattr(layer, n).weights.value.grad is not None
+               for n in ("q_projection", "k_projection", "v_projection"))
+
+
+# A slice of the reference grid (batch 64, N in 2^7..2^12, E in 2^6..2^11, heads 2..16,
+# tests/test_flash_attention.py:24-27,103-106), sized for one test process.
+MHA_GRID = [
+    (8, 128, 64, 2), (8, 128, 256, 4), (4, 512, 512, 8), (2, 1024, 1024, 16),
+    (2, 256, 2048, 4), (1, 2048, 128, 2), (3, 100, 96, 4),
+]
+
+
+@pytest.mark.parametrize("batch_size,queries_len,n_embd,num_heads", MHA_GRID)
+@pytest.mark.parametrize("causal", [False, True])
+def test_multihead_attention_flash(mt, batch_size, queries_len, n_embd, num_heads, causal):
+    minitorch, B = mt
+    _mha_case(minitorch, B, batch_size, queries_len, n_embd, num_heads, causal, use_flash=True)
+
+
+@pytest.mark.parametrize("branch", ["plain", "fused"])
+@pytest.mark.parametrize("causal", [False, True])
+def test_multihead_attention_other_branches(mt, branch, causal):
+    minitorch, B = mt
+    _mha_case(minitorch, B, 4, 96, 64, 4, causal, use_flash=False, use_fused=(branch == "fused"))
+
+
+def test_attn_softmax_kernel(mt):
+    minitorch, B = mt
+    rng = np.random.default_rng(2)
+    for (b, h, f, tl) in [(2, 4, 33, 33), (1, 2, 64, 1500), (3, 1, 5, 7)]:
+        x = rng.standard_normal((b, h, f, tl)).astype(np.float32)
+        mask = (rng.random((b, 1, 1, tl)) < 0.2).astype(np.float32) * -1e4
+        xt = minitorch.tensor_from_numpy(x, B, True)
+        y = xt.attn_softmax(minitorch.tensor_from_numpy(mask, B))
+        z = x + mask
+        e = np.exp(z - z.max(-1, keepdims=True))
+        ref = e / (e.sum(-1, keepdims=True) + 1e-8)
+        np.testing.assert_allclose(y.to_numpy(), ref, atol=1e-3, rtol=1e-3)
+        dy = rng.standard_normal(x.shape).astype(np.float32)
+        (y * minitorch.tensor_from_numpy(dy, B)).sum().backward()
+        dref = ref * (dy - (dy * ref).sum(-1, keepdims=True))
+        np.testing.assert_allclose(xt.grad.to_numpy(), dref, atol=1e-2, rtol=1e-3)
+        # causal: future masked inside the kernel
+        yc = minitorch.tensor_from_numpy(x, B).attn_softmax(None, mask_future=True).to_numpy()
+        zc = np.where(np.triu(np.ones((f, tl)), 1) > 0, -1e8, x)
+        ec = np.exp(zc - zc.max(-1, keepdims=True))
+        np.testing.assert_allclose(yc, ec / (ec.sum(-1, keepdims=True) + 1e-8), atol=1e-3, rtol=1e-3)
+
+
+def test_layernorm_kernel(mt):
+    minitorch, B = mt
+    rng = np.random.default_rng(3)
+    for rows, H in [(64, 256), (999, 32), (7, 1026)]:
+        x = rng.standard_normal((rows, H)).astype(np.float32) * 2 + 0.5
+        g = rng.standard_normal(H).astype(np.float32)
+        bb = rng.standard_normal(H).astype(np.float32)
+        xt = minitorch.tensor_from_numpy(x, B, True)
+        gt = minitorch.tensor_from_numpy(g, B, True)
+        bt = minitorch.tensor_from_numpy(bb, B, True)
+        y = xt.layernorm(gt, bt)
+        x64 = x.astype(np.float64)
+        mu = x64.mean(-1, keepdims=True)
+        var = (x64 * x64).mean(-1, keepdims=True) - mu ** 2 + 1e-8
+        xh = (x64 - mu) / np.sqrt(var)
+        np.testing.assert_allclose(y.to_numpy(), g * xh + bb, atol=1e-2, rtol=1e-3)
+        dy = rng.standard_normal(x.shape)
+        (y * minitorch.tensor_from_numpy(dy, B)).sum().backward()
+        dyg = dy * g
+        dx = (dyg - dyg.mean(-1, keepdims=True) - xh * (dyg * xh).mean(-1, keepdims=True)) / np.sqrt(var)
+        np.testing.assert_allclose(xt.grad.to_numpy(), dx, atol=1e-3, rtol=1e-2)
+        np.testing.assert_allclose(gt.grad.to_numpy(), (dy * xh).sum(0), atol=1e-3, rtol=1e-2)
+        np.testing.assert_allclose(bt.grad.to_numpy(), dy.sum(0), atol=1e-3, rtol=1e-2)
+
+
+def test_reference_host_wrappers(mt):
+    """The reference's extern "C" names with host pointers (combine.cu, softmax_kernel.cu,
+    layernorm_kernel.cu)."""
+    from minitorch import _hip
+    lib = _hip.lib()
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    ip = lambda a: np.ascontiguousarray(a, np.int32).ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    rng = np.random.default_rng(4)
+    # tensorZip: broadcast add
+    a = rng.standard_normal((3, 4)).astype(np.float32)
+    b = rng.standard_normal((1, 4)).astype(np.float32)
+    out = np.zeros((3, 4), np.float32)
+    shp, st = np.array([3, 4], np.int32), np.array([4, 1], np.int32)
+    lib.tensorZip(fp(out), ip(shp), ip(st), 12, 2, fp(a), ip(shp), ip(st), 12, 2,
+                  fp(b), ip([1, 4]), ip([4, 1]), 4, 2, 1)
+    np.testing.assert_allclose(out, a + b, rtol=1e-6)
+    # tensorMap: exp
+    lib.tensorMap(fp(out), ip(shp), ip(st), 12, fp(a), ip(shp), ip(st), 12, 2, 12)
+    np.testing.assert_allclose(out, np.exp(a), rtol=1e-6)
+    # tensorReduce: sum over dim 1
+    r = np.zeros((3, 1), np.float32)
+    lib.tensorReduce(fp(r), ip([3, 1]), ip([1, 1]), 3, fp(a), ip(shp), ip(st), 1, ctypes.c_float(0.0), 2, 1)
+    np.testing.assert_allclose(r, a.sum(1, keepdims=True), rtol=1e-5, atol=1e-6)
+    # MatrixMultiply: [2,3,4] @ [2,4,5]
+    x = rng.standard_normal((2, 3, 4)).astype(np.float32)
+    w = rng.standard_normal((2, 4, 5)).astype(np.float32)
+    o = np.zeros((2, 3, 5), np.float32)
+    lib.MatrixMultiply(fp(o), ip([2, 3, 5]), ip([15, 5, 1]), fp(x), ip([2, 3, 4]), ip([12, 4, 1]),
+                       fp(w), ip([2, 4, 5]), ip([20, 5, 1]), 2, 3, 5)
+    np.testing.assert_allclose(o, x @ w, rtol=1e-5, atol=1e-5)
+    # launch_attn_softmax with a [B, to] padding mask, in place
+    s = rng.standard_normal((2, 3, 4, 6)).astype(np.float32)
+    m = np.zeros((2, 6), np.float32)
+    m[:, -2:] = -1e8
+    s2 = s.copy()
+    lib.launch_attn_softmax(fp(s2), fp(m), 2, 3, 4, 6, False, None)
+    z = s + m[:, None, None, :]
+    e = np.exp(z - z.max(-1, keepdims=True))
+    np.testing.assert_allclose(s2, e / (e.sum(-1, keepdims=True) + 1e-8), atol=1e-6)
+    # launch_layernorm
+    xl = rng.standard_normal((5, 8)).astype(np.float32)
+    g, bb = np.ones(8, np.float32), np.zeros(8, np.float32)
+    ln, var, mean = np.zeros_like(xl), np.zeros(5, np.float32), np.zeros(5, np.float32)
+    lib.launch_layernorm(fp(ln), fp(var), fp(mean), fp(xl), fp(g), fp(bb), 5, 8, None)
+    mu = xl.mean(-1, keepdims=True)
+    np.testing.assert_allclose(ln, (xl - mu) / np.sqrt(xl.var(-1, keepdims=True) + 1e-8), atol=1e-4)
+
+
+def test_decoder_lm_training_step(mt):
+    """BASELINE config 5 shape (n_vocab 10000, n_embd 256, n_head 8, batch 128, seq 39;
+    reference project/run_machine_translation.py:397-407) on synthetic tokens, with the fused
+    HIP LayerNorm + flash attention; the loss must go down over a few Adam steps."""
+    minitorch, B = mt
+    rng = np.random.default_rng(5)
+    lm = minitorch.DecoderLM(n_vocab=10000, n_embd=256, n_head=8, n_positions=40, p_dropout=0.0,
+                             backend=B, use_fused_kernel=True, use_flash_attention=True)
+    opt = minitorch.Adam(lm.parameters(), lr=1e-3)
+    idx = rng.integers(0, 10000, (128, 39)).astype(np.float32)
+    tgt = rng.integers(0, 10000, (128 * 39,)).astype(np.float32)
+    x = minitorch.tensor_from_numpy(idx, B)
+    y = minitorch.tensor_from_numpy(tgt, B)
+    losses = []
+    for _ in range(3):
+        opt.zero_grad()
+        logits = lm(x)
+        loss = minitorch.softmax_loss(logits.view(128 * 39, 10000), y).sum() / (128 * 39)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert np.isfinite(losses).all()
+    assert losses[-1] < losses[0], losses
