@@ -47,6 +47,10 @@ def _ptr(t: Tensor) -> int:
     return _dev(t)._tensor.data_ptr()
 
 
+def _dense(t: Tensor) -> Tensor:
+    return t if t._tensor.is_dense() else t.contiguous()
+
+
 def _stream() -> int:
     return _hip.stream_ptr()
 
@@ -200,11 +204,12 @@ class HipKernelOps(TensorOps):
     def layernorm_fw(inp: Tensor, gamma: Tensor, beta: Tensor):
         x = inp if inp._tensor.is_dense() else inp.contiguous()
         rows, H = x.shape
+        gm, bt = _dense(gamma), _dense(beta)  # held: their device buffers must outlive the launch
         ln = x.zeros(x.shape)
         var = x.zeros((rows,))
         mean = x.zeros((rows,))
         _hip.check(_hip.lib().mt_layernorm_fw(_ptr(ln), _ptr(var), _ptr(mean), _ptr(x),
-                                              _ptr(gamma.contiguous()), _ptr(beta.contiguous()),
+                                              _ptr(gm), _ptr(bt),
                                               rows, H, _stream()), "layernorm_fw")
         return ln, var, mean
 
@@ -215,13 +220,14 @@ class HipKernelOps(TensorOps):
         g = out_grad if out_grad._tensor.is_dense() else out_grad.contiguous()
         x = inp if inp._tensor.is_dense() else inp.contiguous()
         rows, H = x.shape
+        gm, bt = _dense(gamma), _dense(beta)
         dx = x.zeros(x.shape)
         dgamma = x.zeros((1, H))
         dbeta = x.zeros((1, H))
         ws = torch.empty(max(1, _hip.lib().mt_layernorm_bw_workspace_bytes(rows, H) // 4),
                          dtype=torch.float32, device="cuda")
         _hip.check(_hip.lib().mt_layernorm_bw(_ptr(dgamma), _ptr(dbeta), _ptr(dx), _ptr(g), _ptr(x),
-                                              _ptr(gamma.contiguous()), _ptr(beta.contiguous()),
+                                              _ptr(gm), _ptr(bt),
                                               _ptr(var), _ptr(mean), rows, H, ws.data_ptr(),
                                               _stream()), "layernorm_bw")
         return dx, dgamma, dbeta

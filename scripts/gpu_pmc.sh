@@ -1,16 +1,25 @@
-# PMC counter passes on the forward kernel (one rocprofv3 --pmc pass per group).
+# PMC counter passes on the forward kernel (one rocprofv3 --pmc pass per group, kernel
+# trace only: never combined with sys/runtime tracing).
+# Env: POL (kernel policy, default 0), TAG (output tag), CAUSAL=1 for the causal leg,
+#      PMC_GROUPS=all|traffic (traffic = FETCH_SIZE and WRITE_SIZE passes only).
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-POL=${POL:-2}
+POL=${POL:-0}
 TAG=${TAG:-p$POL}
-rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
+EXTRA=""
+[ "${CAUSAL:-0}" = "1" ] && EXTRA="--causal"
+if [ "${PMC_GROUPS:-all}" = "traffic" ]; then
+  set -- "FETCH_SIZE" "WRITE_SIZE"
+else
+  set -- "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+         "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS" \
+         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM" \
+         "FETCH_SIZE" "WRITE_SIZE"
+fi
 i=0
-for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS" \
-           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM" \
-           "FETCH_SIZE" "WRITE_SIZE"; do
+for grp in "$@"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace --kernel-include-regex fa_fwd -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extra --policy $POL > gpurun_out/pmc_${TAG}_$i.log 2>&1 || echo "group $i failed"
+  timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace --kernel-include-regex fa_fwd -d gpurun_out/pmc_${TAG}_$i -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extra --policy $POL $EXTRA > gpurun_out/pmc_${TAG}_$i.log 2>&1 || { echo "group $i failed"; exit 1; }
 done
 python3 scripts/pmc_summary.py gpurun_out/pmc_${TAG}_* > gpurun_out/pmc_${TAG}_summary.txt 2>&1
 cat gpurun_out/pmc_${TAG}_summary.txt

@@ -1,0 +1,94 @@
+"""World-size-2 ``gloo`` tests of the B*H sharding + output all-gather (minitorch/shard.py)
+on CPU. The per-shard attention is the CPU oracle here (test infrastructure); on the GPU
+box the same code calls the HIP kernels with backend "nccl" (RCCL)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from minitorch.shard import bh_range, shard
+
+
+def test_bh_range_partition():
+    for bh in (1, 3, 7, 128, 1024):
+        for world in (1, 2, 3, 4, 8):
+            spans = [bh_range(bh, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == bh
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1
+    t = torch.arange(2 * 3 * 4 * 5, dtype=torch.float32).reshape(2, 3, 4, 5)
+    s = shard(t, 2, 1)
+    assert s.shape == (3, 4, 5) and s.data_ptr() == t.reshape(6, 4, 5)[3].data_ptr()
+
+
+def _oracle_fwd(q, k, v, causal):
+    from oracle import attention as A
+    o, m, l = A.attention_fwd(q.numpy(), k.numpy(), v.numpy(), causal)
+    return torch.from_numpy(o), torch.from_numpy(m), torch.from_numpy(l)
+
+
+def _oracle_bwd(q, k, v, o, do, m, l, causal):
+    from oracle import attention as A
+    g = A.attention_bwd(*(t.numpy() for t in (q, k, v, o, do, m, l)), causal)
+    return tuple(torch.from_numpy(np.ascontiguousarray(x)) for x in g)
+
+
+def _worker(rank, world, port, shape, causal, errq):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "llmsys-project-flashattn_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from minitorch.shard import sharded_flash_bwd, sharded_flash_fwd
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        g = torch.Generator().manual_seed(0)
+        q, k, v, do = (torch.randn(shape, generator=g) for _ in range(4))
+        o, m, l = sharded_flash_fwd(q, k, v, causal, attn=_oracle_fwd)
+        ro, rm, rl = _oracle_fwd(q.reshape(-1, *shape[2:]), k.reshape(-1, *shape[2:]),
+                                 v.reshape(-1, *shape[2:]), causal)
+        np.testing.assert_allclose(o.reshape(ro.shape).numpy(), ro.numpy(), atol=1e-6)
+        np.testing.assert_allclose(m.reshape(rm.shape).numpy(), rm.numpy(), atol=1e-6)
+        dq, dk, dv = sharded_flash_bwd(q, k, v, o, do, m, l, causal, attn_bwd=_oracle_bwd)
+        flat = lambda t: t.reshape(-1, *t.shape[2:])
+        ref = _oracle_bwd(flat(q), flat(k), flat(v), flat(o), flat(do), flat(m), flat(l), causal)
+        for got, want in zip((dq, dk, dv), ref):
+            np.testing.assert_allclose(flat(got).numpy(), want.numpy(), atol=1e-5)
+        # without gather: this rank's rows only
+        os_, _, _ = sharded_flash_fwd(q, k, v, causal, gather=False, attn=_oracle_fwd)
+        lo, hi = bh_range(shape[0] * shape[1], world, rank)
+        np.testing.assert_allclose(os_.numpy(), ro[lo:hi].numpy(), atol=1e-6)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surfaced to the parent
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("shape,causal", [((2, 2, 48, 16), False), ((1, 3, 33, 8), True)])
+def test_sharded_fwd_bwd_gloo_world2(shape, causal):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, shape, causal, errq)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
