@@ -16,6 +16,10 @@ hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
                               hipStream_t st);
 hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStream_t st,
                            bool* handled);
+hipError_t launch_fwd_v2(const AttnArgs& a, bool causal, int nw, int resc, hipStream_t st,
+                         bool* handled);
+hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int nw, bool sched, hipStream_t st,
+                         bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
 
@@ -99,7 +103,14 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
   hipStream_t st = (hipStream_t)stream;
   if (dtype == MT_BF16 && vec && g_kernel_policy != 1) {
     bool handled = false;
-    hipError_t e = launch_fwd_fast(a, causal != 0, g_kernel_policy, st, &handled);
+    hipError_t e = hipSuccess;
+    if (g_kernel_policy >= 7 && g_kernel_policy <= 9)
+      e = launch_fwd_v2(a, causal != 0, g_kernel_policy == 8 ? 8 : 4, g_kernel_policy == 9, st,
+                        &handled);
+    if (g_kernel_policy >= 16 && g_kernel_policy <= 18)
+      e = launch_fwd_v3(a, causal != 0, g_kernel_policy == 17 ? 8 : 4, g_kernel_policy != 18, st,
+                        &handled);
+    if (!handled) e = launch_fwd_fast(a, causal != 0, g_kernel_policy, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");
   }
   return check_hip(launch_fwd_generic(a, dtype == MT_BF16, vec, causal != 0, st),

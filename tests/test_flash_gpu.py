@@ -242,7 +242,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
                for _ in range(3))
     outs = []
     try:
-        for pol in (0, 2, 4, 5, 6, 1):
+        for pol in FAST_POLICIES + (1,):
             _hip.lib().mt_flash_set_kernel_policy(pol)
             o, m, l = _hip.flash_fwd(q, k, v, causal)
             torch.cuda.synchronize()
@@ -254,7 +254,36 @@ def test_kernel_variants_agree(torch_dev, causal, d):
         assert float((lse - outs[0][1]).abs().max()) < 2e-3
 
 
-def test_spiked_rescale(torch_dev):
+# kernel policies of the bf16 fast forward (mt_flash_set_kernel_policy): 0 default,
+# 2 single-phase 8-wave, 4/5 software-pipelined, 6 ping-pong, 7/8/9 v2 (fa_fwd_v2.hip),
+# 16/17/18 v3 (fa_fwd_v3.hip: 4-wave scheduled, 8-wave scheduled, 4-wave unscheduled)
+FAST_POLICIES = (0, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18)
+
+
+@pytest.mark.parametrize("policy", FAST_POLICIES)
+def test_fast_policies_vs_oracle(torch_dev, policy):
+    """Each bf16 forward variant against the oracle on the same bf16 inputs: ragged N,
+    both mask modes, head dims 64 and 128 (variants without a d=128 form fall back)."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(31)
+    try:
+        _hip.lib().mt_flash_set_kernel_policy(policy)
+        for (B, H, N, d) in ((1, 3, 1000, 64), (2, 1, 517, 128), (1, 2, 64, 64)):
+            q, k, v = (A.bf16_round(rng.standard_normal((B, H, N, d)).astype(np.float32))
+                       for _ in range(3))
+            for causal in (False, True):
+                o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
+                o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), causal)
+                torch.cuda.synchronize()
+                np.testing.assert_allclose(_np(o), o_ref, atol=2e-2, err_msg=f"{(B, H, N, d, causal)}")
+                _check_ml(_np(m), _np(l), m_ref, l_ref, exact=False)
+    finally:
+        _hip.lib().mt_flash_set_kernel_policy(0)
+
+
+@pytest.mark.parametrize("policy", FAST_POLICIES)
+def test_spiked_rescale(torch_dev, policy):
     """Force the deferred-rescale branch (rule: a rare data-dependent branch needs its own
     test): one key row aligned with one query row makes that row's max jump past the
     2^8 threshold at a chosen tile, after several tiles at a low max."""
@@ -268,9 +297,13 @@ def test_spiked_rescale(torch_dev):
     for row, key in ((5, 600), (300, 130), (699, 450)):
         k[:, :, key] = q[:, :, row] * 12.0
     q, k, v = (A.bf16_round(x) for x in (q, k, v))
-    for causal in (False, True):
-        o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
-        o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), causal)
-        torch.cuda.synchronize()
-        np.testing.assert_allclose(_np(o), o_ref, atol=2e-2)
-        _check_ml(_np(m), _np(l), m_ref, l_ref, exact=False)
+    try:
+        _hip.lib().mt_flash_set_kernel_policy(policy)
+        for causal in (False, True):
+            o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
+            o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), causal)
+            torch.cuda.synchronize()
+            np.testing.assert_allclose(_np(o), o_ref, atol=2e-2)
+            _check_ml(_np(m), _np(l), m_ref, l_ref, exact=False)
+    finally:
+        _hip.lib().mt_flash_set_kernel_policy(0)
