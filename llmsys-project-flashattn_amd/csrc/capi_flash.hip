@@ -18,14 +18,15 @@ hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStrea
                            bool* handled);
 hipError_t launch_fwd_v2(const AttnArgs& a, bool causal, int nw, int resc, hipStream_t st,
                          bool* handled);
-hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int nw, bool sched, hipStream_t st,
-                         bool* handled);
+hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
+hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
 
 static thread_local char g_err[512] = "";
-static int g_kernel_policy = 0;  // 0: default bf16 MFMA kernel, 1: generic kernels only,
-                                 // other values: A/B variants (fa_fwd_fast.hip)
+static int g_kernel_policy = 0;  // 0: default bf16 MFMA kernels, 1: generic kernels only,
+                                 // other values: A/B variants (fa_fwd_fast/v2/v3/v4.hip,
+                                 // listed in tests/test_flash_gpu.py FAST_POLICIES)
 
 int set_error(const char* fmt, ...) {
   va_list ap;
@@ -107,9 +108,13 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
     if (g_kernel_policy >= 7 && g_kernel_policy <= 9)
       e = launch_fwd_v2(a, causal != 0, g_kernel_policy == 8 ? 8 : 4, g_kernel_policy == 9, st,
                         &handled);
-    if (g_kernel_policy >= 16 && g_kernel_policy <= 18)
-      e = launch_fwd_v3(a, causal != 0, g_kernel_policy == 17 ? 8 : 4, g_kernel_policy != 18, st,
-                        &handled);
+    if (g_kernel_policy >= 16 && g_kernel_policy <= 20)
+      e = launch_fwd_v3(a, causal != 0, g_kernel_policy - 16, st, &handled);
+    if (g_kernel_policy == 21 || g_kernel_policy == 22)
+      e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 22 ? 8 : 4, st, &handled);
+    // default: v4 at d = 64 (8 waves; 4 for causal, whose diagonal blocks finish unevenly),
+    // the single-phase 4-wave kernel otherwise (d = 128)
+    if (g_kernel_policy == 0) e = launch_fwd_v4(a, causal != 0, causal ? 4 : 8, st, &handled);
     if (!handled) e = launch_fwd_fast(a, causal != 0, g_kernel_policy, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");
   }

@@ -58,20 +58,30 @@ __device__ __forceinline__ void v3_qk(const bf16* smem, const Ctx& c, const bf16
 // bf16 P fragments (B operands of PV) of one 32-key block: p = exp2(s*c2 - m*c2); the
 // fp32 p also go into the lane's partial row sum (the two lane halves hold different
 // keys of the same query and are combined once, at the end).
+template <bool LM>
 __device__ __forceinline__ void v3_exp(const f32x16& s, float c2, float nmc, bf16x8& p0, bf16x8& p1,
                                        float& l) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j], c2, nmc));
-    l += e;
+    if (!LM) l += e;
     p0[j] = (bf16)e;
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(s[8 + j], c2, nmc));
-    l += e;
+    if (!LM) l += e;
     p1[j] = (bf16)e;
   }
+}
+
+// Row sum on the matrix pipe: L += 1·Pᵀ (every row of L holds the sum; 4 MFMAs a tile
+// instead of 32 VALU adds).
+__device__ __forceinline__ void v3_lsum(f32x16& L, const bf16x8& p) {
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p, L, 0, 0, 0);
 }
 
 // O += Vᵀ(key block kb of the tile in slot VS)·Pᵀ.
@@ -110,7 +120,7 @@ __device__ __forceinline__ void v3_mask(f32x16 (&S)[2], int k0, int N, int my_q,
 // Deferred-max online-softmax bookkeeping for one tile; returns -m*c2 for the exponent.
 template <int D>
 __device__ __forceinline__ float v3_max(const f32x16 (&S)[2], f32x16 (&O)[D / 32], float& l,
-                                        float& m_run, float c2) {
+                                        f32x16& L, float& m_run, float c2) {
   const float tmax = row_max32(S[0], S[1]);
   if (__builtin_amdgcn_ballot_w64((tmax - m_run) * c2 > kThr)) {
     const float m_new = fmaxf(m_run, tmax);
@@ -121,6 +131,8 @@ __device__ __forceinline__ float v3_max(const f32x16 (&S)[2], f32x16 (&O)[D / 32
 #pragma unroll
       for (int r = 0; r < 16; ++r) O[i][r] *= alpha;
     l *= alpha;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) L[r] *= alpha;
   }
   return -(m_run * c2);
 }
@@ -144,10 +156,10 @@ __device__ __forceinline__ void v3_store(bf16* dst, const uint4 (&r)[4], const i
 //   8 x [K read (2 ahead), QKᵀ(t+1) MFMA, exp(t) slice: 2 keys of block 0]
 //   4 x [Vᵀ reads, PV(t, block 0) MFMA, exp(t) slice: 4 keys of block 1]
 //   4 x [Vᵀ reads, PV(t, block 1) MFMA]
-template <int D, int NW, int KSN, int VS>
+template <int D, int NW, int KSN, int VS, bool LM>
 __device__ __forceinline__ void v3_bulk(const bf16* smem, const Ctx& c, const bf16x8 (&qf)[D / 16],
                                         const f32x16 (&SC)[2], f32x16 (&SN)[2], f32x16 (&O)[D / 32],
-                                        float& l, float c2, float nmc) {
+                                        float& l, f32x16& L, float c2, float nmc) {
   using C = V3<D, NW>;
   static_assert(C::KSTEPS == 4 && C::DB == 2, "d = 64 schedule");
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -168,7 +180,7 @@ __device__ __forceinline__ void v3_bulk(const bf16* smem, const Ctx& c, const bf
 #pragma unroll
     for (int j = 2 * i; j < 2 * i + 2; ++j) {
       const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(SC[0][j], c2, nmc));
-      l += e;
+      if (!LM) l += e;
       pf[j >> 3][j & 7] = (bf16)e;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -195,10 +207,11 @@ __device__ __forceinline__ void v3_bulk(const bf16* smem, const Ctx& c, const bf
   for (int n = 0; n < 4; ++n) {
     if (n + 2 < 4) V3_VREAD(0, n + 2)
     V3_PVMMA(n, pf[n >> 1])
+    if (LM && (n & 1)) v3_lsum(L, pf[n >> 1]);
 #pragma unroll
     for (int j = 4 * n; j < 4 * n + 4; ++j) {
       const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(SC[1][j], c2, nmc));
-      l += e;
+      if (!LM) l += e;
       pf[2 + (j >> 3)][j & 7] = (bf16)e;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -209,6 +222,7 @@ __device__ __forceinline__ void v3_bulk(const bf16* smem, const Ctx& c, const bf
   for (int n = 0; n < 4; ++n) {
     if (n + 2 < 4) V3_VREAD(1, n + 2)
     V3_PVMMA(n, pf[2 + (n >> 1)])
+    if (LM && (n & 1)) v3_lsum(L, pf[2 + (n >> 1)]);
   }
 #undef V3_VREAD
 #undef V3_PVMMA
@@ -216,7 +230,7 @@ __device__ __forceinline__ void v3_bulk(const bf16* smem, const Ctx& c, const bf
 
 }  // namespace
 
-template <int D, bool CAUSAL, int NW, bool SCHED>
+template <int D, bool CAUSAL, int NW, bool SCHED, bool LM>
 __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v3(AttnArgs p, int nqb) {
   using C = V3<D, NW>;
   static_assert(D == 64, "v3 is the d = 64 kernel");
@@ -289,7 +303,8 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v3(AttnArgs p, int nqb
   f32x16 O[C::DB];
 #pragma unroll
   for (int i = 0; i < C::DB; ++i) O[i] = f32x16{};
-  float l_part = 0.f;  // this lane's share of the row sum
+  float l_part = 0.f;  // this lane's share of the row sum (!LM)
+  f32x16 L = f32x16{};  // row sum on the matrix pipe (LM)
   float m_run = -INFINITY;
   const float c2 = p.scale_log2;
 
@@ -317,16 +332,17 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v3(AttnArgs p, int nqb
   {                                                                                        \
     v3_load<D, NW>(rK, rk, c.kgo, ((T_) + 2) * ktile_b);                                   \
     v3_load<D, NW>(rV, rv, c.vgo, ((T_) + 1) * vtile_b);                                   \
-    const float nmc = v3_max<D>(SC_, O, l_part, m_run, c2);                                \
+    const float nmc = v3_max<D>(SC_, O, l_part, L, m_run, c2);                                \
     if (SCHED) {                                                                           \
-      v3_bulk<D, NW, KSN_, VS_>(smem, c, qf, SC_, SN_, O, l_part, c2, nmc);                \
+      v3_bulk<D, NW, KSN_, VS_, LM>(smem, c, qf, SC_, SN_, O, l_part, L, c2, nmc);                \
     } else {                                                                               \
       bf16x8 p0, p1, p2, p3;                                                               \
       v3_qk<D, NW, KSN_>(smem, c, qf, SN_);                                                \
-      v3_exp(SC_[0], c2, nmc, p0, p1, l_part);                                             \
+      v3_exp<LM>(SC_[0], c2, nmc, p0, p1, l_part);                                         \
       v3_pv<D, NW, VS_, 0>(smem, c, p0, p1, O);                                            \
-      v3_exp(SC_[1], c2, nmc, p2, p3, l_part);                                             \
+      v3_exp<LM>(SC_[1], c2, nmc, p2, p3, l_part);                                         \
       v3_pv<D, NW, VS_, 1>(smem, c, p2, p3, O);                                            \
+      if (LM) { v3_lsum(L, p0); v3_lsum(L, p1); v3_lsum(L, p2); v3_lsum(L, p3); }          \
     }                                                                                      \
     v3_store<D, NW>((VS_) ? sK1 : sK0, rK, c.kso);                                         \
     v3_store<D, NW>((VS_) ? sV0 : sV1, rV, c.vso);                                         \
@@ -350,10 +366,11 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v3(AttnArgs p, int nqb
     if (next) v3_load<D, NW>(rV, rv, c.vgo, (t + 1) * vtile_b);
     if (!CAUSAL || t * kBK <= wq_hi) {
       if (t >= nfull) v3_mask<D, CAUSAL>(SA, t * kBK, N, my_q, hf);
-      const float nmc = v3_max<D>(SA, O, l_part, m_run, c2);
+      const float nmc = v3_max<D>(SA, O, l_part, L, m_run, c2);
       bf16x8 p0, p1, p2, p3;
-      v3_exp(SA[0], c2, nmc, p0, p1, l_part);
-      v3_exp(SA[1], c2, nmc, p2, p3, l_part);
+      v3_exp<LM>(SA[0], c2, nmc, p0, p1, l_part);
+      v3_exp<LM>(SA[1], c2, nmc, p2, p3, l_part);
+      if (LM) { v3_lsum(L, p0); v3_lsum(L, p1); v3_lsum(L, p2); v3_lsum(L, p3); }
       const bf16* sv = smem + (2 + par) * C::TILE;
       v3_pv<D, NW, 0, 0>(sv - 2 * C::TILE, c, p0, p1, O);
       v3_pv<D, NW, 0, 1>(sv - 2 * C::TILE, c, p2, p3, O);
@@ -365,9 +382,14 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v3(AttnArgs p, int nqb
     __syncthreads();
   }
 
-  const auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_part), __float_as_uint(l_part),
-                                                    false, false);
-  const float l_tot = __uint_as_float(lsw[0]) + __uint_as_float(lsw[1]);
+  float l_tot;
+  if (LM) {
+    l_tot = L[0];
+  } else {
+    const auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_part), __float_as_uint(l_part),
+                                                      false, false);
+    l_tot = __uint_as_float(lsw[0]) + __uint_as_float(lsw[1]);
+  }
   const float inv_l = 1.f / l_tot;
   if (my_q < N) {
     bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
@@ -385,10 +407,10 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v3(AttnArgs p, int nqb
   }
 }
 
-template <int D, bool CAUSAL, int NW, bool SCHED>
+template <int D, bool CAUSAL, int NW, bool SCHED, bool LM>
 static hipError_t launch_v3_t(const AttnArgs& a, hipStream_t st) {
   const size_t smem = 4 * (size_t)kBK * D * sizeof(bf16);
-  auto kfn = fa_fwd_bf16_v3<D, CAUSAL, NW, SCHED>;
+  auto kfn = fa_fwd_bf16_v3<D, CAUSAL, NW, SCHED, LM>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)smem);
   if (e != hipSuccess) return e;
@@ -401,7 +423,7 @@ static hipError_t launch_v3_t(const AttnArgs& a, hipStream_t st) {
 
 // d = 64 only; every per-head K/V byte offset up to two tiles past N must fit the 31-bit
 // buffer offset (the bulk loop stages one tile ahead of the last one it needs).
-hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int nw, bool sched, hipStream_t st,
+hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int variant, hipStream_t st,
                          bool* handled) {
   *handled = false;
   if (a.d != 64) return hipSuccess;
@@ -409,11 +431,17 @@ hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int nw, bool sched, hip
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
-  if (nw == 8)
-    return causal ? launch_v3_t<64, true, 8, true>(a, st) : launch_v3_t<64, false, 8, true>(a, st);
-  if (!sched)
-    return causal ? launch_v3_t<64, true, 4, false>(a, st) : launch_v3_t<64, false, 4, false>(a, st);
-  return causal ? launch_v3_t<64, true, 4, true>(a, st) : launch_v3_t<64, false, 4, true>(a, st);
+#define V3_DISPATCH(NW_, SCHED_, LM_)                                                   \
+  return causal ? launch_v3_t<64, true, NW_, SCHED_, LM_>(a, st)                       \
+                : launch_v3_t<64, false, NW_, SCHED_, LM_>(a, st);
+  switch (variant) {
+    case 0: V3_DISPATCH(4, true, false)
+    case 1: V3_DISPATCH(8, true, false)
+    case 2: V3_DISPATCH(4, false, false)
+    case 3: V3_DISPATCH(4, true, true)
+    default: V3_DISPATCH(8, true, true)
+  }
+#undef V3_DISPATCH
 }
 
 }  // namespace mt

@@ -1,0 +1,395 @@
+// FlashAttention forward, bf16 MFMA kernel v4 (d = 64): v3's software-pipelined loop with
+// a frozen softmax reference in the bulk tiles.
+//
+// Online softmax subtracts a running max only to keep exp() in range. v4 takes the row max
+// of the FIRST key tile as the reference m0 and, for every following mask-free tile,
+// computes p = exp2(s·c2 − m0·c2) with no tile max, no rescale test and no branch: the
+// bulk loop body is one basic block of MFMAs, exponentials and LDS traffic. Scores that
+// rise above m0 give p > 1; fp32 holds that exactly as long as p stays far from
+// overflow, so each lane's running sum is tested once after the loop: if any lane's
+// share of the row sum exceeds 2^64 (or is not finite), the whole workgroup recomputes
+// its block with the per-tile deferred-max path (general iterations from tile 0). The
+// masked tail tiles (ragged N, causal diagonal) always run the deferred-max path, which
+// continues from m0. The returned (m, l) satisfy the kernel contract P = exp(s − m)/l.
+#include "fa_fwd_bf16.h"
+
+namespace mt {
+
+namespace {
+
+using namespace fwdbf16;
+constexpr int kBK = 64;
+constexpr float kThr = 8.0f;             // log2 units: deferred-rescale threshold (general path)
+constexpr float kBulkLimit = 1.8446744e19f;  // 2^64: bound on a lane's row-sum share
+
+template <int NW>
+struct V4 {
+  static constexpr int D = 64;
+  static constexpr int kThreads = 64 * NW;
+  static constexpr int kBQ = 32 * NW;
+  static constexpr int CPR = D / 8;
+  static constexpr int LPT = kBK * CPR / kThreads;
+  static constexpr int RSTEP = kThreads / CPR;
+  static constexpr int TILE = kBK * D;
+};
+
+struct Ctx4 {
+  int koff[4];
+  int voff[2];
+  int kgo[2], vgo[2];
+  int kso[2], vso[2];
+};
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+// S = K(tile at sk)·Qᵀ (32 queries x 64 keys).
+__device__ __forceinline__ void qk4(const bf16* sk, const Ctx4& c, const bf16x8 (&qf)[4], f32x16 (&S)[2]) {
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const bf16x8 a = *(const bf16x8*)(sk + kb * 32 * 64 + c.koff[ks]);
+      S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], ks ? S[kb] : f32x16{}, 0, 0, 0);
+    }
+}
+
+// O += Vᵀ(key block KB of the tile at sv)·Pᵀ
+template <int KB>
+__device__ __forceinline__ void pv4(const bf16* sv, const Ctx4& c, const bf16x8& p0, const bf16x8& p1,
+                                    f32x16 (&O)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const bf16* a1 = sv + (KB * 32 + 16 * s) * 64 + c.voff[db];
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1 + 8 * 64));
+      const s16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      O[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av), s ? p1 : p0,
+                                                      O[db], 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void exp4(const f32x16& s, float c2, float nmc, bf16x8& p0, bf16x8& p1,
+                                     float& l) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j], c2, nmc));
+    l += e;
+    if (j < 8) p0[j] = (bf16)e;
+    else p1[j - 8] = (bf16)e;
+  }
+}
+
+template <bool CAUSAL>
+__device__ __forceinline__ void mask4(f32x16 (&S)[2], int k0, int N, int my_q, int hf) {
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = k0 + kb * 32 + acc_row(r, hf);
+      if (key >= N || (CAUSAL && key > my_q)) S[kb][r] = -INFINITY;
+    }
+}
+
+// Deferred-max bookkeeping of the general path; returns -m*c2.
+__device__ __forceinline__ float max4(const f32x16 (&S)[2], f32x16 (&O)[2], float& l, float& m_run,
+                                      float c2) {
+  const float tmax = row_max32(S[0], S[1]);
+  if (__builtin_amdgcn_ballot_w64((tmax - m_run) * c2 > kThr)) {
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m_run - m_new) * c2);
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) O[i][r] *= alpha;
+    l *= alpha;
+  }
+  return -(m_run * c2);
+}
+
+template <int NW>
+__device__ __forceinline__ void load4(uint4 (&r)[2], __amdgpu_buffer_rsrc_t rs, const int (&go)[2], int step) {
+#pragma unroll
+  for (int i = 0; i < V4<NW>::LPT; ++i)
+    r[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, go[i] + step, 0, 0));
+}
+
+template <int NW>
+__device__ __forceinline__ void store4x(bf16* dst, const uint4 (&r)[2], const int (&so)[2]) {
+#pragma unroll
+  for (int i = 0; i < V4<NW>::LPT; ++i) *(uint4*)(dst + so[i]) = r[i];
+}
+
+// One bulk iteration: QKᵀ(t+1) from sk ‖ exp(t) ; PV(t) from sv, in an explicit issue order
+// fenced by sched_barrier(0):
+//   8 x [K read (2 ahead), QKᵀ MFMA, 2 exponentials of key block 0]
+//   4 x [Vᵀ reads, PV MFMA (block 0), 4 exponentials of key block 1]
+//   4 x [Vᵀ reads, PV MFMA (block 1)]
+__device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4& c,
+                                      const bf16x8 (&qf)[4], const f32x16 (&SC)[2], f32x16 (&SN)[2],
+                                      f32x16 (&O)[2], float& l, float c2, float nmc) {
+  bf16x8 kf[8];
+  bf16x8 pf[4];
+#define V4_KREAD(I_) kf[I_] = *(const bf16x8*)(sk + ((I_) & 1) * 32 * 64 + c.koff[(I_) >> 1]);
+  V4_KREAD(0)
+  V4_KREAD(1)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i + 2 < 8) V4_KREAD(i + 2)
+    SN[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i >> 1], i < 2 ? f32x16{} : SN[i & 1],
+                                                       0, 0, 0);
+#pragma unroll
+    for (int j = 2 * i; j < 2 * i + 2; ++j) {
+      const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(SC[0][j], c2, nmc));
+      l += e;
+      pf[j >> 3][j & 7] = (bf16)e;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#undef V4_KREAD
+  s16x4 vlo[4], vhi[4];
+#define V4_VREAD(KB_, N_)                                                                  \
+  {                                                                                        \
+    const bf16* a1 = sv + ((KB_) * 32 + 16 * ((N_) >> 1)) * 64 + c.voff[(N_) & 1];         \
+    vlo[N_] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);                     \
+    vhi[N_] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1 + 8 * 64));          \
+  }
+#define V4_PVMMA(N_, PF_)                                                                  \
+  {                                                                                        \
+    const s16x8 av = {vlo[N_][0], vlo[N_][1], vlo[N_][2], vlo[N_][3],                      \
+                      vhi[N_][0], vhi[N_][1], vhi[N_][2], vhi[N_][3]};                     \
+    O[(N_) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av),  \
+                                                          PF_, O[(N_) & 1], 0, 0, 0);      \
+  }
+  V4_VREAD(0, 0)
+  V4_VREAD(0, 1)
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    if (n + 2 < 4) V4_VREAD(0, n + 2)
+    V4_PVMMA(n, pf[n >> 1])
+#pragma unroll
+    for (int j = 4 * n; j < 4 * n + 4; ++j) {
+      const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(SC[1][j], c2, nmc));
+      l += e;
+      pf[2 + (j >> 3)][j & 7] = (bf16)e;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  V4_VREAD(1, 0)
+  V4_VREAD(1, 1)
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    if (n + 2 < 4) V4_VREAD(1, n + 2)
+    V4_PVMMA(n, pf[2 + (n >> 1)])
+  }
+#undef V4_VREAD
+#undef V4_PVMMA
+}
+
+}  // namespace
+
+template <bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb) {
+  using C = V4<NW>;
+  constexpr int D = 64;
+  static_assert(C::LPT == 1 || C::LPT == 2, "staging layout");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* smem = (bf16*)smem_raw;  // K[2][TILE], V[2][TILE]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N;
+
+  const int nblk = gridDim.x;
+  const int hw = blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3;
+  const int qd = nblk >> 3, rm = nblk & 7;
+  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
+  const int bh = logical / nqb;
+  int qb = logical % nqb;
+  if (CAUSAL) qb = nqb - 1 - qb;  // heaviest first
+  const int b = bh / p.H, hh = bh % p.H;
+  const int q0 = qb * C::kBQ;
+
+  const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const int skn = (int)p.sk[2], svn = (int)p.sv[2];
+  const __amdgpu_buffer_rsrc_t rk =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Kg, (short)0, ((N - 1) * skn + D) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Vg, (short)0, ((N - 1) * svn + D) * 2, 0x00020000);
+
+  const int my_q = q0 + wave * 32 + c32;
+  const int wq_hi = q0 + wave * 32 + 31;
+
+  bf16x8 qf[4];
+  {
+    const int qr = min(my_q, N - 1);
+    const bf16* qrow = Qg + (int64_t)qr * p.sq[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const bf16x8*)(qrow + ks * 16 + 8 * hf);
+  }
+
+  Ctx4 c;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) c.koff[ks] = k_swz<D>(c32, 2 * ks + hf);
+  {
+    const int i16 = lane & 15, g = (lane >> 4) & 1;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int col = db * 32 + 16 * g + 4 * (i16 & 3);
+      c.voff[db] = v_swz<D>(4 * hf + (i16 >> 2), col >> 3) + (col & 7);
+    }
+  }
+  {
+    const int st_r = tid / C::CPR, st_c = tid % C::CPR;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = st_r + i * C::RSTEP;
+      c.kgo[i] = (r * skn + st_c * 8) * 2;
+      c.vgo[i] = (r * svn + st_c * 8) * 2;
+      c.kso[i] = k_swz<D>(r, st_c);
+      c.vso[i] = v_swz<D>(r, st_c);
+    }
+  }
+  const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
+  bf16* const sK0 = smem;
+  bf16* const sK1 = smem + C::TILE;
+  bf16* const sV0 = smem + 2 * C::TILE;
+  bf16* const sV1 = smem + 3 * C::TILE;
+
+  const float c2 = p.scale_log2;
+  const int kend = CAUSAL ? min(N, q0 + C::kBQ) : N;
+  const int ntiles = (kend + kBK - 1) / kBK;
+  const int nfull = CAUSAL ? min(N / kBK, q0 / kBK) : N / kBK;  // mask-free tiles
+
+  f32x16 O[2];
+  float l_part, m_run;
+  uint4 rK[2], rV[2];
+  f32x16 SA[2], SB[2];
+
+  // Pass 0: frozen-reference bulk loop. Pass 1 (only if a lane's row-sum share left the
+  // safe range): the whole workgroup recomputes with the deferred-max path throughout.
+  for (int pass = 0; pass < 2; ++pass) {
+    O[0] = f32x16{};
+    O[1] = f32x16{};
+    l_part = 0.f;
+    m_run = -INFINITY;
+    // Prologue: K(0), V(0) -> slot 0, K(1) -> slot 1; S(0).
+    load4<NW>(rK, rk, c.kgo, 0);
+    load4<NW>(rV, rv, c.vgo, 0);
+    store4x<NW>(sK0, rK, c.kso);
+    store4x<NW>(sV0, rV, c.vso);
+    load4<NW>(rK, rk, c.kgo, ktile_b);
+    store4x<NW>(sK1, rK, c.kso);
+    __syncthreads();
+    qk4(sK0, c, qf, SA);
+    __syncthreads();  // iteration 0 overwrites K slot 0, which every wave just read
+
+    // General iteration t (deferred max, masks, per-wave causal skipping); S(t) in SA,
+    // QK(t+1) after PV(t) into SA. LDS slots by runtime parity.
+#define V4_GENERAL(T_)                                                                       \
+  {                                                                                          \
+    const int t_ = (T_);                                                                     \
+    const int par = t_ & 1;                                                                  \
+    const bool next = t_ + 1 < ntiles;                                                       \
+    if (t_ + 2 < ntiles) load4<NW>(rK, rk, c.kgo, (t_ + 2) * ktile_b);                       \
+    if (next) load4<NW>(rV, rv, c.vgo, (t_ + 1) * vtile_b);                                  \
+    if (!CAUSAL || t_ * kBK <= wq_hi) {                                                      \
+      if (t_ >= nfull) mask4<CAUSAL>(SA, t_ * kBK, N, my_q, hf);                             \
+      const float nmc = max4(SA, O, l_part, m_run, c2);                                      \
+      bf16x8 p0, p1, p2, p3;                                                                 \
+      exp4(SA[0], c2, nmc, p0, p1, l_part);                                                  \
+      exp4(SA[1], c2, nmc, p2, p3, l_part);                                                  \
+      const bf16* sv = par ? sV1 : sV0;                                                      \
+      pv4<0>(sv, c, p0, p1, O);                                                              \
+      pv4<1>(sv, c, p2, p3, O);                                                              \
+    }                                                                                        \
+    if (next && (!CAUSAL || (t_ + 1) * kBK <= wq_hi)) qk4(par ? sK0 : sK1, c, qf, SA);       \
+    if (t_ + 2 < ntiles) store4x<NW>(par ? sK1 : sK0, rK, c.kso);                            \
+    if (next) store4x<NW>(par ? sV0 : sV1, rV, c.vso);                                       \
+    __syncthreads();                                                                         \
+  }
+
+    V4_GENERAL(0)  // tile 0 sets the reference max
+    int t = 1;
+    if (pass == 0) {
+      const float nmc = -(m_run * c2);
+      // Bulk iteration t (tiles t, t+1, t+2 mask-free and active for every wave). Staging
+      // of K(t+2) / V(t+1) is unconditional (past the end it reads zeros or unused rows
+      // into a slot nobody reads).
+#define V4_BULK(T_, SC_, SN_, SKN_, SVC_, SKW_, SVW_)                                       \
+  {                                                                                         \
+    load4<NW>(rK, rk, c.kgo, ((T_) + 2) * ktile_b);                                         \
+    load4<NW>(rV, rv, c.vgo, ((T_) + 1) * vtile_b);                                         \
+    bulk4(SKN_, SVC_, c, qf, SC_, SN_, O, l_part, c2, nmc);                                 \
+    store4x<NW>(SKW_, rK, c.kso);                                                           \
+    store4x<NW>(SVW_, rV, c.vso);                                                           \
+    __syncthreads();                                                                        \
+  }
+      // t odd: S(t) in SA, K(t+1) in slot 0, V(t) in slot 1; writes K(t+2) -> slot 1,
+      // V(t+1) -> slot 0. t+1 even: mirror.
+      for (; t + 2 < nfull; t += 2) {
+        V4_BULK(t, SA, SB, sK0, sV1, sK1, sV0)
+        V4_BULK(t + 1, SB, SA, sK1, sV0, sK0, sV1)
+      }
+#undef V4_BULK
+    }
+    for (; t < ntiles; ++t) V4_GENERAL(t)
+#undef V4_GENERAL
+    const bool bad = !(l_part <= kBulkLimit);
+    if (pass == 1 || !__syncthreads_or(bad)) break;
+  }
+
+  const auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_part), __float_as_uint(l_part),
+                                                    false, false);
+  const float l_tot = __uint_as_float(lsw[0]) + __uint_as_float(lsw[1]);
+  const float inv_l = 1.f / l_tot;
+  if (my_q < N) {
+    bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(Og + db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
+               O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l, true);
+    if (hf == 0) {
+      const int64_t row = (int64_t)bh * N + my_q;
+      if (p.m) p.m[row] = m_run * p.scale;
+      if (p.l) p.l[row] = l_tot;
+    }
+  }
+}
+
+template <bool CAUSAL, int NW>
+static hipError_t launch_v4_t(const AttnArgs& a, hipStream_t st) {
+  const size_t smem = 4 * (size_t)kBK * 64 * sizeof(bf16);
+  auto kfn = fa_fwd_bf16_v4<CAUSAL, NW>;
+  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)smem);
+  if (e != hipSuccess) return e;
+  const int nqb = (a.N + 32 * NW - 1) / (32 * NW);
+  const int64_t nblk = (int64_t)nqb * a.B * a.H;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(64 * NW), smem, st, a, nqb);
+  return hipGetLastError();
+}
+
+// d = 64 only; every per-head K/V byte offset up to two tiles past N must fit the 31-bit
+// buffer offset (the bulk loop stages one tile ahead of the last one it needs).
+hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled) {
+  *handled = false;
+  if (a.d != 64) return hipSuccess;
+  const int64_t lim = (int64_t)1 << 31;
+  if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
+    return hipSuccess;
+  *handled = true;
+  if (nw == 8) return causal ? launch_v4_t<true, 8>(a, st) : launch_v4_t<false, 8>(a, st);
+  return causal ? launch_v4_t<true, 4>(a, st) : launch_v4_t<false, 4>(a, st);
+}
+
+}  // namespace mt

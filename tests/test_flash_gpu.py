@@ -28,15 +28,17 @@ def torch_dev():
 
 def _check_ml(m, l, m_ref, l_ref, exact):
     """(m, l) contract: P = exp(s - m)/l, i.e. m + ln(l) is the row log-sum-exp. The
-    generic kernels return the true row max; the bf16 MFMA kernels may return a max
-    that lags by up to 8·ln2 (deferred rescale), which the contract allows."""
+    generic kernels return the true row max; the bf16 MFMA kernels may return a reference
+    below it: up to 8·ln2 with the deferred rescale, and up to 64·ln2 with v4's frozen
+    first-tile reference (beyond that v4 recomputes the block). The contract allows both;
+    l then stays below 2^64·N."""
     lse, lse_ref = m + np.log(l), m_ref + np.log(l_ref)
     np.testing.assert_allclose(lse, lse_ref, atol=2e-3 if not exact else 1e-5, rtol=1e-5)
     if exact:
         np.testing.assert_allclose(m, m_ref, atol=1e-5, rtol=1e-5)
         np.testing.assert_allclose(l, l_ref, rtol=1e-5)
     else:
-        assert np.all(m <= m_ref + 1e-3) and np.all(m >= m_ref - 8 * np.log(2) - 1e-3)
+        assert np.all(m <= m_ref + 1e-3) and np.all(m >= m_ref - 64 * np.log(2) - 1e-3)
 
 
 def _dev(torch, a, dtype=None):
@@ -159,7 +161,7 @@ def test_host_pointer_abi():
 def _subset_check_fwd(torch, q, k, v, o, causal, heads, atol, pv_rel=0.0):
     """Exact check of a subset of (b,h) slices at full N against the C oracle:
     |O - O_ref| <= atol + pv_rel * (P|V|) elementwise, where P|V| = softmax(QKᵀ/√d)|V|
-    bounds what rounding P to bf16 (relative 2^-9 per element) can move O."""
+    bounds what the bf16 roundings of P (and of the output) can move O."""
     B, H, N, d = q.shape
     for (b, h) in heads:
         qs, ks, vs = (_np(t[b, h]) for t in (q, k, v))
@@ -189,9 +191,10 @@ def test_config2_fp32_full_size(torch_dev):
 def test_config3_bf16_full_size(torch_dev, causal):
     """BASELINE config 3: (8,16,4096,64) bf16 fwd + bwd vs the CPU reference fed the
     same bf16 inputs. Non-causal: ≤1e-3 max-abs on O (the north_star bound). Causal:
-    the first rows average only a few V rows, so |O| reaches ~2.5 and the bf16 output's
-    rounding of P to bf16 (2^-9 relative per weight) moves O by up to 2^-9·(P|V|), which
-    exceeds 1e-3 there -> bound 1e-3 + 2^-8·(P|V|) elementwise.
+    the first rows average only a few V rows, so |O| reaches ~2.5, where two bf16
+    roundings each exceed 1e-3: the bf16 output itself (≤2^-8·|O|) and the bf16 P weights
+    of the PV product against the fp32 row sum (≤2^-8·(P|V|)); since |O| ≤ P|V| the
+    bound is 1e-3 + 2^-7·(P|V|) elementwise.
     Gradients on 2 slices at 2% of their max magnitude."""
     from minitorch import _hip
     torch = torch_dev
@@ -203,7 +206,7 @@ def test_config3_bf16_full_size(torch_dev, causal):
     torch.cuda.synchronize()
     assert torch.isfinite(o.float()).all()
     _subset_check_fwd(torch, q, k, v, o, causal, [(0, 0), (5, 9)], 1e-3,
-                      2.0 ** -8 if causal else 0.0)
+                      2.0 ** -7 if causal else 0.0)
     for (b, h) in [(0, 1), (7, 15)]:
         qs, ks, vs, dos = (_np(t[b, h])[None] for t in (q, k, v, do))
         o_ref, m_ref, l_ref = cref.attn_fwd(qs, ks, vs, causal)
@@ -254,10 +257,12 @@ def test_kernel_variants_agree(torch_dev, causal, d):
         assert float((lse - outs[0][1]).abs().max()) < 2e-3
 
 
-# kernel policies of the bf16 fast forward (mt_flash_set_kernel_policy): 0 default,
+# kernel policies of the bf16 fast forward (mt_flash_set_kernel_policy): 0 default (v4 at
+# d = 64), 3 single-phase 4-wave (fa_fwd_fast.hip),
 # 2 single-phase 8-wave, 4/5 software-pipelined, 6 ping-pong, 7/8/9 v2 (fa_fwd_v2.hip),
-# 16/17/18 v3 (fa_fwd_v3.hip: 4-wave scheduled, 8-wave scheduled, 4-wave unscheduled)
-FAST_POLICIES = (0, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18)
+# 16..20 v3 (fa_fwd_v3.hip: 4-wave, 8-wave, 4-wave unscheduled, 4-/8-wave with MFMA row sum),
+# 21/22 v4 (fa_fwd_v4.hip: frozen first-tile reference, 4-/8-wave)
+FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
@@ -278,6 +283,34 @@ def test_fast_policies_vs_oracle(torch_dev, policy):
                 torch.cuda.synchronize()
                 np.testing.assert_allclose(_np(o), o_ref, atol=2e-2, err_msg=f"{(B, H, N, d, causal)}")
                 _check_ml(_np(m), _np(l), m_ref, l_ref, exact=False)
+    finally:
+        _hip.lib().mt_flash_set_kernel_policy(0)
+
+
+@pytest.mark.parametrize("policy", FAST_POLICIES)
+def test_huge_spike_fallback(torch_dev, policy):
+    """A score far above the first tile's max (> 64 log2 units): v4's bulk loop leaves the
+    safe range and its workgroup recomputes the block with the deferred-max path; every
+    other variant rescales. Rows without the spike are unaffected."""
+    from minitorch import _hip
+    torch = torch_dev
+    B, H, N, d = 1, 1, 1024, 64
+    rng = np.random.default_rng(23)
+    q = rng.standard_normal((B, H, N, d)).astype(np.float32) * 0.3
+    k = rng.standard_normal((B, H, N, d)).astype(np.float32) * 0.3
+    v = rng.standard_normal((B, H, N, d)).astype(np.float32)
+    for row, key in ((3, 900), (400, 700)):
+        k[:, :, key] = q[:, :, row] * 150.0
+    q, k, v = (A.bf16_round(x) for x in (q, k, v))
+    try:
+        _hip.lib().mt_flash_set_kernel_policy(policy)
+        for causal in (False, True):
+            o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
+            o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), causal)
+            torch.cuda.synchronize()
+            assert np.isfinite(_np(o)).all()
+            np.testing.assert_allclose(_np(o), o_ref, atol=2e-2)
+            _check_ml(_np(m), _np(l), m_ref, l_ref, exact=False)
     finally:
         _hip.lib().mt_flash_set_kernel_policy(0)
 
