@@ -20,6 +20,7 @@ hipError_t launch_fwd_v2(const AttnArgs& a, bool causal, int nw, int resc, hipSt
                          bool* handled);
 hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled);
+hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
 
@@ -149,6 +150,11 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
   const int es = dtype == MT_BF16 ? 2 : 4;
   const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv},
                           {q, k, v, o, dout, dq, dk, dv});
+  if (dtype == MT_BF16 && vec && g_kernel_policy != 1) {
+    bool handled = false;
+    const hipError_t e = launch_bwd_bf16(a, causal != 0, (hipStream_t)stream, &handled);
+    if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
+  }
   return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream),
                    "mt_flash_attn_bwd");
 }

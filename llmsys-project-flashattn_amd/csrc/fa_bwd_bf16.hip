@@ -1,0 +1,502 @@
+// FlashAttention backward, bf16 MFMA kernels for head dim 64 (BASELINE config 3).
+//
+// Same mathematics and the same deterministic three-launch split as the generic backward
+// (fa_bwd.hip; reference backward_kernel, src/flashattention_kernel.cu:115-255, with the
+// reference's dV term corrected):
+//     P = exp(s − m)/l,  dV = Pᵀ dO,  dP = dO Vᵀ,  δ = rowsum(dO ∘ O),
+//     dS = P ∘ (dP − δ),  dQ = dS K/√d,  dK = dSᵀ Q/√d,
+// specialised for bf16 I/O at d = 64 the way the forward kernels are:
+//  * prep   : 8 lanes per row; writes the row constants pre-negated and pre-scaled
+//             (−lse2/c2 and −δ, c2 = log2e/√d) so they can seed MFMA accumulators.
+//  * dkv    : a wave owns 32 keys (K, V rows as register-resident B operands) and sweeps
+//             32-query tiles staged in LDS twice — a row image (ds_read_b128, A operand of
+//             S = Q·Kᵀ and dP = dO·Vᵀ) and a transpose image (ds_read_b64_tr_b16, A operand
+//             of dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS). S and dP start from the row constants
+//             (C-init), so p = exp2(c2·S') and dS = p·dP' need no subtraction; their
+//             accumulators are directly the B operands of the next two products.
+//  * dq     : a wave owns 32 queries (Q, dO rows in registers) and sweeps 64-key tiles
+//             (K row + transpose images, V row image); Sᵀ, dPᵀ with the query on the lane,
+//             dQᵀ += Kᵀ·dSᵀ.
+// Staging uses buffer loads (rows past N read as zero) into a double-buffered LDS ring,
+// one barrier per tile; masked tiles (ragged N, causal diagonal) are peeled from the bulk.
+#include "fa_fwd_bf16.h"
+
+namespace mt {
+
+namespace {
+
+using namespace fwdbf16;
+constexpr int D = 64;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+// A operand Xᵀ (rows = d block db, k = rows row0..row0+15 of X in the 8(j>>2)+4h+(j&3)
+// order of an accumulator reused as B) from a transpose-swizzled image of X [rows][64].
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int row0, int voff) {
+  const bf16* a1 = img + row0 * D + voff;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1 + 8 * D));
+  const s16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, av);
+}
+
+__device__ __forceinline__ int tr_off(int lane, int db) {
+  const int hf = lane >> 5, i16 = lane & 15, g = (lane >> 4) & 1;
+  const int col = db * 32 + 16 * g + 4 * (i16 & 3);
+  return v_swz<D>(4 * hf + (i16 >> 2), col >> 3) + (col & 7);
+}
+
+__device__ __forceinline__ bf16x8 to_bf16x8(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+
+__device__ __forceinline__ int xcd_remap(int hw, int nblk) {
+  const int xcd = hw & 7, slot = hw >> 3;
+  const int qd = nblk >> 3, rm = nblk & 7;
+  return (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const bf16* base, int N, int stride) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, ((N - 1) * stride + D) * 2, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// prep: nlse = −(m·log2e + log2 l)/c2, ndel = −rowsum(dO ∘ O); 8 lanes per row.
+__global__ __launch_bounds__(256) void fa_bwd_prep_bf16(AttnArgs p) {
+  const int64_t rows = (int64_t)p.B * p.H * p.N;
+  const int64_t row = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int sub = threadIdx.x & 7;
+  float acc = 0.f;
+  if (row < rows) {
+    const int n = (int)(row % p.N);
+    const int64_t bh = row / p.N;
+    const int b = (int)(bh / p.H), hh = (int)(bh % p.H);
+    const bf16* O = (const bf16*)p.o + b * p.so[0] + hh * p.so[1] + (int64_t)n * p.so[2];
+    const bf16* dO = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + (int64_t)n * p.sdo[2];
+    const bf16x8 o = *(const bf16x8*)(O + 8 * sub), g = *(const bf16x8*)(dO + 8 * sub);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += (float)o[j] * (float)g[j];
+  }
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  acc += __shfl_xor(acc, 4);
+  if (row < rows && sub == 0) {
+    p.delta[row] = -acc;
+    p.lse2[row] = -(p.m[row] * kLog2e + log2f(p.l[row])) / p.scale_log2;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// dK, dV. Workgroup = 4 waves = 128 keys; 32-query tiles.
+namespace {
+constexpr int kQT = 32;
+constexpr int kImgQ = kQT * D;                       // elements of one Q / dO image
+constexpr int kBufQ = 4 * kImgQ * 2 + 2 * kQT * 4;   // bytes per ring slot: 4 images + 2 row vectors
+
+struct DkvCtx {
+  bf16x8 kf[4], vf[4];  // B operands: K / V rows of this lane's key
+  int roff[4];          // row-image offsets per k-step
+  int toff[2];          // transpose-image offsets per d block
+};
+
+template <bool CAUSAL, bool MASK>
+__device__ __forceinline__ void dkv_tile(const char* slot, const DkvCtx& c, f32x16 (&dK)[2],
+                                         f32x16 (&dV)[2], float c2, int qt, int N, int my_k, int hf) {
+  const bf16* Qr = (const bf16*)slot;
+  const bf16* Qt = Qr + kImgQ;
+  const bf16* Or = Qr + 2 * kImgQ;
+  const bf16* Ot = Qr + 3 * kImgQ;
+  const float* nl = (const float*)(Qr + 4 * kImgQ);
+  const float* nd = nl + kQT;
+  f32x16 S, dP;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 a = *(const float4*)(nl + 8 * g + 4 * hf);
+    const float4 e = *(const float4*)(nd + 8 * g + 4 * hf);
+    S[4 * g] = a.x; S[4 * g + 1] = a.y; S[4 * g + 2] = a.z; S[4 * g + 3] = a.w;
+    dP[4 * g] = e.x; dP[4 * g + 1] = e.y; dP[4 * g + 2] = e.z; dP[4 * g + 3] = e.w;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Qr + c.roff[ks]), c.kf[ks], S, 0, 0, 0);
+    dP = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Or + c.roff[ks]), c.vf[ks], dP, 0, 0, 0);
+  }
+  if (MASK) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = qt + acc_row(r, hf);
+      if (q >= N || (CAUSAL && my_k > q)) S[r] = -INFINITY;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float pv = __builtin_amdgcn_exp2f(S[r] * c2);
+    S[r] = pv;
+    dP[r] = pv * dP[r];
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 pf = to_bf16x8(S, s), sf = to_bf16x8(dP, s);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      dV[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ot, 16 * s, c.toff[db]), pf, dV[db], 0, 0, 0);
+      dK[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qt, 16 * s, c.toff[db]), sf, dK[db], 0, 0, 0);
+    }
+  }
+}
+}  // namespace
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16(AttnArgs p, int nkb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = logical / nkb, kb = logical % nkb;
+  const int b = bh / p.H, hh = bh % p.H;
+  const int k0 = kb * 128;
+  const int my_k = k0 + wave * 32 + c32;
+  const int wk_lo = k0 + wave * 32;
+
+  DkvCtx c;
+  {
+    const int kr = min(my_k, N - 1);
+    const bf16* krow = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1] + (int64_t)kr * p.sk[2];
+    const bf16* vrow = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1] + (int64_t)kr * p.sv[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      c.kf[ks] = *(const bf16x8*)(krow + 16 * ks + 8 * hf);
+      c.vf[ks] = *(const bf16x8*)(vrow + 16 * ks + 8 * hf);
+      c.roff[ks] = k_swz<D>(c32, 2 * ks + hf);
+    }
+    c.toff[0] = tr_off(lane, 0);
+    c.toff[1] = tr_off(lane, 1);
+  }
+
+  // Staging: thread -> (row, chunk) of the 32 x 64 Q and dO tiles; 64 threads move the
+  // two row-constant vectors.
+  const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* Og = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int sqn = (int)p.sq[2], son = (int)p.sdo[2];
+  const __amdgpu_buffer_rsrc_t rq = head_rsrc(Qg, N, sqn), ro = head_rsrc(Og, N, son);
+  const int st_r = tid >> 3, st_c = tid & 7;
+  const int goq = (st_r * sqn + st_c * 8) * 2, goo = (st_r * son + st_c * 8) * 2;
+  const int srow = k_swz<D>(st_r, st_c), stri = v_swz<D>(st_r, st_c);
+  const float* nlse = p.lse2 + (int64_t)bh * N;
+  const float* ndel = p.delta + (int64_t)bh * N;
+
+  const int qt0 = CAUSAL ? k0 : 0;
+  const int ntile = N > qt0 ? (N - qt0 + kQT - 1) / kQT : 0;
+  // mask-free tiles: [ndiag, nfull)
+  const int ndiag = CAUSAL ? min(ntile, 128 / kQT) : 0;
+  const int nfull = max(ndiag, (N - qt0) / kQT);
+
+  uint4 sq, so;
+  float sv = 0.f;
+#define DKV_LOAD(T_)                                                                     \
+  {                                                                                      \
+    const int qt_ = qt0 + (T_) * kQT;                                                    \
+    sq = bload(rq, goq + qt_ * sqn * 2);                                                 \
+    so = bload(ro, goo + qt_ * son * 2);                                                 \
+    if (tid < 2 * kQT) {                                                                 \
+      const int q_ = qt_ + (tid & (kQT - 1));                                            \
+      sv = q_ < N ? (tid < kQT ? nlse[q_] : ndel[q_]) : 0.f;                             \
+    }                                                                                    \
+  }
+#define DKV_STORE(SLOT_)                                                                 \
+  {                                                                                      \
+    bf16* img = (bf16*)(smem + (SLOT_) * kBufQ);                                         \
+    *(uint4*)(img + srow) = sq;                                                          \
+    *(uint4*)(img + kImgQ + stri) = sq;                                                  \
+    *(uint4*)(img + 2 * kImgQ + srow) = so;                                              \
+    *(uint4*)(img + 3 * kImgQ + stri) = so;                                              \
+    if (tid < 2 * kQT) ((float*)(img + 4 * kImgQ))[tid] = sv;                            \
+  }
+
+  f32x16 dK[2], dV[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
+  const float c2 = p.scale_log2;
+
+  if (ntile > 0) {
+    DKV_LOAD(0)
+    DKV_STORE(0)
+  }
+  __syncthreads();
+#define DKV_STEP(MASK_, SLOT_, T_)                                                       \
+  {                                                                                      \
+    const int t_ = (T_);                                                                 \
+    const bool more_ = t_ + 1 < ntile;                                                   \
+    if (more_) DKV_LOAD(t_ + 1)                                                          \
+    const int qt_ = qt0 + t_ * kQT;                                                      \
+    if (!(MASK_) || !CAUSAL || qt_ + kQT - 1 >= wk_lo)                                   \
+      dkv_tile<CAUSAL, MASK_>(smem + (SLOT_) * kBufQ, c, dK, dV, c2, qt_, N, my_k, hf);  \
+    if (more_) DKV_STORE((SLOT_) ^ 1)                                                    \
+    __syncthreads();                                                                     \
+  }
+  int t = 0;
+  for (; t < ndiag; ++t) {
+    if (t & 1) DKV_STEP(true, 1, t) else DKV_STEP(true, 0, t)
+  }
+  if ((t & 1) && t < nfull) {
+    DKV_STEP(false, 1, t)
+    ++t;
+  }
+  for (; t + 1 < nfull; t += 2) {
+    DKV_STEP(false, 0, t)
+    DKV_STEP(false, 1, t + 1)
+  }
+  for (; t < ntile; ++t) {
+    if (t < nfull) {
+      if (t & 1) DKV_STEP(false, 1, t) else DKV_STEP(false, 0, t)
+    } else {
+      if (t & 1) DKV_STEP(true, 1, t) else DKV_STEP(true, 0, t)
+    }
+  }
+#undef DKV_STEP
+#undef DKV_LOAD
+#undef DKV_STORE
+
+  if (my_k < N) {
+    bf16* dKg = (bf16*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
+    bf16* dVg = (bf16*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
+    const float sc = p.scale;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = db * 32 + 8 * g + 4 * hf;
+        store4(dKg + col, dK[db][4 * g] * sc, dK[db][4 * g + 1] * sc, dK[db][4 * g + 2] * sc,
+               dK[db][4 * g + 3] * sc, true);
+        store4(dVg + col, dV[db][4 * g], dV[db][4 * g + 1], dV[db][4 * g + 2], dV[db][4 * g + 3], true);
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// dQ. Workgroup = 4 waves = 128 queries; 64-key tiles.
+namespace {
+constexpr int kKT = 64;
+constexpr int kImgK = kKT * D;
+constexpr int kBufK = 3 * kImgK * 2;  // K row image, K transpose image, V row image
+
+struct DqCtx {
+  bf16x8 qf[4], of[4];  // B operands: Q / dO rows of this lane's query
+  int roff[4];
+  int toff[2];
+};
+
+template <bool CAUSAL, bool MASK>
+__device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16 (&dQ)[2], float c2,
+                                        float nlq, float del, int k0, int N, int my_q, int hf) {
+  const bf16* Kr = (const bf16*)slot;
+  const bf16* Kt = Kr + kImgK;
+  const bf16* Vr = Kr + 2 * kImgK;
+  f32x16 S[2], dP[2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Kr + kb * 32 * D + c.roff[ks]),
+                                                      c.qf[ks], ks ? S[kb] : f32x16{}, 0, 0, 0);
+      dP[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Vr + kb * 32 * D + c.roff[ks]),
+                                                       c.of[ks], ks ? dP[kb] : f32x16{}, 0, 0, 0);
+    }
+  if (MASK) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + kb * 32 + acc_row(r, hf);
+        if (key >= N || (CAUSAL && key > my_q)) S[kb][r] = -INFINITY;
+      }
+  }
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[kb][r], c2, nlq));
+      dP[kb][r] = pv * (dP[kb][r] - del);
+    }
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 sf = to_bf16x8(dP[kb], s);
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+        dQ[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Kt, kb * 32 + 16 * s, c.toff[db]), sf,
+                                                         dQ[db], 0, 0, 0);
+    }
+}
+}  // namespace
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = logical / nqb;
+  int qb = logical % nqb;
+  if (CAUSAL) qb = nqb - 1 - qb;  // heaviest first
+  const int b = bh / p.H, hh = bh % p.H;
+  const int q0 = qb * 128;
+  const int my_q = q0 + wave * 32 + c32;
+  const int wq_hi = q0 + wave * 32 + 31;
+
+  DqCtx c;
+  float nlq, del;
+  {
+    const int qr = min(my_q, N - 1);
+    const bf16* qrow = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1] + (int64_t)qr * p.sq[2];
+    const bf16* orow = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + (int64_t)qr * p.sdo[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      c.qf[ks] = *(const bf16x8*)(qrow + 16 * ks + 8 * hf);
+      c.of[ks] = *(const bf16x8*)(orow + 16 * ks + 8 * hf);
+      c.roff[ks] = k_swz<D>(c32, 2 * ks + hf);
+    }
+    c.toff[0] = tr_off(lane, 0);
+    c.toff[1] = tr_off(lane, 1);
+    const int64_t row = (int64_t)bh * N + qr;
+    nlq = p.lse2[row] * p.scale_log2;  // = −lse2
+    del = -p.delta[row];
+  }
+
+  const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const int skn = (int)p.sk[2], svn = (int)p.sv[2];
+  const __amdgpu_buffer_rsrc_t rk = head_rsrc(Kg, N, skn), rv = head_rsrc(Vg, N, svn);
+  int gk[2], gv[2], srow[2], stri[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (tid >> 3) + 32 * i, cc = tid & 7;
+    gk[i] = (r * skn + cc * 8) * 2;
+    gv[i] = (r * svn + cc * 8) * 2;
+    srow[i] = k_swz<D>(r, cc);
+    stri[i] = v_swz<D>(r, cc);
+  }
+
+  const int kend = CAUSAL ? min(N, q0 + 128) : N;
+  const int ntile = (kend + kKT - 1) / kKT;
+  const int nfull = CAUSAL ? min(N / kKT, q0 / kKT) : N / kKT;
+
+  uint4 sk[2], svv[2];
+#define DQ_LOAD(T_)                                                                      \
+  {                                                                                      \
+    const int k0_ = (T_) * kKT;                                                          \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                      \
+      sk[i] = bload(rk, gk[i] + k0_ * skn * 2);                                          \
+      svv[i] = bload(rv, gv[i] + k0_ * svn * 2);                                         \
+    }                                                                                    \
+  }
+#define DQ_STORE(SLOT_)                                                                  \
+  {                                                                                      \
+    bf16* img = (bf16*)(smem + (SLOT_) * kBufK);                                         \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                      \
+      *(uint4*)(img + srow[i]) = sk[i];                                                  \
+      *(uint4*)(img + kImgK + stri[i]) = sk[i];                                          \
+      *(uint4*)(img + 2 * kImgK + srow[i]) = svv[i];                                     \
+    }                                                                                    \
+  }
+
+  f32x16 dQ[2] = {f32x16{}, f32x16{}};
+  const float c2 = p.scale_log2;
+  DQ_LOAD(0)
+  DQ_STORE(0)
+  __syncthreads();
+#define DQ_STEP(MASK_, SLOT_, T_)                                                        \
+  {                                                                                      \
+    const int t_ = (T_);                                                                 \
+    const bool more_ = t_ + 1 < ntile;                                                   \
+    if (more_) DQ_LOAD(t_ + 1)                                                           \
+    if (!(MASK_) || !CAUSAL || t_ * kKT <= wq_hi)                                        \
+      dq_tile<CAUSAL, MASK_>(smem + (SLOT_) * kBufK, c, dQ, c2, nlq, del, t_ * kKT, N,   \
+                             my_q, hf);                                                  \
+    if (more_) DQ_STORE((SLOT_) ^ 1)                                                     \
+    __syncthreads();                                                                     \
+  }
+  int t = 0;
+  for (; t + 1 < nfull; t += 2) {
+    DQ_STEP(false, 0, t)
+    DQ_STEP(false, 1, t + 1)
+  }
+  if (t < nfull) {
+    DQ_STEP(false, 0, t)
+    ++t;
+  }
+  for (; t < ntile; ++t) {
+    if (t & 1) DQ_STEP(true, 1, t) else DQ_STEP(true, 0, t)
+  }
+#undef DQ_STEP
+#undef DQ_LOAD
+#undef DQ_STORE
+
+  if (my_q < N) {
+    bf16* dQg = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)my_q * p.sdq[2];
+    const float sc = p.scale;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        store4(dQg + db * 32 + 8 * g + 4 * hf, dQ[db][4 * g] * sc, dQ[db][4 * g + 1] * sc,
+               dQ[db][4 * g + 2] * sc, dQ[db][4 * g + 3] * sc, true);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+template <bool CAUSAL>
+static hipError_t launch_bwd_bf16_t(const AttnArgs& a, hipStream_t st) {
+  const int64_t rows = (int64_t)a.B * a.H * a.N;
+  hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  {
+    const int nkb = (a.N + 127) / 128;
+    const int64_t nblk = (int64_t)nkb * a.B * a.H;
+    if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+    const size_t smem = 2 * (size_t)kBufQ;
+    auto kfn = fa_bwd_dkv_bf16<CAUSAL>;
+    e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(256), smem, st, a, nkb);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  {
+    const int nqb = (a.N + 127) / 128;
+    const int64_t nblk = (int64_t)nqb * a.B * a.H;
+    const size_t smem = 2 * (size_t)kBufK;
+    auto kfn = fa_bwd_dq_bf16<CAUSAL>;
+    e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(256), smem, st, a, nqb);
+    return hipGetLastError();
+  }
+}
+
+// bf16, d = 64, every per-head row offset of Q/K/V/dO (plus one tile past N) inside the
+// 31-bit buffer range; otherwise the caller falls back to the generic kernels.
+hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, hipStream_t st, bool* handled) {
+  *handled = false;
+  if (a.d != 64) return hipSuccess;
+  const int64_t lim = (int64_t)1 << 31;
+  for (const int64_t s : {a.sq[2], a.sk[2], a.sv[2], a.sdo[2]})
+    if (((int64_t)a.N + 64) * s * 2 >= lim) return hipSuccess;
+  *handled = true;
+  return causal ? launch_bwd_bf16_t<true>(a, st) : launch_bwd_bf16_t<false>(a, st);
+}
+
+}  // namespace mt
