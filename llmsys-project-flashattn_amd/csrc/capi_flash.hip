@@ -19,7 +19,8 @@ hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStrea
 hipError_t launch_fwd_v2(const AttnArgs& a, bool causal, int nw, int resc, hipStream_t st,
                          bool* handled);
 hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
-hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled);
+hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
+                         bool* handled);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
@@ -111,11 +112,13 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
                         &handled);
     if (g_kernel_policy >= 16 && g_kernel_policy <= 20)
       e = launch_fwd_v3(a, causal != 0, g_kernel_policy - 16, st, &handled);
-    if (g_kernel_policy == 21 || g_kernel_policy == 22)
-      e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 22 ? 8 : 4, st, &handled);
-    // default: v4 at d = 64 (8 waves; 4 for causal, whose diagonal blocks finish unevenly),
-    // the single-phase 4-wave kernel otherwise (d = 128)
-    if (g_kernel_policy == 0) e = launch_fwd_v4(a, causal != 0, causal ? 4 : 8, st, &handled);
+    if (g_kernel_policy >= 21 && g_kernel_policy <= 24)
+      e = launch_fwd_v4(a, causal != 0, (g_kernel_policy & 1) ? 4 : 8, g_kernel_policy >= 23, st,
+                        &handled);
+    // default: v4 at d = 64, 4 waves (packed-f32 softmax arithmetic for the full-tile
+    // non-causal case, scalar for causal: the faster of each in the A/B, profiles/), the
+    // single-phase 4-wave kernel otherwise (d = 128)
+    if (g_kernel_policy == 0) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
     if (!handled) e = launch_fwd_fast(a, causal != 0, g_kernel_policy, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");
   }

@@ -128,11 +128,35 @@ __device__ __forceinline__ void store4x(bf16* dst, const uint4 (&r)[2], const in
 //   8 x [K read (2 ahead), QKᵀ MFMA, 2 exponentials of key block 0]
 //   4 x [Vᵀ reads, PV MFMA (block 0), 4 exponentials of key block 1]
 //   4 x [Vᵀ reads, PV MFMA (block 1)]
+// PK: the scale-and-shift and the row-sum adds as packed f32 pairs (v_pk_fma_f32 /
+// v_pk_add_f32) instead of scalar ops — an A/B switch.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+template <bool PK>
+__device__ __forceinline__ void exp_pair(float s0, float s1, float c2, float nmc, f32x2& acc, float& l,
+                                         bf16& p0, bf16& p1) {
+  float e0, e1;
+  if (PK) {
+    const f32x2 x = f32x2{s0, s1} * f32x2{c2, c2} + f32x2{nmc, nmc};
+    e0 = __builtin_amdgcn_exp2f(x[0]);
+    e1 = __builtin_amdgcn_exp2f(x[1]);
+    acc += f32x2{e0, e1};
+  } else {
+    e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s0, c2, nmc));
+    e1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s1, c2, nmc));
+    l += e0;
+    l += e1;
+  }
+  p0 = (bf16)e0;
+  p1 = (bf16)e1;
+}
+
+template <bool PK>
 __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4& c,
                                       const bf16x8 (&qf)[4], const f32x16 (&SC)[2], f32x16 (&SN)[2],
                                       f32x16 (&O)[2], float& l, float c2, float nmc) {
   bf16x8 kf[8];
   bf16x8 pf[4];
+  f32x2 acc = {0.f, 0.f};
 #define V4_KREAD(I_) kf[I_] = *(const bf16x8*)(sk + ((I_) & 1) * 32 * 64 + c.koff[(I_) >> 1]);
   V4_KREAD(0)
   V4_KREAD(1)
@@ -141,11 +165,12 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
     if (i + 2 < 8) V4_KREAD(i + 2)
     SN[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i >> 1], i < 2 ? f32x16{} : SN[i & 1],
                                                        0, 0, 0);
-#pragma unroll
-    for (int j = 2 * i; j < 2 * i + 2; ++j) {
-      const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(SC[0][j], c2, nmc));
-      l += e;
-      pf[j >> 3][j & 7] = (bf16)e;
+    {
+      const int j = 2 * i;
+      bf16 e0, e1;
+      exp_pair<PK>(SC[0][j], SC[0][j + 1], c2, nmc, acc, l, e0, e1);
+      pf[j >> 3][j & 7] = e0;
+      pf[j >> 3][(j & 7) + 1] = e1;
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -171,10 +196,11 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
     if (n + 2 < 4) V4_VREAD(0, n + 2)
     V4_PVMMA(n, pf[n >> 1])
 #pragma unroll
-    for (int j = 4 * n; j < 4 * n + 4; ++j) {
-      const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(SC[1][j], c2, nmc));
-      l += e;
-      pf[2 + (j >> 3)][j & 7] = (bf16)e;
+    for (int j = 4 * n; j < 4 * n + 4; j += 2) {
+      bf16 e0, e1;
+      exp_pair<PK>(SC[1][j], SC[1][j + 1], c2, nmc, acc, l, e0, e1);
+      pf[2 + (j >> 3)][j & 7] = e0;
+      pf[2 + (j >> 3)][(j & 7) + 1] = e1;
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -187,11 +213,12 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
   }
 #undef V4_VREAD
 #undef V4_PVMMA
+  if (PK) l += acc[0] + acc[1];
 }
 
 }  // namespace
 
-template <bool CAUSAL, int NW>
+template <bool CAUSAL, int NW, bool PK>
 __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb) {
   using C = V4<NW>;
   constexpr int D = 64;
@@ -326,7 +353,7 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb
   {                                                                                         \
     load4<NW>(rK, rk, c.kgo, ((T_) + 2) * ktile_b);                                         \
     load4<NW>(rV, rv, c.vgo, ((T_) + 1) * vtile_b);                                         \
-    bulk4(SKN_, SVC_, c, qf, SC_, SN_, O, l_part, c2, nmc);                                 \
+    bulk4<PK>(SKN_, SVC_, c, qf, SC_, SN_, O, l_part, c2, nmc);                                 \
     store4x<NW>(SKW_, rK, c.kso);                                                           \
     store4x<NW>(SVW_, rV, c.vso);                                                           \
     __syncthreads();                                                                        \
@@ -365,10 +392,10 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb
   }
 }
 
-template <bool CAUSAL, int NW>
+template <bool CAUSAL, int NW, bool PK>
 static hipError_t launch_v4_t(const AttnArgs& a, hipStream_t st) {
   const size_t smem = 4 * (size_t)kBK * 64 * sizeof(bf16);
-  auto kfn = fa_fwd_bf16_v4<CAUSAL, NW>;
+  auto kfn = fa_fwd_bf16_v4<CAUSAL, NW, PK>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)smem);
   if (e != hipSuccess) return e;
@@ -381,15 +408,20 @@ static hipError_t launch_v4_t(const AttnArgs& a, hipStream_t st) {
 
 // d = 64 only; every per-head K/V byte offset up to two tiles past N must fit the 31-bit
 // buffer offset (the bulk loop stages one tile ahead of the last one it needs).
-hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled) {
+hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
+                         bool* handled) {
   *handled = false;
   if (a.d != 64) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
-  if (nw == 8) return causal ? launch_v4_t<true, 8>(a, st) : launch_v4_t<false, 8>(a, st);
-  return causal ? launch_v4_t<true, 4>(a, st) : launch_v4_t<false, 4>(a, st);
+  if (pk) {
+    if (nw == 8) return causal ? launch_v4_t<true, 8, true>(a, st) : launch_v4_t<false, 8, true>(a, st);
+    return causal ? launch_v4_t<true, 4, true>(a, st) : launch_v4_t<false, 4, true>(a, st);
+  }
+  if (nw == 8) return causal ? launch_v4_t<true, 8, false>(a, st) : launch_v4_t<false, 8, false>(a, st);
+  return causal ? launch_v4_t<true, 4, false>(a, st) : launch_v4_t<false, 4, false>(a, st);
 }
 
 }  // namespace mt

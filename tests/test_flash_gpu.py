@@ -261,8 +261,9 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # d = 64), 3 single-phase 4-wave (fa_fwd_fast.hip),
 # 2 single-phase 8-wave, 4/5 software-pipelined, 6 ping-pong, 7/8/9 v2 (fa_fwd_v2.hip),
 # 16..20 v3 (fa_fwd_v3.hip: 4-wave, 8-wave, 4-wave unscheduled, 4-/8-wave with MFMA row sum),
-# 21/22 v4 (fa_fwd_v4.hip: frozen first-tile reference, 4-/8-wave)
-FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22)
+# 21/22 v4 (fa_fwd_v4.hip: frozen first-tile reference, 4-/8-wave), 23/24 the same with
+# packed-f32 scale and row sum (8-/4-wave)
+FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
