@@ -10,6 +10,7 @@
 
 #include "../../include/minitorch_hip.h"
 #include "fa_common.h"
+#include <algorithm>
 
 namespace mt {
 hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
@@ -21,6 +22,9 @@ hipError_t launch_fwd_v2(const AttnArgs& a, bool causal, int nw, int resc, hipSt
 hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
                          bool* handled);
+hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
+hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
+hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, hipStream_t st, bool* handled);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
@@ -115,10 +119,24 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
     if (g_kernel_policy >= 21 && g_kernel_policy <= 24)
       e = launch_fwd_v4(a, causal != 0, (g_kernel_policy & 1) ? 4 : 8, g_kernel_policy >= 23, st,
                         &handled);
-    // default: v4 at d = 64, 4 waves (packed-f32 softmax arithmetic for the full-tile
-    // non-causal case, scalar for causal: the faster of each in the A/B, profiles/), the
-    // single-phase 4-wave kernel otherwise (d = 128)
-    if (g_kernel_policy == 0) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
+    // default at d = 64: v5 (two query blocks per wave) for non-causal N % 64 == 0, else
+    // 4-wave v4 (packed-f32 softmax arithmetic when non-causal, scalar when causal: the
+    // faster of each in the A/B, profiles/r1_ab_*); the single-phase 4-wave kernel at d = 128
+    if ((g_kernel_policy == 25 || g_kernel_policy == 26) && d == 64 &&
+        ((int64_t)N + 128) * std::max(a.sk[2], a.sv[2]) * 2 < ((int64_t)1 << 31)) {
+      e = launch_fwd_v4_deep(a, causal != 0, g_kernel_policy == 25, st);  // 4-wave, deep staging
+      handled = true;
+    }
+    if (g_kernel_policy >= 27 && g_kernel_policy <= 29)
+      e = launch_fwd_v5(a, causal != 0, 2 * (g_kernel_policy - 26), st, &handled);
+    if (g_kernel_policy >= 91 && g_kernel_policy <= 96 && d == 64 && !causal) {
+      e = launch_fwd_v4_ablation(a, g_kernel_policy - 90, st);  // diagnostics only
+      handled = true;
+    }
+    if (g_kernel_policy == 0) {
+      e = launch_fwd_v5(a, causal != 0, 2, st, &handled);  // non-causal, N % 64 == 0
+      if (!handled) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
+    }
     if (!handled) e = launch_fwd_fast(a, causal != 0, g_kernel_policy, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");
   }

@@ -131,15 +131,17 @@ __device__ __forceinline__ void store4x(bf16* dst, const uint4 (&r)[2], const in
 // PK: the scale-and-shift and the row-sum adds as packed f32 pairs (v_pk_fma_f32 /
 // v_pk_add_f32) instead of scalar ops — an A/B switch.
 typedef __attribute__((ext_vector_type(2))) float f32x2;
-template <bool PK>
+// ABL (diagnostic builds only, policies 90+): 1 = no K/V staging, 2 = also no barrier,
+// 3 = no exponential, 4 = no row-sum adds, 5 = no K operand reads, 6 = no Vᵀ operand reads.
+template <bool PK, int ABL = 0>
 __device__ __forceinline__ void exp_pair(float s0, float s1, float c2, float nmc, f32x2& acc, float& l,
                                          bf16& p0, bf16& p1) {
   float e0, e1;
   if (PK) {
     const f32x2 x = f32x2{s0, s1} * f32x2{c2, c2} + f32x2{nmc, nmc};
-    e0 = __builtin_amdgcn_exp2f(x[0]);
-    e1 = __builtin_amdgcn_exp2f(x[1]);
-    acc += f32x2{e0, e1};
+    e0 = ABL == 3 ? x[0] : __builtin_amdgcn_exp2f(x[0]);
+    e1 = ABL == 3 ? x[1] : __builtin_amdgcn_exp2f(x[1]);
+    if (ABL != 4) acc += f32x2{e0, e1};
   } else {
     e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s0, c2, nmc));
     e1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s1, c2, nmc));
@@ -150,14 +152,14 @@ __device__ __forceinline__ void exp_pair(float s0, float s1, float c2, float nmc
   p1 = (bf16)e1;
 }
 
-template <bool PK>
+template <bool PK, int ABL = 0>
 __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4& c,
                                       const bf16x8 (&qf)[4], const f32x16 (&SC)[2], f32x16 (&SN)[2],
                                       f32x16 (&O)[2], float& l, float c2, float nmc) {
   bf16x8 kf[8];
   bf16x8 pf[4];
   f32x2 acc = {0.f, 0.f};
-#define V4_KREAD(I_) kf[I_] = *(const bf16x8*)(sk + ((I_) & 1) * 32 * 64 + c.koff[(I_) >> 1]);
+#define V4_KREAD(I_) kf[I_] = ABL == 5 ? qf[((I_) + 1) & 3] : *(const bf16x8*)(sk + ((I_) & 1) * 32 * 64 + c.koff[(I_) >> 1]);
   V4_KREAD(0)
   V4_KREAD(1)
 #pragma unroll
@@ -168,7 +170,7 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
     {
       const int j = 2 * i;
       bf16 e0, e1;
-      exp_pair<PK>(SC[0][j], SC[0][j + 1], c2, nmc, acc, l, e0, e1);
+      exp_pair<PK, ABL>(SC[0][j], SC[0][j + 1], c2, nmc, acc, l, e0, e1);
       pf[j >> 3][j & 7] = e0;
       pf[j >> 3][(j & 7) + 1] = e1;
     }
@@ -179,8 +181,13 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
 #define V4_VREAD(KB_, N_)                                                                  \
   {                                                                                        \
     const bf16* a1 = sv + ((KB_) * 32 + 16 * ((N_) >> 1)) * 64 + c.voff[(N_) & 1];         \
-    vlo[N_] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);                     \
-    vhi[N_] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1 + 8 * 64));          \
+    if (ABL == 6) {                                                                        \
+      vlo[N_] = __builtin_bit_cast(s16x4, (uint2){(unsigned)c.voff[(N_) & 1], (unsigned)(KB_)}); \
+      vhi[N_] = vlo[N_];                                                                   \
+    } else {                                                                               \
+      vlo[N_] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);                   \
+      vhi[N_] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1 + 8 * 64));        \
+    }                                                                                      \
   }
 #define V4_PVMMA(N_, PF_)                                                                  \
   {                                                                                        \
@@ -198,7 +205,7 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
 #pragma unroll
     for (int j = 4 * n; j < 4 * n + 4; j += 2) {
       bf16 e0, e1;
-      exp_pair<PK>(SC[1][j], SC[1][j + 1], c2, nmc, acc, l, e0, e1);
+      exp_pair<PK, ABL>(SC[1][j], SC[1][j + 1], c2, nmc, acc, l, e0, e1);
       pf[2 + (j >> 3)][j & 7] = e0;
       pf[2 + (j >> 3)][(j & 7) + 1] = e1;
     }
@@ -218,7 +225,7 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
 
 }  // namespace
 
-template <bool CAUSAL, int NW, bool PK>
+template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false>
 __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb) {
   using C = V4<NW>;
   constexpr int D = 64;
@@ -351,18 +358,41 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb
       // into a slot nobody reads).
 #define V4_BULK(T_, SC_, SN_, SKN_, SVC_, SKW_, SVW_)                                       \
   {                                                                                         \
-    load4<NW>(rK, rk, c.kgo, ((T_) + 2) * ktile_b);                                         \
-    load4<NW>(rV, rv, c.vgo, ((T_) + 1) * vtile_b);                                         \
-    bulk4<PK>(SKN_, SVC_, c, qf, SC_, SN_, O, l_part, c2, nmc);                                 \
-    store4x<NW>(SKW_, rK, c.kso);                                                           \
-    store4x<NW>(SVW_, rV, c.vso);                                                           \
-    __syncthreads();                                                                        \
+    if (ABL != 1 && ABL != 2) load4<NW>(rK, rk, c.kgo, ((T_) + 2) * ktile_b);               \
+    if (ABL != 1 && ABL != 2) load4<NW>(rV, rv, c.vgo, ((T_) + 1) * vtile_b);               \
+    bulk4<PK, ABL>(SKN_, SVC_, c, qf, SC_, SN_, O, l_part, c2, nmc);                        \
+    if (ABL != 1 && ABL != 2) store4x<NW>(SKW_, rK, c.kso);                                 \
+    if (ABL != 1 && ABL != 2) store4x<NW>(SVW_, rV, c.vso);                                 \
+    if (ABL != 2) __syncthreads();                                                          \
   }
       // t odd: S(t) in SA, K(t+1) in slot 0, V(t) in slot 1; writes K(t+2) -> slot 1,
       // V(t+1) -> slot 0. t+1 even: mirror.
-      for (; t + 2 < nfull; t += 2) {
-        V4_BULK(t, SA, SB, sK0, sV1, sK1, sV0)
-        V4_BULK(t + 1, SB, SA, sK1, sV0, sK0, sV1)
+      if (!DEEP) {
+        for (; t + 2 < nfull; t += 2) {
+          V4_BULK(t, SA, SB, sK0, sV1, sK1, sV0)
+          V4_BULK(t + 1, SB, SA, sK1, sV0, sK0, sV1)
+        }
+      } else if (t + 2 < nfull) {
+        // DEEP: the global loads run one iteration further ahead, alternating between two
+        // register sets: iteration t writes K(t+2) / V(t+1) (loaded during t-1) and loads
+        // K(t+3) / V(t+2), so each load has a whole iteration more to land.
+        uint4 rK2[2], rV2[2];
+        load4<NW>(rK, rk, c.kgo, (t + 2) * ktile_b);
+        load4<NW>(rV, rv, c.vgo, (t + 1) * vtile_b);
+#define V4_DEEP(T_, SC_, SN_, SKN_, SVC_, SKW_, SVW_, ST_K, ST_V, LD_K, LD_V)                \
+  {                                                                                         \
+    load4<NW>(LD_K, rk, c.kgo, ((T_) + 3) * ktile_b);                                       \
+    load4<NW>(LD_V, rv, c.vgo, ((T_) + 2) * vtile_b);                                       \
+    bulk4<PK, ABL>(SKN_, SVC_, c, qf, SC_, SN_, O, l_part, c2, nmc);                        \
+    store4x<NW>(SKW_, ST_K, c.kso);                                                         \
+    store4x<NW>(SVW_, ST_V, c.vso);                                                         \
+    __syncthreads();                                                                        \
+  }
+        for (; t + 2 < nfull; t += 2) {
+          V4_DEEP(t, SA, SB, sK0, sV1, sK1, sV0, rK, rV, rK2, rV2)
+          V4_DEEP(t + 1, SB, SA, sK1, sV0, sK0, sV1, rK2, rV2, rK, rV)
+        }
+#undef V4_DEEP
       }
 #undef V4_BULK
     }
@@ -392,10 +422,10 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb
   }
 }
 
-template <bool CAUSAL, int NW, bool PK>
+template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false>
 static hipError_t launch_v4_t(const AttnArgs& a, hipStream_t st) {
   const size_t smem = 4 * (size_t)kBK * 64 * sizeof(bf16);
-  auto kfn = fa_fwd_bf16_v4<CAUSAL, NW, PK>;
+  auto kfn = fa_fwd_bf16_v4<CAUSAL, NW, PK, ABL, DEEP>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)smem);
   if (e != hipSuccess) return e;
@@ -408,6 +438,23 @@ static hipError_t launch_v4_t(const AttnArgs& a, hipStream_t st) {
 
 // d = 64 only; every per-head K/V byte offset up to two tiles past N must fit the 31-bit
 // buffer offset (the bulk loop stages one tile ahead of the last one it needs).
+// Diagnostic ablations (wrong results by construction; timing only): d = 64, non-causal.
+hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st) {
+  switch (abl) {
+    case 1: return launch_v4_t<false, 4, true, 1>(a, st);
+    case 2: return launch_v4_t<false, 4, true, 2>(a, st);
+    case 3: return launch_v4_t<false, 4, true, 3>(a, st);
+    case 4: return launch_v4_t<false, 4, true, 4>(a, st);
+    case 5: return launch_v4_t<false, 4, true, 5>(a, st);
+    default: return launch_v4_t<false, 4, true, 6>(a, st);
+  }
+}
+
+hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st) {
+  if (pk) return causal ? launch_v4_t<true, 4, true, 0, true>(a, st) : launch_v4_t<false, 4, true, 0, true>(a, st);
+  return causal ? launch_v4_t<true, 4, false, 0, true>(a, st) : launch_v4_t<false, 4, false, 0, true>(a, st);
+}
+
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
                          bool* handled) {
   *handled = false;

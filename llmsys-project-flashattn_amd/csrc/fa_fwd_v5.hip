@@ -1,0 +1,363 @@
+// FlashAttention forward, bf16 MFMA kernel v5 (d = 64, non-causal, N % 64 == 0):
+// two 32-query blocks per wave, skewed by half a tile.
+//
+// v4 gives each wave one 32-query block and relies on the second wave of its SIMD to
+// overlap one wave's softmax with the other's MFMAs. v5 gives each wave two blocks, A and
+// B, and interleaves them inside the wave's own instruction stream: block B runs half a
+// tile behind block A, so every phase pairs 8 MFMAs of one block with the softmax of a
+// 32-key half of the other:
+//     P1: Sᵀ_A(t)   = K(t)·Q_Aᵀ        ‖ softmax B(t), keys 32-63
+//     P2: Oᵀ_B     += Vᵀ(t)·P_Bᵀ(t)    ‖ softmax A(t), keys 0-31
+//     P3: Sᵀ_B(t+1) = K(t+1)·Q_Bᵀ      ‖ softmax A(t), keys 32-63
+//     P4: Oᵀ_A     += Vᵀ(t)·P_Aᵀ(t)    ‖ softmax B(t+1), keys 0-31
+// Each phase is 8 x [MFMA, two scores' pk_fma / 2 exp / pk_add / cvt], fenced with
+// sched_barrier(0). Only S_B(t+1)'s upper half and P_B(t+1)'s lower half cross an
+// iteration, so a wave holds 64 queries in about the registers v4 needs for 32 and still
+// runs two waves per SIMD. K uses a 4-slot LDS ring (an iteration reads K(t) and K(t+1)
+// and writes K(t+2)), V a 2-slot ring; one barrier per iteration.
+// Softmax: v4's frozen first-tile reference (row max of tile 0 per block); a lane whose
+// row-sum share leaves 2^64 sends its workgroup through a serial deferred-max recompute.
+#include "fa_fwd_bf16.h"
+
+namespace mt {
+
+namespace {
+
+using namespace fwdbf16;
+constexpr int D = 64;
+constexpr int kBK = 64;
+constexpr int TILE = kBK * D;              // elements per K or V tile
+constexpr int NWV = 4;                     // waves per workgroup
+constexpr int kBQ = 64 * NWV;              // queries per workgroup
+constexpr int kKSlots = 4, kVSlots = 2;
+constexpr int LPT = kBK * (D / 8) / (64 * NWV);  // 16-B staging chunks per thread per tile
+constexpr float kLimit = 1.8446744e19f;   // 2^64
+constexpr float kThr = 8.0f;
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+struct Ctx5 {
+  int koff[4];  // per-lane K row-image offsets per k-step (slot 0, key block 0)
+  int voff[2];  // per-lane Vᵀ transpose-read offsets per d block (slot 0, row block 0)
+  int kgo[LPT], vgo[LPT], kso[LPT], vso[LPT];
+};
+
+// Softmax of one 32-key half of a block: pair i (0..7) of the 16 scores of S_half.
+__device__ __forceinline__ void sm_pair(const f32x16& s, int i, float c2, float nmc, f32x2& acc,
+                                        bf16x8 (&pf)[2]) {
+  const int j = 2 * i;
+  const f32x2 x = f32x2{s[j], s[j + 1]} * f32x2{c2, c2} + f32x2{nmc, nmc};
+  const float e0 = __builtin_amdgcn_exp2f(x[0]);
+  const float e1 = __builtin_amdgcn_exp2f(x[1]);
+  acc += f32x2{e0, e1};
+  pf[j >> 3][j & 7] = (bf16)e0;
+  pf[j >> 3][(j & 7) + 1] = (bf16)e1;
+}
+
+__device__ __forceinline__ bf16x8 kread(const bf16* sk, const int (&ko)[4], int i) {
+  // MFMA i of a QKᵀ phase: key block i/4, k-step i%4 (block 0's chain completes first)
+  return *(const bf16x8*)(sk + (i >> 2) * 32 * D + ko[i & 3]);
+}
+
+__device__ __forceinline__ bf16x8 vread(const bf16* sv, const int (&vo)[2], int n) {
+  // MFMA n of a PV phase: key block n/4, 16-key step (n/2)%2, d block n%2
+  const bf16* a1 = sv + ((n >> 2) * 32 + 16 * ((n >> 1) & 1)) * D + vo[n & 1];
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1 + 8 * D));
+  const s16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, av);
+}
+
+// QKᵀ phase (8 MFMAs into S) interleaved with the softmax of s_in (8 pairs) -> pf.
+// SOFT = false: MFMAs only.
+template <bool SOFT, int kAhead>
+__device__ __forceinline__ void phase_qk(const bf16* sk, const int (&ko)[4], const bf16x8 (&qf)[4],
+                                         f32x16 (&S)[2], const f32x16& s_in, float c2, float nmc,
+                                         f32x2& acc, bf16x8 (&pf)[2]) {
+  bf16x8 kf[8];
+#pragma unroll
+  for (int i = 0; i < kAhead; ++i) kf[i] = kread(sk, ko, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i + kAhead < 8) kf[i + kAhead] = kread(sk, ko, i + kAhead);
+    S[i >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i & 3], (i & 3) ? S[i >> 2] : f32x16{},
+                                                       0, 0, 0);
+    if (SOFT) sm_pair(s_in, i, c2, nmc, acc, pf);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// PV phase (8 MFMAs into O with P fragments p_lo (keys 0-31) and p_hi (keys 32-63))
+// interleaved with the softmax of s_in (8 pairs) -> pf.
+template <bool SOFT, int kAhead>
+__device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32x16 (&O)[2],
+                                         const bf16x8 (&p_lo)[2], const bf16x8 (&p_hi)[2],
+                                         const f32x16& s_in, float c2, float nmc, f32x2& acc,
+                                         bf16x8 (&pf)[2]) {
+  bf16x8 vf[8];
+#pragma unroll
+  for (int n = 0; n < kAhead; ++n) vf[n] = vread(sv, vo, n);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    if (n + kAhead < 8) vf[n + kAhead] = vread(sv, vo, n + kAhead);
+    const bf16x8& p = (n >> 2) ? p_hi[(n >> 1) & 1] : p_lo[(n >> 1) & 1];
+    O[n & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[n], p, O[n & 1], 0, 0, 0);
+    if (SOFT) sm_pair(s_in, n, c2, nmc, acc, pf);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ void load5(uint4 (&r)[LPT], __amdgpu_buffer_rsrc_t rs, const int (&go)[LPT],
+                                      int step) {
+#pragma unroll
+  for (int i = 0; i < LPT; ++i)
+    r[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, go[i] + step, 0, 0));
+}
+
+__device__ __forceinline__ void store5(bf16* dst, const uint4 (&r)[LPT], const int (&so)[LPT]) {
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) *(uint4*)(dst + so[i]) = r[i];
+}
+
+__device__ __forceinline__ float lane_pair_sum(float x) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+}
+
+}  // namespace
+
+// AHEAD: LDS operand reads are issued this many MFMAs ahead of their use.
+template <int AHEAD>
+__global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* const sK = (bf16*)smem_raw;          // [kKSlots][TILE]
+  bf16* const sV = sK + kKSlots * TILE;      // [kVSlots][TILE]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N;
+
+  const int nblk = gridDim.x, hw = blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
+  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
+  const int bh = logical / nqb, qb = logical % nqb;
+  const int b = bh / p.H, hh = bh % p.H;
+  const int qA = qb * kBQ + wave * 64 + c32;  // this lane's query in block A; B = qA + 32
+
+  const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const int skn = (int)p.sk[2], svn = (int)p.sv[2];
+  const __amdgpu_buffer_rsrc_t rk =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Kg, (short)0, ((N - 1) * skn + D) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Vg, (short)0, ((N - 1) * svn + D) * 2, 0x00020000);
+
+  bf16x8 qfA[4], qfB[4];
+  {
+    const bf16* ra = Qg + (int64_t)min(qA, N - 1) * p.sq[2];
+    const bf16* rb = Qg + (int64_t)min(qA + 32, N - 1) * p.sq[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qfA[ks] = *(const bf16x8*)(ra + ks * 16 + 8 * hf);
+      qfB[ks] = *(const bf16x8*)(rb + ks * 16 + 8 * hf);
+    }
+  }
+  Ctx5 c;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) c.koff[ks] = k_swz<D>(c32, 2 * ks + hf);
+  {
+    const int i16 = lane & 15, g = (lane >> 4) & 1;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int col = db * 32 + 16 * g + 4 * (i16 & 3);
+      c.voff[db] = v_swz<D>(4 * hf + (i16 >> 2), col >> 3) + (col & 7);
+    }
+    const int st_r = tid / (D / 8), st_c = tid % (D / 8);
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int r = st_r + i * (256 / (D / 8));
+      c.kgo[i] = (r * skn + st_c * 8) * 2;
+      c.vgo[i] = (r * svn + st_c * 8) * 2;
+      c.kso[i] = k_swz<D>(r, st_c);
+      c.vso[i] = v_swz<D>(r, st_c);
+    }
+  }
+  const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
+  const int ntiles = N / kBK;
+  const float c2 = p.scale_log2;
+
+  f32x16 OA[2], OB[2];
+  float mA, mB, lA, lB;
+
+  // ---- pass 0: the pipelined loop with the frozen first-tile reference ----------------
+  {
+    uint4 rK[LPT], rV[LPT];
+    load5(rK, rk, c.kgo, 0);
+    load5(rV, rv, c.vgo, 0);
+    store5(sK, rK, c.kso);
+    store5(sV, rV, c.vso);
+    load5(rK, rk, c.kgo, ktile_b);
+    store5(sK + TILE, rK, c.kso);
+    __syncthreads();
+
+    // reference maxima from tile 0; S_B(0) kept for the pipeline, P_B(0) keys 0-31 computed
+    f32x16 SA[2], SB[2];
+    {
+      int ko[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) ko[ks] = c.koff[ks];
+      f32x2 dummy = {0.f, 0.f};
+      bf16x8 dpf[2];
+      phase_qk<false, AHEAD>(sK, ko, qfA, SA, SA[0], c2, 0.f, dummy, dpf);
+      phase_qk<false, AHEAD>(sK, ko, qfB, SB, SB[0], c2, 0.f, dummy, dpf);
+    }
+    mA = row_max32(SA[0], SA[1]);
+    mB = row_max32(SB[0], SB[1]);
+    const float nmcA = -(mA * c2), nmcB = -(mB * c2);
+    f32x2 accA = {0.f, 0.f}, accB = {0.f, 0.f};
+    bf16x8 pB0[2], pB1[2], pA0[2], pA1[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm_pair(SB[0], i, c2, nmcB, accB, pB0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
+
+    // iteration t: K(t) in slot t%4, K(t+1) in slot (t+1)%4, V(t) in slot t%2; stages
+    // K(t+2) -> slot (t+2)%4 and V(t+1) -> slot (t+1)%2. The last tile is peeled.
+    for (int t = 0; t + 1 < ntiles; ++t) {
+      load5(rK, rk, c.kgo, (t + 2) * ktile_b);
+      load5(rV, rv, c.vgo, (t + 1) * vtile_b);
+      int koA[4], koB[4], vo[2];
+      const int kslA = (t & 3) * TILE, kslB = ((t + 1) & 3) * TILE, vsl = (t & 1) * TILE;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        koA[ks] = c.koff[ks] + kslA;
+        koB[ks] = c.koff[ks] + kslB;
+      }
+      vo[0] = c.voff[0] + vsl;
+      vo[1] = c.voff[1] + vsl;
+      phase_qk<true, AHEAD>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);             // P1
+      phase_pv<true, AHEAD>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);         // P2
+      phase_qk<true, AHEAD>(sK, koB, qfB, SB, SA[1], c2, nmcA, accA, pA1);             // P3
+      phase_pv<true, AHEAD>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0);         // P4
+      store5(sK + ((t + 2) & 3) * TILE, rK, c.kso);
+      store5(sV + ((t + 1) & 1) * TILE, rV, c.vso);
+      __syncthreads();
+    }
+    {
+      const int t = ntiles - 1;
+      int koA[4], vo[2];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) koA[ks] = c.koff[ks] + (t & 3) * TILE;
+      vo[0] = c.voff[0] + (t & 1) * TILE;
+      vo[1] = c.voff[1] + (t & 1) * TILE;
+      phase_qk<true, AHEAD>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);
+      phase_pv<true, AHEAD>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sm_pair(SA[1], i, c2, nmcA, accA, pA1);
+      f32x2 d2 = {0.f, 0.f};
+      bf16x8 dpf[2];
+      phase_pv<false, AHEAD>(sV, vo, OA, pA0, pA1, SA[0], c2, 0.f, d2, dpf);
+    }
+    lA = lane_pair_sum(accA[0] + accA[1]);
+    lB = lane_pair_sum(accB[0] + accB[1]);
+  }
+
+  // ---- pass 1 (rare): serial deferred-max recompute for the whole workgroup -----------
+  if (__syncthreads_or(!(lA <= kLimit) || !(lB <= kLimit))) {
+    mA = mB = -INFINITY;
+    float pA = 0.f, pB = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
+    int ko[4], vo[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) ko[ks] = c.koff[ks];
+    vo[0] = c.voff[0];
+    vo[1] = c.voff[1];
+    for (int t = 0; t < ntiles; ++t) {
+      uint4 rK[LPT], rV[LPT];
+      load5(rK, rk, c.kgo, t * ktile_b);
+      load5(rV, rv, c.vgo, t * vtile_b);
+      __syncthreads();
+      store5(sK, rK, c.kso);
+      store5(sV, rV, c.vso);
+      __syncthreads();
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        f32x16 S[2];
+        f32x2 acc = {0.f, 0.f};
+        bf16x8 plo[2], phi[2], dpf[2];
+        phase_qk<false, AHEAD>(sK, ko, blk ? qfB : qfA, S, S[0], c2, 0.f, acc, dpf);
+        float& m = blk ? mB : mA;
+        float& l = blk ? pB : pA;
+        f32x16(&O)[2] = blk ? OB : OA;
+        const float tmax = row_max32(S[0], S[1]);
+        if (__builtin_amdgcn_ballot_w64((tmax - m) * c2 > kThr)) {
+          const float m_new = fmaxf(m, tmax);
+          const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - m_new) * c2);
+          m = m_new;
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) O[i][r] *= alpha;
+          l *= alpha;
+        }
+        const float nmc = -(m * c2);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm_pair(S[0], i, c2, nmc, acc, plo);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm_pair(S[1], i, c2, nmc, acc, phi);
+        l += acc[0] + acc[1];
+        phase_pv<false, AHEAD>(sV, vo, O, plo, phi, S[0], c2, 0.f, acc, dpf);
+      }
+    }
+    lA = lane_pair_sum(pA);
+    lB = lane_pair_sum(pB);
+  }
+
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int q = qA + 32 * blk;
+    const float l = blk ? lB : lA, m = blk ? mB : mA;
+    const f32x16(&O)[2] = blk ? OB : OA;
+    const float inv = 1.f / l;
+    if (q < N) {
+      bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)q * p.so[2];
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          store4(Og + db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv, O[db][4 * g + 1] * inv,
+                 O[db][4 * g + 2] * inv, O[db][4 * g + 3] * inv, true);
+      if (hf == 0) {
+        const int64_t row = (int64_t)bh * N + q;
+        if (p.m) p.m[row] = m * p.scale;
+        if (p.l) p.l[row] = l;
+      }
+    }
+  }
+}
+
+// d = 64, non-causal, N a multiple of 64 (no masked tile) and at least two tiles, and all
+// per-head K/V offsets (two tiles past N) inside the 31-bit buffer range.
+hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, hipStream_t st, bool* handled) {
+  *handled = false;
+  if (a.d != 64 || causal || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
+  const int64_t lim = (int64_t)1 << 31;
+  if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
+    return hipSuccess;
+  *handled = true;
+  const size_t smem = (size_t)(kKSlots + kVSlots) * TILE * sizeof(bf16);
+  auto kfn = ahead >= 6 ? fa_fwd_bf16_v5<6> : ahead >= 4 ? fa_fwd_bf16_v5<4> : fa_fwd_bf16_v5<2>;
+  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (e != hipSuccess) return e;
+  const int nqb = (a.N + kBQ - 1) / kBQ;
+  const int64_t nblk = (int64_t)nqb * a.B * a.H;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(256), smem, st, a, nqb);
+  return hipGetLastError();
+}
+
+}  // namespace mt

@@ -262,8 +262,10 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # 2 single-phase 8-wave, 4/5 software-pipelined, 6 ping-pong, 7/8/9 v2 (fa_fwd_v2.hip),
 # 16..20 v3 (fa_fwd_v3.hip: 4-wave, 8-wave, 4-wave unscheduled, 4-/8-wave with MFMA row sum),
 # 21/22 v4 (fa_fwd_v4.hip: frozen first-tile reference, 4-/8-wave), 23/24 the same with
-# packed-f32 scale and row sum (8-/4-wave)
-FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24)
+# packed-f32 scale and row sum (8-/4-wave), 25/26 4-wave with staging one iteration deeper
+# (packed / scalar), 27/28/29 v5 (fa_fwd_v5.hip: two skewed query blocks per wave, LDS reads
+# 2/4/6 MFMAs ahead; non-causal N % 64 == 0 only, other shapes fall back)
+FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
