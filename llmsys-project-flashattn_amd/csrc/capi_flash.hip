@@ -25,7 +25,7 @@ hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStr
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, hipStream_t st, bool* handled);
-hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, hipStream_t st, bool* handled);
+hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, bool pipe, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
 
@@ -121,7 +121,7 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
                         &handled);
     // default at d = 64: v5 (two query blocks per wave) for non-causal N % 64 == 0, else
     // 4-wave v4 (packed-f32 softmax arithmetic when non-causal, scalar when causal: the
-    // faster of each in the A/B, profiles/r1_ab_*); the single-phase 4-wave kernel at d = 128
+    // faster of each in the A/B, profiles/r1_ab_*)
     if ((g_kernel_policy == 25 || g_kernel_policy == 26) && d == 64 &&
         ((int64_t)N + 128) * std::max(a.sk[2], a.sv[2]) * 2 < ((int64_t)1 << 31)) {
       e = launch_fwd_v4_deep(a, causal != 0, g_kernel_policy == 25, st);  // 4-wave, deep staging
@@ -137,7 +137,10 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       e = launch_fwd_v5(a, causal != 0, 2, st, &handled);  // non-causal, N % 64 == 0
       if (!handled) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
     }
-    if (!handled) e = launch_fwd_fast(a, causal != 0, g_kernel_policy, st, &handled);
+    // d = 128 (and any shape the d = 64 kernels decline): the single-phase kernel, 8 waves
+    // by default (faster than 4 at d = 128: 959 vs 802 TF/s at (1,16,16384,128))
+    if (!handled)
+      e = launch_fwd_fast(a, causal != 0, g_kernel_policy == 0 ? 2 : g_kernel_policy, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");
   }
   return check_hip(launch_fwd_generic(a, dtype == MT_BF16, vec, causal != 0, st),
@@ -173,7 +176,8 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
                           {q, k, v, o, dout, dq, dk, dv});
   if (dtype == MT_BF16 && vec && g_kernel_policy != 1) {
     bool handled = false;
-    const hipError_t e = launch_bwd_bf16(a, causal != 0, (hipStream_t)stream, &handled);
+    const hipError_t e = launch_bwd_bf16(a, causal != 0, g_kernel_policy == 40, (hipStream_t)stream,
+                                         &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }
   return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream),

@@ -153,7 +153,273 @@ __device__ __forceinline__ void dkv_tile(const char* slot, const DkvCtx& c, f32x
     }
   }
 }
+// Software-pipelined bulk iteration of the dK/dV kernel (mask-free tiles t and t+1):
+//   C-init S(t+1), dP(t+1) from the row constants of slot sn;
+//   phase A: 8 x [Q/dO row read (2 ahead), S(t+1) or dP(t+1) MFMA, softmax of 2 scores of t]
+//   phase B: 8 x [Qᵀ/dOᵀ transpose reads (2 ahead), dV(t) or dK(t) MFMA]
+// so tile t's exponentials overlap tile t+1's score products inside one wave.
+__device__ __forceinline__ void dkv_pipe(const char* slot_c, const char* slot_n, const DkvCtx& c,
+                                         const f32x16& Sc, const f32x16& dPc, f32x16& Sn,
+                                         f32x16& dPn, f32x16 (&dK)[2], f32x16 (&dV)[2], float c2,
+                                         int hf) {
+  const bf16* Qrn = (const bf16*)slot_n;
+  const float* nln = (const float*)(Qrn + 4 * kImgQ);
+  const float* ndn = nln + kQT;
+  // per-lane operand bases: one add each, every read then takes an immediate offset
+  const bf16* qr[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qr[ks] = Qrn + c.roff[ks];
+  const bf16* tq[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db) tq[db] = (const bf16*)slot_c + kImgQ + c.toff[db];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 a = *(const float4*)(nln + 8 * g + 4 * hf);
+    const float4 e = *(const float4*)(ndn + 8 * g + 4 * hf);
+    Sn[4 * g] = a.x; Sn[4 * g + 1] = a.y; Sn[4 * g + 2] = a.z; Sn[4 * g + 3] = a.w;
+    dPn[4 * g] = e.x; dPn[4 * g + 1] = e.y; dPn[4 * g + 2] = e.z; dPn[4 * g + 3] = e.w;
+  }
+  bf16x8 af[8];
+#define DKV_AREAD(I_) af[I_] = *(const bf16x8*)(qr[(I_) >> 1] + ((I_) & 1 ? 2 * kImgQ : 0));
+  DKV_AREAD(0)
+  DKV_AREAD(1)
+  bf16x8 pf[2], sf[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i + 2 < 8) DKV_AREAD(i + 2)
+    if (i & 1) dPn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], c.vf[i >> 1], dPn, 0, 0, 0);
+    else Sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], c.kf[i >> 1], Sn, 0, 0, 0);
+#pragma unroll
+    for (int r = 2 * i; r < 2 * i + 2; ++r) {
+      const float e = __builtin_amdgcn_exp2f(Sc[r] * c2);
+      pf[r >> 3][r & 7] = (bf16)e;
+      sf[r >> 3][r & 7] = (bf16)(e * dPc[r]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#undef DKV_AREAD
+  bf16x8 bt[8];
+  // MFMA n: 16-query step s = n/4, d block db = (n/2)%2, dV (even n) or dK (odd n)
+#define DKV_BREAD(N_) bt[N_] = tr_frag(tq[((N_) >> 1) & 1] + (((N_) & 1) ? 0 : 2 * kImgQ), 16 * ((N_) >> 2), 0);
+  DKV_BREAD(0)
+  DKV_BREAD(1)
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    if (n + 2 < 8) DKV_BREAD(n + 2)
+    const int s = n >> 2, db = (n >> 1) & 1;
+    if (n & 1) dK[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bt[n], sf[s], dK[db], 0, 0, 0);
+    else dV[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bt[n], pf[s], dV[db], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#undef DKV_BREAD
+}
+
+// S(t), dP(t) for a mask-free tile (C-init + 8 MFMAs), the pipeline's entry.
+__device__ __forceinline__ void dkv_scores(const char* slot, const DkvCtx& c, f32x16& S, f32x16& dP,
+                                           int hf) {
+  const bf16* Qr = (const bf16*)slot;
+  const bf16* Or = Qr + 2 * kImgQ;
+  const float* nl = (const float*)(Qr + 4 * kImgQ);
+  const float* nd = nl + kQT;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 a = *(const float4*)(nl + 8 * g + 4 * hf);
+    const float4 e = *(const float4*)(nd + 8 * g + 4 * hf);
+    S[4 * g] = a.x; S[4 * g + 1] = a.y; S[4 * g + 2] = a.z; S[4 * g + 3] = a.w;
+    dP[4 * g] = e.x; dP[4 * g + 1] = e.y; dP[4 * g + 2] = e.z; dP[4 * g + 3] = e.w;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Qr + c.roff[ks]), c.kf[ks], S, 0, 0, 0);
+    dP = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Or + c.roff[ks]), c.vf[ks], dP, 0, 0, 0);
+  }
+}
+
+// softmax + dV/dK of a tile whose S, dP are already computed (the pipeline's exit).
+__device__ __forceinline__ void dkv_finish(const char* slot, const DkvCtx& c, const f32x16& S,
+                                           const f32x16& dP, f32x16 (&dK)[2], f32x16 (&dV)[2],
+                                           float c2) {
+  const bf16* Qt = (const bf16*)slot + kImgQ;
+  const bf16* Ot = (const bf16*)slot + 3 * kImgQ;
+  bf16x8 pf[2], sf[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float e = __builtin_amdgcn_exp2f(S[r] * c2);
+    pf[r >> 3][r & 7] = (bf16)e;
+    sf[r >> 3][r & 7] = (bf16)(e * dP[r]);
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      dV[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ot, 16 * s, c.toff[db]), pf[s], dV[db], 0, 0, 0);
+      dK[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qt, 16 * s, c.toff[db]), sf[s], dK[db], 0, 0, 0);
+    }
+}
 }  // namespace
+
+// dK/dV with the software-pipelined bulk loop (3-slot LDS ring: an iteration reads the
+// transposes of tile t and the rows of tile t+1 while tile t+2 is staged).
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16_p(AttnArgs p, int nkb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = logical / nkb, kb = logical % nkb;
+  const int b = bh / p.H, hh = bh % p.H;
+  const int k0 = kb * 128;
+  const int my_k = k0 + wave * 32 + c32;
+  const int wk_lo = k0 + wave * 32;
+
+  DkvCtx c;
+  {
+    const int kr = min(my_k, N - 1);
+    const bf16* krow = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1] + (int64_t)kr * p.sk[2];
+    const bf16* vrow = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1] + (int64_t)kr * p.sv[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      c.kf[ks] = *(const bf16x8*)(krow + 16 * ks + 8 * hf);
+      c.vf[ks] = *(const bf16x8*)(vrow + 16 * ks + 8 * hf);
+      c.roff[ks] = k_swz<D>(c32, 2 * ks + hf);
+    }
+    c.toff[0] = tr_off(lane, 0);
+    c.toff[1] = tr_off(lane, 1);
+  }
+  const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* Og = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int sqn = (int)p.sq[2], son = (int)p.sdo[2];
+  const __amdgpu_buffer_rsrc_t rq = head_rsrc(Qg, N, sqn), ro = head_rsrc(Og, N, son);
+  const int st_r = tid >> 3, st_c = tid & 7;
+  const int goq = (st_r * sqn + st_c * 8) * 2, goo = (st_r * son + st_c * 8) * 2;
+  const int srow = k_swz<D>(st_r, st_c), stri = v_swz<D>(st_r, st_c);
+  const float* nlse = p.lse2 + (int64_t)bh * N;
+  const float* ndel = p.delta + (int64_t)bh * N;
+
+  const int qt0 = CAUSAL ? k0 : 0;
+  const int ntile = N > qt0 ? (N - qt0 + kQT - 1) / kQT : 0;
+  const int ndiag = CAUSAL ? min(ntile, 128 / kQT) : 0;
+  const int nfull = max(ndiag, (N - qt0) / kQT);
+
+  uint4 sq, so;
+  float sv = 0.f;
+#define DKV_LOAD(T_)                                                                     \
+  {                                                                                      \
+    const int qt_ = qt0 + (T_) * kQT;                                                    \
+    sq = bload(rq, goq + qt_ * sqn * 2);                                                 \
+    so = bload(ro, goo + qt_ * son * 2);                                                 \
+    if (tid < 2 * kQT) {                                                                 \
+      const int q_ = qt_ + (tid & (kQT - 1));                                            \
+      sv = q_ < N ? (tid < kQT ? nlse[q_] : ndel[q_]) : 0.f;                             \
+    }                                                                                    \
+  }
+#define DKV_STORE(T_)                                                                    \
+  {                                                                                      \
+    bf16* img = (bf16*)(smem + ((T_) % 3) * kBufQ);                                      \
+    *(uint4*)(img + srow) = sq;                                                          \
+    *(uint4*)(img + kImgQ + stri) = sq;                                                  \
+    *(uint4*)(img + 2 * kImgQ + srow) = so;                                              \
+    *(uint4*)(img + 3 * kImgQ + stri) = so;                                              \
+    if (tid < 2 * kQT) ((float*)(img + 4 * kImgQ))[tid] = sv;                            \
+  }
+#define SLOT(T_) (smem + ((T_) % 3) * kBufQ)
+
+  f32x16 dK[2], dV[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
+  const float c2 = p.scale_log2;
+
+  // prologue: tiles 0 and 1 staged
+  for (int i = 0; i < 2 && i < ntile; ++i) {
+    DKV_LOAD(i)
+    DKV_STORE(i)
+  }
+  __syncthreads();
+  // general step: tile t from scratch (masks, per-wave causal skip); stages tile t+2
+#define DKV_GEN(MASK_, T_)                                                               \
+  {                                                                                      \
+    const int t_ = (T_);                                                                 \
+    const bool st_ = t_ + 2 < ntile;                                                     \
+    if (st_) DKV_LOAD(t_ + 2)                                                            \
+    const int qt_ = qt0 + t_ * kQT;                                                      \
+    if (!(MASK_) || !CAUSAL || qt_ + kQT - 1 >= wk_lo)                                   \
+      dkv_tile<CAUSAL, MASK_>(SLOT(t_), c, dK, dV, c2, qt_, N, my_k, hf);                \
+    if (st_) DKV_STORE(t_ + 2)                                                           \
+    __syncthreads();                                                                     \
+  }
+  int t = 0;
+  for (; t < ndiag; ++t) DKV_GEN(true, t)
+  if (nfull - t >= 2) {
+    // pipelined bulk: S(t) computed ahead; iteration t also computes S(t+1)
+    f32x16 SA, dPA, SB, dPB;
+    dkv_scores(SLOT(t), c, SA, dPA, hf);
+    // ring offsets rotate (current, next, write) without per-iteration modulo arithmetic
+    int oc = (t % 3) * kBufQ, on = ((t + 1) % 3) * kBufQ, ow = ((t + 2) % 3) * kBufQ;
+#define DKV_PIPE(T_, SC_, DPC_, SN_, DPN_)                                               \
+  {                                                                                      \
+    const int t_ = (T_);                                                                 \
+    const bool st_ = t_ + 2 < ntile;                                                     \
+    if (st_) DKV_LOAD(t_ + 2)                                                            \
+    dkv_pipe(smem + oc, smem + on, c, SC_, DPC_, SN_, DPN_, dK, dV, c2, hf);             \
+    if (st_) {                                                                           \
+      bf16* img = (bf16*)(smem + ow);                                                    \
+      *(uint4*)(img + srow) = sq;                                                        \
+      *(uint4*)(img + kImgQ + stri) = sq;                                                \
+      *(uint4*)(img + 2 * kImgQ + srow) = so;                                            \
+      *(uint4*)(img + 3 * kImgQ + stri) = so;                                            \
+      if (tid < 2 * kQT) ((float*)(img + 4 * kImgQ))[tid] = sv;                          \
+    }                                                                                    \
+    __syncthreads();                                                                     \
+    const int o_ = oc;                                                                   \
+    oc = on;                                                                             \
+    on = ow;                                                                             \
+    ow = o_;                                                                             \
+  }
+    for (; t + 2 < nfull; t += 2) {
+      DKV_PIPE(t, SA, dPA, SB, dPB)
+      DKV_PIPE(t + 1, SB, dPB, SA, dPA)
+    }
+    if (t + 1 < nfull) {
+      DKV_PIPE(t, SA, dPA, SB, dPB)
+      ++t;
+      SA = SB;
+      dPA = dPB;
+    }
+#undef DKV_PIPE
+    // last bulk tile: S(t) in SA
+    {
+      const bool st_ = t + 2 < ntile;
+      if (st_) DKV_LOAD(t + 2)
+      dkv_finish(SLOT(t), c, SA, dPA, dK, dV, c2);
+      if (st_) DKV_STORE(t + 2)
+      __syncthreads();
+      ++t;
+    }
+  }
+  for (; t < ntile; ++t) {
+    if (t < nfull) DKV_GEN(false, t) else DKV_GEN(true, t)
+  }
+#undef DKV_GEN
+#undef DKV_LOAD
+#undef DKV_STORE
+#undef SLOT
+
+  if (my_k < N) {
+    bf16* dKg = (bf16*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
+    bf16* dVg = (bf16*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
+    const float sc = p.scale;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = db * 32 + 8 * g + 4 * hf;
+        store4(dKg + col, dK[db][4 * g] * sc, dK[db][4 * g + 1] * sc, dK[db][4 * g + 2] * sc,
+               dK[db][4 * g + 3] * sc, true);
+        store4(dVg + col, dV[db][4 * g], dV[db][4 * g + 1], dV[db][4 * g + 2], dV[db][4 * g + 3], true);
+      }
+  }
+}
 
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16(AttnArgs p, int nkb) {
@@ -458,7 +724,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
 
 // ---------------------------------------------------------------------------------------
 template <bool CAUSAL>
-static hipError_t launch_bwd_bf16_t(const AttnArgs& a, hipStream_t st) {
+static hipError_t launch_bwd_bf16_t(const AttnArgs& a, bool pipe, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.H * a.N;
   hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
@@ -467,8 +733,8 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, hipStream_t st) {
     const int nkb = (a.N + 127) / 128;
     const int64_t nblk = (int64_t)nkb * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-    const size_t smem = 2 * (size_t)kBufQ;
-    auto kfn = fa_bwd_dkv_bf16<CAUSAL>;
+    const size_t smem = (pipe ? 3 : 2) * (size_t)kBufQ;
+    auto kfn = pipe ? fa_bwd_dkv_bf16_p<CAUSAL> : fa_bwd_dkv_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(256), smem, st, a, nkb);
@@ -489,14 +755,14 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, hipStream_t st) {
 
 // bf16, d = 64, every per-head row offset of Q/K/V/dO (plus one tile past N) inside the
 // 31-bit buffer range; otherwise the caller falls back to the generic kernels.
-hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, hipStream_t st, bool* handled) {
+hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, bool pipe, hipStream_t st, bool* handled) {
   *handled = false;
   if (a.d != 64) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   for (const int64_t s : {a.sq[2], a.sk[2], a.sv[2], a.sdo[2]})
     if (((int64_t)a.N + 64) * s * 2 >= lim) return hipSuccess;
   *handled = true;
-  return causal ? launch_bwd_bf16_t<true>(a, st) : launch_bwd_bf16_t<false>(a, st);
+  return causal ? launch_bwd_bf16_t<true>(a, pipe, st) : launch_bwd_bf16_t<false>(a, pipe, st);
 }
 
 }  // namespace mt

@@ -1,0 +1,24 @@
+"""Forward timing for arbitrary (B,H,N,d) shapes and policies (diagnostics).
+usage: python scripts/shape_bench.py B H N d [causal] [policies]"""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "llmsys-project-flashattn_amd"))
+import torch
+from minitorch import _hip
+B, H, N, d = (int(x) for x in sys.argv[1:5])
+causal = len(sys.argv) > 5 and sys.argv[5] == "causal"
+pols = [int(x) for x in sys.argv[6].split(",")] if len(sys.argv) > 6 else [0]
+g = torch.Generator(device="cuda").manual_seed(0)
+q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
+o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
+flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
+for p in pols:
+    _hip.lib().mt_flash_set_kernel_policy(p)
+    for _ in range(2): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(); e0.record()
+    reps = 5
+    for _ in range(reps): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
+    e1.record(); torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    print(f"({B},{H},{N},{d}) causal={causal} policy {p}: {ms:.3f} ms  {flops / ms / 1e9:.1f} TF/s")
+_hip.lib().mt_flash_set_kernel_policy(0)
