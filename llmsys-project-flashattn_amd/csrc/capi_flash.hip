@@ -24,7 +24,9 @@ hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStr
                          bool* handled);
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
-hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, hipStream_t st, bool* handled);
+hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
+                         bool* handled);
+hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, bool pipe, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
@@ -128,17 +130,29 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       handled = true;
     }
     if (g_kernel_policy >= 27 && g_kernel_policy <= 29)
-      e = launch_fwd_v5(a, causal != 0, 2 * (g_kernel_policy - 26), st, &handled);
+      e = launch_fwd_v5(a, causal != 0, 2 * (g_kernel_policy - 26), g_kernel_policy == 27 ? 4 : 0, st,
+                        &handled);
+    if (g_kernel_policy == 31)  // tile loop not unrolled (the pre-unroll default)
+      e = launch_fwd_v5(a, causal != 0, 2, 0, st, &handled);
+    if (g_kernel_policy == 97)  // diagnostics only (wrong results): no scale-and-shift
+      e = launch_fwd_v5(a, causal != 0, 2, 2, st, &handled);
     if (g_kernel_policy >= 91 && g_kernel_policy <= 96 && d == 64 && !causal) {
       e = launch_fwd_v4_ablation(a, g_kernel_policy - 90, st);  // diagnostics only
       handled = true;
     }
     if (g_kernel_policy == 0) {
-      e = launch_fwd_v5(a, causal != 0, 2, st, &handled);  // non-causal, N % 64 == 0
+      e = launch_fwd_v5(a, causal != 0, 2, 4, st, &handled);  // non-causal, N % 64 == 0
       if (!handled) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
     }
-    // d = 128 (and any shape the d = 64 kernels decline): the single-phase kernel, 8 waves
-    // by default (faster than 4 at d = 128: 959 vs 802 TF/s at (1,16,16384,128))
+    // d = 128: the pipelined frozen-reference kernel (fa_fwd_d128.hip). Default: 8 waves for
+    // long non-causal heads, else 4 (1214 vs 1125 TF/s at (8,16,16384,128); 948 vs 892 at
+    // (8,16,4096,128); causal 774 vs 701). 32 / 33 force 8 / 4 waves.
+    if (!handled && (g_kernel_policy == 0 || g_kernel_policy == 32 || g_kernel_policy == 33)) {
+      const int nw = g_kernel_policy == 32 ? 8 : g_kernel_policy == 33 ? 4 : (!causal && N >= 8192) ? 8 : 4;
+      e = launch_fwd_d128(a, causal != 0, nw, st, &handled);
+    }
+    // any shape the kernels above decline: the single-phase kernel, 8 waves by default
+    // (faster than 4 at d = 128: 959 vs 802 TF/s at (1,16,16384,128))
     if (!handled)
       e = launch_fwd_fast(a, causal != 0, g_kernel_policy == 0 ? 2 : g_kernel_policy, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");

@@ -45,10 +45,19 @@ struct Ctx5 {
 };
 
 // Softmax of one 32-key half of a block: pair i (0..7) of the 16 scores of S_half.
+// VAR bit 1 (diagnostic timing builds only, wrong results): no scale-and-shift.
+// (A v_dot2c_f32_bf16 row sum of the bf16-rounded pair was tried as VAR bit 0: slower,
+// 962 vs 978 TF/s, and it failed the 150x spike test; removed.)
+// VAR bit 2: the tile loop unrolled by 4 (see iter in the kernel).
+template <int VAR>
 __device__ __forceinline__ void sm_pair(const f32x16& s, int i, float c2, float nmc, f32x2& acc,
                                         bf16x8 (&pf)[2]) {
   const int j = 2 * i;
-  const f32x2 x = f32x2{s[j], s[j + 1]} * f32x2{c2, c2} + f32x2{nmc, nmc};
+  f32x2 x;
+  if (VAR & 2)
+    x = f32x2{s[j], s[j + 1]};
+  else
+    x = f32x2{s[j], s[j + 1]} * f32x2{c2, c2} + f32x2{nmc, nmc};
   const float e0 = __builtin_amdgcn_exp2f(x[0]);
   const float e1 = __builtin_amdgcn_exp2f(x[1]);
   acc += f32x2{e0, e1};
@@ -72,7 +81,7 @@ __device__ __forceinline__ bf16x8 vread(const bf16* sv, const int (&vo)[2], int 
 
 // QKᵀ phase (8 MFMAs into S) interleaved with the softmax of s_in (8 pairs) -> pf.
 // SOFT = false: MFMAs only.
-template <bool SOFT, int kAhead>
+template <bool SOFT, int kAhead, int VAR>
 __device__ __forceinline__ void phase_qk(const bf16* sk, const int (&ko)[4], const bf16x8 (&qf)[4],
                                          f32x16 (&S)[2], const f32x16& s_in, float c2, float nmc,
                                          f32x2& acc, bf16x8 (&pf)[2]) {
@@ -84,14 +93,14 @@ __device__ __forceinline__ void phase_qk(const bf16* sk, const int (&ko)[4], con
     if (i + kAhead < 8) kf[i + kAhead] = kread(sk, ko, i + kAhead);
     S[i >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i & 3], (i & 3) ? S[i >> 2] : f32x16{},
                                                        0, 0, 0);
-    if (SOFT) sm_pair(s_in, i, c2, nmc, acc, pf);
+    if (SOFT) sm_pair<VAR>(s_in, i, c2, nmc, acc, pf);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // PV phase (8 MFMAs into O with P fragments p_lo (keys 0-31) and p_hi (keys 32-63))
 // interleaved with the softmax of s_in (8 pairs) -> pf.
-template <bool SOFT, int kAhead>
+template <bool SOFT, int kAhead, int VAR>
 __device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32x16 (&O)[2],
                                          const bf16x8 (&p_lo)[2], const bf16x8 (&p_hi)[2],
                                          const f32x16& s_in, float c2, float nmc, f32x2& acc,
@@ -104,7 +113,7 @@ __device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32
     if (n + kAhead < 8) vf[n + kAhead] = vread(sv, vo, n + kAhead);
     const bf16x8& p = (n >> 2) ? p_hi[(n >> 1) & 1] : p_lo[(n >> 1) & 1];
     O[n & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[n], p, O[n & 1], 0, 0, 0);
-    if (SOFT) sm_pair(s_in, n, c2, nmc, acc, pf);
+    if (SOFT) sm_pair<VAR>(s_in, n, c2, nmc, acc, pf);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -128,8 +137,8 @@ __device__ __forceinline__ float lane_pair_sum(float x) {
 
 }  // namespace
 
-// AHEAD: LDS operand reads are issued this many MFMAs ahead of their use.
-template <int AHEAD>
+// AHEAD: LDS operand reads are issued this many MFMAs ahead of their use. VAR: see sm_pair.
+template <int AHEAD, int VAR>
 __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* const sK = (bf16*)smem_raw;          // [kKSlots][TILE]
@@ -211,8 +220,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
       for (int ks = 0; ks < 4; ++ks) ko[ks] = c.koff[ks];
       f32x2 dummy = {0.f, 0.f};
       bf16x8 dpf[2];
-      phase_qk<false, AHEAD>(sK, ko, qfA, SA, SA[0], c2, 0.f, dummy, dpf);
-      phase_qk<false, AHEAD>(sK, ko, qfB, SB, SB[0], c2, 0.f, dummy, dpf);
+      phase_qk<false, AHEAD, VAR>(sK, ko, qfA, SA, SA[0], c2, 0.f, dummy, dpf);
+      phase_qk<false, AHEAD, VAR>(sK, ko, qfB, SB, SB[0], c2, 0.f, dummy, dpf);
     }
     mA = row_max32(SA[0], SA[1]);
     mB = row_max32(SB[0], SB[1]);
@@ -220,17 +229,21 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
     f32x2 accA = {0.f, 0.f}, accB = {0.f, 0.f};
     bf16x8 pB0[2], pB1[2], pA0[2], pA1[2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sm_pair(SB[0], i, c2, nmcB, accB, pB0);
+    for (int i = 0; i < 8; ++i) sm_pair<VAR>(SB[0], i, c2, nmcB, accB, pB0);
 #pragma unroll
     for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
 
     // iteration t: K(t) in slot t%4, K(t+1) in slot (t+1)%4, V(t) in slot t%2; stages
     // K(t+2) -> slot (t+2)%4 and V(t+1) -> slot (t+1)%2. The last tile is peeled.
-    for (int t = 0; t + 1 < ntiles; ++t) {
+    // One iteration; s0 = t & 3. With VAR bit 2 the loop is unrolled by the K ring size so
+    // that every slot offset is a compile-time constant (folded into the LDS instructions'
+    // immediate offsets instead of per-iteration address VALU).
+    auto iter = [&](int t, int s0) __attribute__((always_inline)) {
+      __builtin_amdgcn_sched_barrier(0);
       load5(rK, rk, c.kgo, (t + 2) * ktile_b);
       load5(rV, rv, c.vgo, (t + 1) * vtile_b);
       int koA[4], koB[4], vo[2];
-      const int kslA = (t & 3) * TILE, kslB = ((t + 1) & 3) * TILE, vsl = (t & 1) * TILE;
+      const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & 1) * TILE;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         koA[ks] = c.koff[ks] + kslA;
@@ -238,14 +251,23 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
       }
       vo[0] = c.voff[0] + vsl;
       vo[1] = c.voff[1] + vsl;
-      phase_qk<true, AHEAD>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);             // P1
-      phase_pv<true, AHEAD>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);         // P2
-      phase_qk<true, AHEAD>(sK, koB, qfB, SB, SA[1], c2, nmcA, accA, pA1);             // P3
-      phase_pv<true, AHEAD>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0);         // P4
-      store5(sK + ((t + 2) & 3) * TILE, rK, c.kso);
-      store5(sV + ((t + 1) & 1) * TILE, rV, c.vso);
+      phase_qk<true, AHEAD, VAR>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);             // P1
+      phase_pv<true, AHEAD, VAR>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);         // P2
+      phase_qk<true, AHEAD, VAR>(sK, koB, qfB, SB, SA[1], c2, nmcA, accA, pA1);             // P3
+      phase_pv<true, AHEAD, VAR>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0);         // P4
+      store5(sK + ((s0 + 2) & 3) * TILE, rK, c.kso);
+      store5(sV + ((s0 + 1) & 1) * TILE, rV, c.vso);
       __syncthreads();
-    }
+    };
+    int t = 0;
+    if (VAR & 4)
+      for (; t + 4 < ntiles; t += 4) {
+        iter(t, 0);
+        iter(t + 1, 1);
+        iter(t + 2, 2);
+        iter(t + 3, 3);
+      }
+    for (; t + 1 < ntiles; ++t) iter(t, t & 3);
     {
       const int t = ntiles - 1;
       int koA[4], vo[2];
@@ -253,13 +275,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
       for (int ks = 0; ks < 4; ++ks) koA[ks] = c.koff[ks] + (t & 3) * TILE;
       vo[0] = c.voff[0] + (t & 1) * TILE;
       vo[1] = c.voff[1] + (t & 1) * TILE;
-      phase_qk<true, AHEAD>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);
-      phase_pv<true, AHEAD>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);
+      phase_qk<true, AHEAD, VAR>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);
+      phase_pv<true, AHEAD, VAR>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sm_pair(SA[1], i, c2, nmcA, accA, pA1);
+      for (int i = 0; i < 8; ++i) sm_pair<VAR>(SA[1], i, c2, nmcA, accA, pA1);
       f32x2 d2 = {0.f, 0.f};
       bf16x8 dpf[2];
-      phase_pv<false, AHEAD>(sV, vo, OA, pA0, pA1, SA[0], c2, 0.f, d2, dpf);
+      phase_pv<false, AHEAD, VAR>(sV, vo, OA, pA0, pA1, SA[0], c2, 0.f, d2, dpf);
     }
     lA = lane_pair_sum(accA[0] + accA[1]);
     lB = lane_pair_sum(accB[0] + accB[1]);
@@ -289,7 +311,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
         f32x16 S[2];
         f32x2 acc = {0.f, 0.f};
         bf16x8 plo[2], phi[2], dpf[2];
-        phase_qk<false, AHEAD>(sK, ko, blk ? qfB : qfA, S, S[0], c2, 0.f, acc, dpf);
+        phase_qk<false, AHEAD, VAR>(sK, ko, blk ? qfB : qfA, S, S[0], c2, 0.f, acc, dpf);
         float& m = blk ? mB : mA;
         float& l = blk ? pB : pA;
         f32x16(&O)[2] = blk ? OB : OA;
@@ -306,11 +328,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
         }
         const float nmc = -(m * c2);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm_pair(S[0], i, c2, nmc, acc, plo);
+        for (int i = 0; i < 8; ++i) sm_pair<VAR & 1>(S[0], i, c2, nmc, acc, plo);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm_pair(S[1], i, c2, nmc, acc, phi);
+        for (int i = 0; i < 8; ++i) sm_pair<VAR & 1>(S[1], i, c2, nmc, acc, phi);
         l += acc[0] + acc[1];
-        phase_pv<false, AHEAD>(sV, vo, O, plo, phi, S[0], c2, 0.f, acc, dpf);
+        phase_pv<false, AHEAD, VAR>(sV, vo, O, plo, phi, S[0], c2, 0.f, acc, dpf);
       }
     }
     lA = lane_pair_sum(pA);
@@ -342,7 +364,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
 
 // d = 64, non-causal, N a multiple of 64 (no masked tile) and at least two tiles, and all
 // per-head K/V offsets (two tiles past N) inside the 31-bit buffer range.
-hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, hipStream_t st, bool* handled) {
+hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
+                         bool* handled) {
   *handled = false;
   if (a.d != 64 || causal || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
@@ -350,7 +373,11 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, hipStream_t 
     return hipSuccess;
   *handled = true;
   const size_t smem = (size_t)(kKSlots + kVSlots) * TILE * sizeof(bf16);
-  auto kfn = ahead >= 6 ? fa_fwd_bf16_v5<6> : ahead >= 4 ? fa_fwd_bf16_v5<4> : fa_fwd_bf16_v5<2>;
+  auto kfn = var == 4   ? fa_fwd_bf16_v5<2, 4>
+             : var == 2 ? fa_fwd_bf16_v5<2, 2>
+             : ahead >= 6 ? fa_fwd_bf16_v5<6, 0>
+             : ahead >= 4 ? fa_fwd_bf16_v5<4, 0>
+                          : fa_fwd_bf16_v5<2, 0>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
   const int nqb = (a.N + kBQ - 1) / kBQ;

@@ -264,8 +264,11 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # 21/22 v4 (fa_fwd_v4.hip: frozen first-tile reference, 4-/8-wave), 23/24 the same with
 # packed-f32 scale and row sum (8-/4-wave), 25/26 4-wave with staging one iteration deeper
 # (packed / scalar), 27/28/29 v5 (fa_fwd_v5.hip: two skewed query blocks per wave, LDS reads
-# 2/4/6 MFMAs ahead; non-causal N % 64 == 0 only, other shapes fall back)
-FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29)
+# 2/4/6 MFMAs ahead; non-causal N % 64 == 0 only, other shapes fall back; 27 and the
+# default unroll the tile loop by 4, 31 does not), 32/33 the d = 128 kernel (fa_fwd_d128.hip,
+# 8 / 4 waves; the d = 128 default)
+FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32,
+                 33)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
@@ -290,14 +293,15 @@ def test_fast_policies_vs_oracle(torch_dev, policy):
         _hip.lib().mt_flash_set_kernel_policy(0)
 
 
+@pytest.mark.parametrize("d", [64, 128])
 @pytest.mark.parametrize("policy", FAST_POLICIES)
-def test_huge_spike_fallback(torch_dev, policy):
+def test_huge_spike_fallback(torch_dev, policy, d):
     """A score far above the first tile's max (> 64 log2 units): v4's bulk loop leaves the
     safe range and its workgroup recomputes the block with the deferred-max path; every
     other variant rescales. Rows without the spike are unaffected."""
     from minitorch import _hip
     torch = torch_dev
-    B, H, N, d = 1, 1, 1024, 64
+    B, H, N = 1, 1, 1024
     rng = np.random.default_rng(23)
     q = rng.standard_normal((B, H, N, d)).astype(np.float32) * 0.3
     k = rng.standard_normal((B, H, N, d)).astype(np.float32) * 0.3
@@ -318,14 +322,15 @@ def test_huge_spike_fallback(torch_dev, policy):
         _hip.lib().mt_flash_set_kernel_policy(0)
 
 
+@pytest.mark.parametrize("d", [64, 128])
 @pytest.mark.parametrize("policy", FAST_POLICIES)
-def test_spiked_rescale(torch_dev, policy):
+def test_spiked_rescale(torch_dev, policy, d):
     """Force the deferred-rescale branch (rule: a rare data-dependent branch needs its own
     test): one key row aligned with one query row makes that row's max jump past the
     2^8 threshold at a chosen tile, after several tiles at a low max."""
     from minitorch import _hip
     torch = torch_dev
-    B, H, N, d = 1, 2, 700, 64
+    B, H, N = 1, 2, 700
     rng = np.random.default_rng(21)
     q = rng.standard_normal((B, H, N, d)).astype(np.float32) * 0.3
     k = rng.standard_normal((B, H, N, d)).astype(np.float32) * 0.3
