@@ -277,6 +277,17 @@ def main():
         extra["c2_fp32_fwd_ms"] = round(c2_ms, 4)
         extra["c2_fp32_fwd_tflops"] = round(fwd_flops(*c2) / (c2_ms * 1e-3) / 1e12, 2)
         extra["c2_fp32_frac_of_f32_peak"] = round(extra["c2_fp32_fwd_tflops"] / PEAK_F32_TFLOPS, 4)
+        del q2, k2, v2
+        # config 4's per-GPU shard at 8 GPUs: (8,16,16384,128) bf16 forward (1/8 of B=64)
+        c4 = (8, 16, 16384, 128)
+        q4, k4, v4 = (make_inputs(torch, c4, torch.bfloat16, s, 0) for s in (8, 9, 10))
+        o4 = torch.empty_like(q4)
+        m4 = torch.empty(c4[:3], dtype=torch.float32, device="cuda")
+        l4 = torch.empty_like(m4)
+        c4_ms = time_kernel(torch, lambda: _hip.flash_fwd(q4, k4, v4, False, out=o4, m=m4, l=l4), 5, 1)
+        extra["c4_shard_bf16_fwd_ms"] = round(c4_ms, 3)
+        extra["c4_shard_bf16_fwd_tflops"] = round(fwd_flops(*c4) / (c4_ms * 1e-3) / 1e12, 2)
+        del q4, k4, v4, o4, m4, l4
         result["extra"] = extra
 
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -190,6 +190,8 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
                           {q, k, v, o, dout, dq, dk, dv});
   if (dtype == MT_BF16 && vec && g_kernel_policy != 1) {
     bool handled = false;
+    // 40: software-pipelined dK/dV (A/B variant). An in-wave interleaved dQ tile was
+    // measured 1.7 % slower than the plain tile and removed (profiles/r1_ab_bwd_dq.txt).
     const hipError_t e = launch_bwd_bf16(a, causal != 0, g_kernel_policy == 40, (hipStream_t)stream,
                                          &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");

@@ -564,7 +564,7 @@ struct DqCtx {
 
 template <bool CAUSAL, bool MASK>
 __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16 (&dQ)[2], float c2,
-                                        float nlq, float del, int k0, int N, int my_q, int hf) {
+                                        float nlq, const f32x16& dinit, int k0, int N, int my_q, int hf) {
   const bf16* Kr = (const bf16*)slot;
   const bf16* Kt = Kr + kImgK;
   const bf16* Vr = Kr + 2 * kImgK;
@@ -575,8 +575,9 @@ __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16
     for (int kb = 0; kb < 2; ++kb) {
       S[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Kr + kb * 32 * D + c.roff[ks]),
                                                       c.qf[ks], ks ? S[kb] : f32x16{}, 0, 0, 0);
+      // dP chain starts from −δ (row constant as the initial accumulator): dP' = dP − δ
       dP[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Vr + kb * 32 * D + c.roff[ks]),
-                                                       c.of[ks], ks ? dP[kb] : f32x16{}, 0, 0, 0);
+                                                       c.of[ks], ks ? dP[kb] : dinit, 0, 0, 0);
     }
   if (MASK) {
 #pragma unroll
@@ -592,7 +593,7 @@ __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[kb][r], c2, nlq));
-      dP[kb][r] = pv * (dP[kb][r] - del);
+      dP[kb][r] = pv * dP[kb][r];
     }
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb)
@@ -605,6 +606,7 @@ __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16
                                                          dQ[db], 0, 0, 0);
     }
 }
+
 }  // namespace
 
 template <bool CAUSAL>
@@ -679,6 +681,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
   }
 
   f32x16 dQ[2] = {f32x16{}, f32x16{}};
+  f32x16 dinit;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dinit[r] = -del;  // = −δ
   const float c2 = p.scale_log2;
   DQ_LOAD(0)
   DQ_STORE(0)
@@ -689,7 +694,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
     const bool more_ = t_ + 1 < ntile;                                                   \
     if (more_) DQ_LOAD(t_ + 1)                                                           \
     if (!(MASK_) || !CAUSAL || t_ * kKT <= wq_hi)                                        \
-      dq_tile<CAUSAL, MASK_>(smem + (SLOT_) * kBufK, c, dQ, c2, nlq, del, t_ * kKT, N,   \
+      dq_tile<CAUSAL, MASK_>(smem + (SLOT_) * kBufK, c, dQ, c2, nlq, dinit, t_ * kKT, N, \
                              my_q, hf);                                                  \
     if (more_) DQ_STORE((SLOT_) ^ 1)                                                     \
     __syncthreads();                                                                     \
