@@ -141,7 +141,10 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       handled = true;
     }
     if (g_kernel_policy == 0) {
-      e = launch_fwd_v5(a, causal != 0, 2, 4, st, &handled);  // non-causal, N % 64 == 0
+      // v5 for non-causal N % 64 == 0. Causal v5 (policies 27-31) is correct but slower
+      // than the 4-wave v4 (790 vs 811 TF/s at C3, 813 vs 836 at (1,16,16384,64)):
+      // 256-query workgroups balance the triangle worse and its diagonal tiles run serially.
+      if (!causal) e = launch_fwd_v5(a, false, 2, 4, st, &handled);
       if (!handled) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
     }
     // d = 128: the pipelined frozen-reference kernel (fa_fwd_d128.hip). Default: 8 waves for

@@ -1,5 +1,6 @@
-// FlashAttention forward, bf16 MFMA kernel v5 (d = 64, non-causal, N % 64 == 0):
-// two 32-query blocks per wave, skewed by half a tile.
+// FlashAttention forward, bf16 MFMA kernel v5 (d = 64, N % 64 == 0): two 32-query blocks
+// per wave, skewed by half a tile. Causal: the pipelined loop covers the key tiles below
+// the workgroup's first query; the four diagonal tiles run a serial masked path.
 //
 // v4 gives each wave one 32-query block and relies on the second wave of its SIMD to
 // overlap one wave's softmax with the other's MFMAs. v5 gives each wave two blocks, A and
@@ -138,7 +139,7 @@ __device__ __forceinline__ float lane_pair_sum(float x) {
 }  // namespace
 
 // AHEAD: LDS operand reads are issued this many MFMAs ahead of their use. VAR: see sm_pair.
-template <int AHEAD, int VAR>
+template <int AHEAD, int VAR, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* const sK = (bf16*)smem_raw;          // [kKSlots][TILE]
@@ -151,9 +152,12 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
   const int nblk = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
   const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  const int bh = logical / nqb, qb = logical % nqb;
+  const int bh = logical / nqb;
+  const int qb = CAUSAL ? nqb - 1 - logical % nqb : logical % nqb;  // causal: heaviest first
   const int b = bh / p.H, hh = bh % p.H;
-  const int qA = qb * kBQ + wave * 64 + c32;  // this lane's query in block A; B = qA + 32
+  const int q0 = qb * kBQ;
+  const int qw = q0 + wave * 64;              // first query of this wave (block A; B = +32)
+  const int qA = qw + c32;                    // this lane's query in block A; B = qA + 32
 
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
   const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
@@ -195,14 +199,22 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
     }
   }
   const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
-  const int ntiles = N / kBK;
+  // Tiles: non-causal, all N / 64 and every one mask-free. Causal: the keys below the
+  // workgroup's last query; the first q0 / 64 tiles are mask-free for all its queries, the
+  // last four hold the diagonal (serial path, masked per block, skipped where fully masked).
+  const int ntiles = CAUSAL ? min(N, q0 + kBQ) / kBK : N / kBK;
+  const int nbulk = CAUSAL ? q0 / kBK : ntiles;
   const float c2 = p.scale_log2;
 
   f32x16 OA[2], OB[2];
-  float mA, mB, lA, lB;
+  float mA = -INFINITY, mB = -INFINITY;
+  float pA = 0.f, pB = 0.f;  // this lane's share of each block's row sum
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
 
-  // ---- pass 0: the pipelined loop with the frozen first-tile reference ----------------
-  {
+  // ---- pass 0: the pipelined loop with the frozen first-tile reference over the tiles
+  //      [0, nbulk), mask-free for every query of the workgroup ---------------------------
+  if (!CAUSAL || nbulk >= 2) {  // non-causal: the launcher guarantees N >= 128
     uint4 rK[LPT], rV[LPT];
     load5(rK, rk, c.kgo, 0);
     load5(rV, rv, c.vgo, 0);
@@ -261,15 +273,15 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
     };
     int t = 0;
     if (VAR & 4)
-      for (; t + 4 < ntiles; t += 4) {
+      for (; t + 4 < nbulk; t += 4) {
         iter(t, 0);
         iter(t + 1, 1);
         iter(t + 2, 2);
         iter(t + 3, 3);
       }
-    for (; t + 1 < ntiles; ++t) iter(t, t & 3);
+    for (; t + 1 < nbulk; ++t) iter(t, t & 3);
     {
-      const int t = ntiles - 1;
+      const int t = nbulk - 1;
       int koA[4], vo[2];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) koA[ks] = c.koff[ks] + (t & 3) * TILE;
@@ -283,22 +295,20 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
       bf16x8 dpf[2];
       phase_pv<false, AHEAD, VAR>(sV, vo, OA, pA0, pA1, SA[0], c2, 0.f, d2, dpf);
     }
-    lA = lane_pair_sum(accA[0] + accA[1]);
-    lB = lane_pair_sum(accB[0] + accB[1]);
+    pA = accA[0] + accA[1];
+    pB = accB[0] + accB[1];
   }
 
-  // ---- pass 1 (rare): serial deferred-max recompute for the whole workgroup -----------
-  if (__syncthreads_or(!(lA <= kLimit) || !(lB <= kLimit))) {
-    mA = mB = -INFINITY;
-    float pA = 0.f, pB = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
+  // ---- serial path: tiles [t0, ntiles) with the per-tile deferred-max bookkeeping ------
+  // (causal diagonal tiles after the bulk; the whole range if the bulk was too short or a
+  // lane's row-sum share left 2^64, in which case the workgroup starts over)
+  auto serial = [&](int t0) {
     int ko[4], vo[2];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) ko[ks] = c.koff[ks];
     vo[0] = c.voff[0];
     vo[1] = c.voff[1];
-    for (int t = 0; t < ntiles; ++t) {
+    for (int t = t0; t < ntiles; ++t) {
       uint4 rK[LPT], rV[LPT];
       load5(rK, rk, c.kgo, t * ktile_b);
       load5(rV, rv, c.vgo, t * vtile_b);
@@ -308,10 +318,20 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
       __syncthreads();
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk) {
+        const int qf0 = qw + 32 * blk;  // the block's first query (wave-uniform)
+        if (CAUSAL && qf0 + 31 < t * kBK) continue;  // every key of the tile is masked
         f32x16 S[2];
         f32x2 acc = {0.f, 0.f};
         bf16x8 plo[2], phi[2], dpf[2];
         phase_qk<false, AHEAD, VAR>(sK, ko, blk ? qfB : qfA, S, S[0], c2, 0.f, acc, dpf);
+        if (CAUSAL && t * kBK + kBK - 1 > qf0) {
+          const int q = qf0 + c32;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (t * kBK + kb * 32 + acc_row(r, hf) > q) S[kb][r] = -INFINITY;
+        }
         float& m = blk ? mB : mA;
         float& l = blk ? pB : pA;
         f32x16(&O)[2] = blk ? OB : OA;
@@ -328,16 +348,25 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
         }
         const float nmc = -(m * c2);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm_pair<VAR & 1>(S[0], i, c2, nmc, acc, plo);
+        for (int i = 0; i < 8; ++i) sm_pair<VAR>(S[0], i, c2, nmc, acc, plo);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm_pair<VAR & 1>(S[1], i, c2, nmc, acc, phi);
+        for (int i = 0; i < 8; ++i) sm_pair<VAR>(S[1], i, c2, nmc, acc, phi);
         l += acc[0] + acc[1];
         phase_pv<false, AHEAD, VAR>(sV, vo, O, plo, phi, S[0], c2, 0.f, acc, dpf);
       }
     }
-    lA = lane_pair_sum(pA);
-    lB = lane_pair_sum(pB);
+  };
+  const int tdone = (!CAUSAL || nbulk >= 2) ? nbulk : 0;
+  if (__syncthreads_or(!(pA <= kLimit) || !(pB <= kLimit))) {
+    mA = mB = -INFINITY;
+    pA = pB = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
+    serial(0);
+  } else if (CAUSAL && tdone < ntiles) {
+    serial(tdone);
   }
+  const float lA = lane_pair_sum(pA), lB = lane_pair_sum(pB);
 
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
@@ -362,22 +391,27 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
   }
 }
 
-// d = 64, non-causal, N a multiple of 64 (no masked tile) and at least two tiles, and all
-// per-head K/V offsets (two tiles past N) inside the 31-bit buffer range.
+// d = 64, N a multiple of 64 (no ragged tile) and at least two tiles, and all per-head K/V
+// offsets (two tiles past N) inside the 31-bit buffer range. Causal runs the mask-free
+// prefix through the pipelined loop and the diagonal tiles through the serial path.
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
                          bool* handled) {
   *handled = false;
-  if (a.d != 64 || causal || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
+  if (a.d != 64 || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
   const size_t smem = (size_t)(kKSlots + kVSlots) * TILE * sizeof(bf16);
-  auto kfn = var == 4   ? fa_fwd_bf16_v5<2, 4>
-             : var == 2 ? fa_fwd_bf16_v5<2, 2>
-             : ahead >= 6 ? fa_fwd_bf16_v5<6, 0>
-             : ahead >= 4 ? fa_fwd_bf16_v5<4, 0>
-                          : fa_fwd_bf16_v5<2, 0>;
+  void (*kfn)(AttnArgs, int);
+  if (causal)
+    kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;
+  else
+    kfn = var == 4   ? fa_fwd_bf16_v5<2, 4, false>
+          : var == 2 ? fa_fwd_bf16_v5<2, 2, false>
+          : ahead >= 6 ? fa_fwd_bf16_v5<6, 0, false>
+          : ahead >= 4 ? fa_fwd_bf16_v5<4, 0, false>
+                       : fa_fwd_bf16_v5<2, 0, false>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
   const int nqb = (a.N + kBQ - 1) / kBQ;

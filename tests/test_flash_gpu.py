@@ -280,7 +280,8 @@ def test_fast_policies_vs_oracle(torch_dev, policy):
     rng = np.random.default_rng(31)
     try:
         _hip.lib().mt_flash_set_kernel_policy(policy)
-        for (B, H, N, d) in ((1, 3, 1000, 64), (2, 1, 517, 128), (1, 2, 64, 64)):
+        for (B, H, N, d) in ((1, 3, 1000, 64), (2, 1, 517, 128), (1, 2, 64, 64), (1, 2, 1216, 64),
+                             (1, 1, 1536, 128)):
             q, k, v = (A.bf16_round(rng.standard_normal((B, H, N, d)).astype(np.float32))
                        for _ in range(3))
             for causal in (False, True):
