@@ -39,6 +39,9 @@ PEAK_HBM_GBPS = 8000.0
 WORKLOAD = (8, 16, 4096, 64)
 
 
+PREWARM_S = 0.3  # untimed steady-clock ramp before the timed region (seconds)
+
+
 def fwd_flops(B, H, N, d, causal=False):
     f = 4.0 * B * H * N * N * d
     return f / 2 if causal else f
@@ -165,6 +168,14 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # untimed clock ramp: keep stepping until PREWARM_S of GPU work has run, so the timed
+    # region starts at the steady-state clock whatever W the caller passes (the first
+    # launches on a cold GPU run up to 30 % slower: profiles/r1e_kernel_stats.csv max)
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < PREWARM_S:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -203,6 +214,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "prewarm_s": PREWARM_S,
         "ms_per_step": round(ms_per_step, 5),
         "higher_is_better": True,
         "scaling": "weak",

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1 \
   && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
   && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
-       -- python3 bench.py --steps 20 --warmup 5 --no-cpu > gpurun_out/prof_$TAG.log 2>&1 \
+       -- python3 bench.py --steps 100 --warmup 20 --no-cpu > gpurun_out/prof_$TAG.log 2>&1 \
   && timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 rc=$?
 tail -3 gpurun_out/tests_$TAG.log
