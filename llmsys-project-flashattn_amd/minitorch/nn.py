@@ -58,9 +58,25 @@ def GELU(input: Tensor) -> Tensor:  # noqa: N802,A002 - reference name
     return 0.5 * input * (1 + (math.sqrt(2 / math.pi) * (input + 0.044715 * (input ** 3))).tanh())
 
 
+_CLASS_IDS: dict = {}
+
+
 def one_hot(input: Tensor, num_classes: int) -> Tensor:  # noqa: A002
-    idx = input.to_numpy().astype(np.int64)
-    return tensor_from_numpy(np.eye(num_classes, dtype=np.float32)[idx], backend=input.backend)
+    """(*) integer-valued indices -> (*, num_classes) one-hot rows.
+
+    The reference builds ``np.eye(num_classes)[idx]`` on the host and copies it in
+    (minitorch/nn.py:212-222): at config 5 (4992 rows x 10000 classes) that is 200 MB built
+    and transferred per call, about half of a training step. Here it is one broadcast
+    ``==`` of the indices against a cached 0..num_classes-1 row on the tensor's own
+    backend (a device zip kernel on the HIP backend). Same values, same shape."""
+    be = input.backend
+    key = (num_classes, id(be))
+    ids = _CLASS_IDS.get(key)
+    if ids is None:
+        ids = tensor_from_numpy(np.arange(num_classes, dtype=np.float32), backend=be)
+        _CLASS_IDS[key] = ids
+    shape = tuple(input.shape)
+    return input.contiguous().view(*shape, 1) == ids.view(*([1] * len(shape)), num_classes)
 
 
 def logsumexp(input: Tensor, dim: int) -> Tensor:  # noqa: A002

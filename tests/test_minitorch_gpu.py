@@ -49,6 +49,23 @@ def test_generic_ops(mt):
     np.testing.assert_allclose(p.contiguous().to_numpy(), x.transpose(2, 0, 1))
 
 
+def test_one_hot_and_softmax_loss(mt):
+    """nn.one_hot (device broadcast ==) equals the reference's np.eye(C)[idx]
+    (minitorch/nn.py:212-222), and softmax_loss equals log-sum-exp minus the picked logit."""
+    minitorch, B = mt
+    rng = np.random.default_rng(3)
+    idx = rng.integers(0, 37, (6, 5))
+    oh = minitorch.nn.one_hot(minitorch.tensor_from_numpy(idx.astype(np.float32), B), 37).to_numpy()
+    np.testing.assert_array_equal(oh, np.eye(37, dtype=np.float32)[idx])
+    logits = rng.standard_normal((9, 37)).astype(np.float32)
+    y = rng.integers(0, 37, 9)
+    loss = minitorch.nn.softmax_loss(minitorch.tensor_from_numpy(logits, B),
+                                     minitorch.tensor_from_numpy(y.astype(np.float32), B)).to_numpy()
+    m = logits.max(1, keepdims=True)
+    ref = (np.log(np.exp(logits - m).sum(1)) + m[:, 0]) - logits[np.arange(9), y]
+    np.testing.assert_allclose(loss, ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("shapes", [((5, 7), (7, 3)), ((4, 33, 65), (4, 65, 70)),
                                     ((2, 3, 17, 8), (2, 3, 8, 40)), ((1, 64, 96), (3, 96, 5))])
 def test_matmul(mt, shapes):
