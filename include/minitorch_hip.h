@@ -119,6 +119,12 @@ int mt_matmul_f32(float* c, const float* a, const float* b, int64_t batch, int64
                   int64_t K, const int64_t* a_strides, const int64_t* b_strides,
                   const int64_t* c_strides, void* stream);
 
+/* out[0..n) <- U[0,1) from a stateless counter-based hash of (seed, index). Replaces the
+ * host draws of the reference's dropout paths (minitorch/nn.py dropout via
+ * tensor_functions.rand, modules_basic.py Dropout via np.random.binomial), which build and
+ * copy a host mask per call. */
+int mt_rand_uniform(float* out, int64_t n, uint64_t seed, void* stream);
+
 /* ---- reference-compatible host-pointer wrappers (companion + combine) ----- */
 /* reference src/softmax_kernel.cu:233 (stream: hipStream_t) */
 void launch_attn_softmax(float* inp, const float* attn_mask, int batch_size, int nhead,

@@ -225,6 +225,23 @@ static int check_dims(int d) {
 
 using namespace mt;
 
+// ---- counter-based uniform RNG ---------------------------------------------------------
+// u[i] = top 24 bits of splitmix64(seed + golden·(i+1)) / 2^24, in [0, 1). Stateless: a
+// launch is reproducible from (seed, n) and any element is independent of the grid.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ void rand_uniform_kernel(float* out, int64_t n, uint64_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = mix64(seed + 0x9e3779b97f4a7c15ull * (uint64_t)(i + 1));
+    out[i] = (float)(h >> 40) * (1.0f / 16777216.0f);
+  }
+}
+
 extern "C" {
 
 int mt_tensor_map(int fn, float* out, const int64_t* out_shape, const int64_t* out_strides,
@@ -295,6 +312,15 @@ int mt_matmul_f32(float* c, const float* a, const float* b, int64_t batch, int64
   dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64), (unsigned)batch);
   hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
   return check_hip(hipGetLastError(), "mt_matmul_f32");
+}
+
+int mt_rand_uniform(float* out, int64_t n, uint64_t seed, void* stream) {
+  if (n < 0) return set_error("mt_rand_uniform: n = %lld", (long long)n);
+  if (n == 0) return 0;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(rand_uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     out, n, seed);
+  return check_hip(hipGetLastError(), "mt_rand_uniform");
 }
 
 }  // extern "C"

@@ -50,6 +50,7 @@ _PROTOS = {
     "mt_tensor_reduce": (_int, [_int, _vp, _i64p, _i64p, _vp, _i64p, _i64p, _int, _int,
                                 ctypes.c_float, _vp]),
     "mt_matmul_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _i64p, _i64p, _vp]),
+    "mt_rand_uniform": (_int, [_vp, _i64, ctypes.c_uint64, _vp]),
     "launch_attn_softmax": (None, [_fp, _fp, _int, _int, _int, _int, ctypes.c_bool, _vp]),
     "launch_attn_softmax_bw": (None, [_fp, _fp, _int, _int, _vp]),
     "launch_layernorm": (None, [_fp] * 6 + [_int, _int, _vp]),

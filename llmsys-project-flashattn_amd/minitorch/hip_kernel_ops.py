@@ -174,6 +174,16 @@ class HipKernelOps(TensorOps):
             return out.view(M, N)
         return out
 
+    @staticmethod
+    def rand_uniform(out: Tensor, seed: int) -> Tensor:
+        """Fill the dense fp32 ``out`` with U[0,1) on the device (counter-based hash of
+        (seed, index)); the reference draws dropout randomness on the host
+        (tensor_functions.rand, modules_basic.py Dropout)."""
+        assert out._tensor.is_dense()
+        _hip.check(_hip.lib().mt_rand_uniform(_ptr(out), out.size, seed & 0xFFFFFFFFFFFFFFFF,
+                                              _stream()), "rand_uniform")
+        return out
+
     # ---- fused kernels -------------------------------------------------------------------
     @staticmethod
     def attn_softmax_fw(inp: Tensor, mask: Optional[Tensor], mask_future: bool = False) -> Tensor:

@@ -8,7 +8,7 @@ import numpy as np
 from .module import Module, Parameter
 from .nn import one_hot
 from .tensor import Tensor
-from .tensor_functions import ones, tensor_from_numpy, zeros
+from .tensor_functions import rand, ones, tensor_from_numpy, zeros
 
 
 class Embedding(Module):
@@ -34,8 +34,11 @@ class Dropout(Module):
     def forward(self, x: Tensor) -> Tensor:
         if self.p_dropout == 0 or not self.training:
             return x
-        mask = np.random.binomial(1, 1 - self.p_dropout, x.shape).astype(np.float32)
-        return (x * tensor_from_numpy(mask, backend=x.backend)) / (1 - self.p_dropout)
+        # keep with probability 1 - p, scale by 1 / (1 - p) (reference modules_basic.py
+        # Dropout, which draws the mask with np.random.binomial on the host); here the
+        # uniform draw is on the device when the backend has one
+        keep = rand(x.shape, backend=x.backend) > self.p_dropout
+        return (x * keep) / (1 - self.p_dropout)
 
 
 class Linear(Module):

@@ -387,6 +387,13 @@ def ones(shape: UserShape, backend=None):
 def rand(shape: UserShape, backend=None, requires_grad: bool = False):
     from .tensor import Tensor
     backend = _backend_or_raise(backend)
+    if getattr(backend, "rand_uniform", None) is not None:
+        # device draw; the seed comes from NumPy's global generator so np.random.seed()
+        # still makes a run reproducible
+        t = zeros(shape, backend=backend)
+        backend.rand_uniform(t, int(np.random.randint(0, 2**63 - 1, dtype=np.int64)))
+        t.requires_grad_(requires_grad)
+        return t
     vals = np.array([random.random() for _ in range(int(np.prod(shape)))], dtype=datatype)
     t = Tensor.make(vals, tuple(shape), backend=backend)
     t._type_(backend)

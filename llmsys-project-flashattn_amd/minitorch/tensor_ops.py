@@ -108,6 +108,8 @@ class TensorBackend:
         self.max_reduce = ops.reduce(operators.max, -1e9)
         self.matrix_multiply = ops.matrix_multiply
         self.cuda = ops.cuda
+        # optional device RNG (HipKernelOps.rand_uniform); None -> host draws
+        self.rand_uniform = getattr(ops, "rand_uniform", None)
         # fused kernels
         self.attn_softmax_fw = ops.attn_softmax_fw
         self.attn_softmax_bw = ops.attn_softmax_bw

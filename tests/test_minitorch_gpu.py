@@ -66,6 +66,28 @@ def test_one_hot_and_softmax_loss(mt):
     np.testing.assert_allclose(loss, ref, rtol=1e-5, atol=1e-5)
 
 
+def test_device_rand_and_dropout(mt):
+    """mt_rand_uniform: U[0,1) moments, reproducible per seed; Dropout keeps ~(1-p) of the
+    entries, each scaled by 1/(1-p) (reference modules_basic.py Dropout semantics)."""
+    minitorch, B = mt
+    t = minitorch.zeros((1000, 1000), backend=B)
+    B.rand_uniform(t, 1234)
+    u = t.to_numpy()
+    assert u.min() >= 0.0 and u.max() < 1.0
+    assert abs(u.mean() - 0.5) < 2e-3 and abs(u.var() - 1 / 12) < 2e-3
+    t2 = minitorch.zeros((1000, 1000), backend=B)
+    B.rand_uniform(t2, 1234)
+    np.testing.assert_array_equal(t2.to_numpy(), u)
+    B.rand_uniform(t2, 1235)
+    assert (t2.to_numpy() != u).mean() > 0.99
+    x = np.full((64, 513), 2.0, dtype=np.float32)
+    drop = minitorch.Dropout(0.25)
+    y = drop(minitorch.tensor_from_numpy(x, B)).to_numpy()
+    kept = y != 0
+    assert abs(kept.mean() - 0.75) < 0.02
+    np.testing.assert_allclose(y[kept], 2.0 / 0.75, rtol=1e-6)
+
+
 @pytest.mark.parametrize("shapes", [((5, 7), (7, 3)), ((4, 33, 65), (4, 65, 70)),
                                     ((2, 3, 17, 8), (2, 3, 8, 40)), ((1, 64, 96), (3, 96, 5))])
 def test_matmul(mt, shapes):
