@@ -106,7 +106,12 @@ def _torch():
 
 
 def stream_ptr(device=None) -> int:
+    """The current torch stream of `device` (default: the current device) as a raw
+    hipStream_t. Uses the raw-stream accessor when present (no Stream object per call)."""
     torch = _torch()
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if raw is not None and (device is None or isinstance(device, int)):
+        return raw(torch.cuda.current_device() if device is None else device)
     return torch.cuda.current_stream(device).cuda_stream
 
 

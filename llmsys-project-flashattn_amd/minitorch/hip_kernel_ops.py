@@ -21,6 +21,7 @@ kernels take (batch, head, seq) strides, so no ``.contiguous()`` copy is made.
 from __future__ import annotations
 
 import ctypes
+import functools
 from typing import Callable, Optional
 
 import numpy as np
@@ -32,9 +33,24 @@ from .tensor_data import TensorData, shape_broadcast
 from .tensor_ops import MapProto, TensorOps
 
 
-def _i64(vals) -> ctypes.Array:
-    vals = [int(v) for v in vals]
+@functools.lru_cache(maxsize=4096)
+def _i64_cached(vals: tuple) -> ctypes.Array:
     return (ctypes.c_int64 * max(1, len(vals)))(*vals)
+
+
+def _i64(vals) -> ctypes.Array:
+    """int64 array argument; shapes/strides repeat every step, so the ctypes arrays are
+    cached by value (the callee only reads them)."""
+    return _i64_cached(tuple(int(v) for v in vals))
+
+
+def _out(like: Tensor, shape) -> Tensor:
+    """Uninitialised dense fp32 device output (every kernel below writes all of it)."""
+    import torch
+    shape = tuple(int(s) for s in shape)
+    size = int(np.prod(shape)) if shape else 1
+    st = torch.empty(size, dtype=torch.float32, device="cuda")
+    return Tensor(TensorData(st, shape), backend=like.backend)
 
 
 def _dev(t: Tensor) -> Tensor:
@@ -83,7 +99,7 @@ class HipKernelOps(TensorOps):
 
         def ret(a: Tensor, out: Optional[Tensor] = None) -> Tensor:
             if out is None:
-                out = a.zeros(a.shape)
+                out = _out(a, a.shape)
             _hip.check(_hip.lib().mt_tensor_map(
                 fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides), out.dims,
                 _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims, _stream()), "map")
@@ -109,7 +125,7 @@ class HipKernelOps(TensorOps):
 
         def ret(a: Tensor, b: Tensor) -> Tensor:
             shape = shape_broadcast(a.shape, b.shape)
-            out = a.zeros(shape)
+            out = _out(a, shape)
             _hip.check(_hip.lib().mt_tensor_zip(
                 fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides), out.dims,
                 _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims,
@@ -125,7 +141,7 @@ class HipKernelOps(TensorOps):
         def ret(a: Tensor, dim: int) -> Tensor:
             shape = list(a.shape)
             shape[dim] = 1
-            out = a.zeros(tuple(shape))
+            out = _out(a, shape)
             _hip.check(_hip.lib().mt_tensor_reduce(
                 fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides),
                 _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims, int(dim),
@@ -166,7 +182,7 @@ class HipKernelOps(TensorOps):
 
         a, sa = batch_view(a)
         b, sb = batch_view(b)
-        out = a.zeros(lead + (M, N))
+        out = _out(a, lead + (M, N))
         so = (M * N, N, 1)
         _hip.check(_hip.lib().mt_matmul_f32(_ptr(out), _ptr(a), _ptr(b), batch, M, N, K,
                                             _i64(sa), _i64(sb), _i64(so), _stream()), "matmul")

@@ -74,7 +74,12 @@ class Tensor:
 
     def _ensure_tensor(self, b: TensorLike) -> "Tensor":
         if isinstance(b, (int, float, np.floating, np.integer)):
-            return Tensor.make([float(b)], (1,), backend=self.backend, device=self.backend.cuda)
+            if self.backend.cuda:
+                # filled on the device (no synchronous host-to-device copy per scalar)
+                import torch
+                st = torch.full((1,), float(b), dtype=torch.float32, device="cuda")
+                return Tensor(TensorData(st, (1,)), backend=self.backend)
+            return Tensor.make([float(b)], (1,), backend=self.backend)
         b._type_(self.backend)
         return b
 
