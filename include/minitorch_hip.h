@@ -114,10 +114,15 @@ int mt_tensor_zip(int fn, float* out, const int64_t* out_shape, const int64_t* o
 int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t* out_strides,
                      const float* a, const int64_t* a_shape, const int64_t* a_strides, int dims,
                      int reduce_dim, float start, void* stream);
-/* c[b] = a[b] @ b[b]; strides are (batch, row, col) triples, batch stride 0 broadcasts. */
+/* c[b] = a[b] @ b[b]; strides are (batch, row, col) triples, batch stride 0 broadcasts.
+ * (reference combine.cu:148-210 MatrixMultiply; cuda_kernel_ops.py:340-437). Plain layouts
+ * (a unit stride in one dim of each operand) run on rocBLAS sgemm_strided_batched, others
+ * on the library's own fp32 MFMA kernel. */
 int mt_matmul_f32(float* c, const float* a, const float* b, int64_t batch, int64_t M, int64_t N,
                   int64_t K, const int64_t* a_strides, const int64_t* b_strides,
                   const int64_t* c_strides, void* stream);
+/* 0 (default): rocBLAS for plain layouts; 1: the library's own GEMM kernel only (A/B). */
+void mt_set_gemm_backend(int backend);
 
 /* out[0..n) <- U[0,1) from a stateless counter-based hash of (seed, index). Replaces the
  * host draws of the reference's dropout paths (minitorch/nn.py dropout via

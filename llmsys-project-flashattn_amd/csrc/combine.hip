@@ -9,11 +9,18 @@
 //
 // MI355X design: device pointers and stream-ordered launches (the reference copies
 // every operand host<->device per call), int64 indexing, grid-stride loops sized for
-// 256 CUs, a contiguous fast path, wave-per-row reductions for long reduce axes, and a
-// batched GEMM on the exact-fp32 MFMA (v_mfma_f32_32x32x2_f32) through LDS tiles.
+// 256 CUs, a contiguous fast path, wave-per-row reductions for long reduce axes. The
+// batched matmul is a plain library GEMM: rocBLAS sgemm_strided_batched whenever each
+// operand has a unit stride in one of its two dims (every Linear / attention / one-hot
+// product of the model), else our own exact-fp32 MFMA kernel (v_mfma_f32_32x32x2_f32)
+// for arbitrary strides.
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <mutex>
+
+#include <rocblas/rocblas.h>
 
 #include "../../include/minitorch_hip.h"
 #include "fa_common.h"
@@ -297,12 +304,73 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   return check_hip(hipGetLastError(), "mt_tensor_reduce");
 }
 
+static int g_gemm_backend = 0;  // 0: rocBLAS where the layout allows, 1: own kernel only
+
+void mt_set_gemm_backend(int backend) { g_gemm_backend = backend; }
+
+// One rocBLAS handle per device, created on first use.
+static rocblas_handle blas_handle() {
+  static std::mutex mu;
+  static rocblas_handle handles[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!handles[dev] && rocblas_create_handle(&handles[dev]) != rocblas_status_success) {
+    handles[dev] = nullptr;
+  }
+  return handles[dev];
+}
+
+// Row-major C[M,N] = A[M,K]·B[K,N] as column-major Cᵀ = Bᵀ·Aᵀ. Returns false (caller
+// falls back) when a layout has no unit stride or a leading dimension rocBLAS rejects.
+static bool gemm_rocblas(float* c, const float* a, const float* b, int64_t batch, int64_t M,
+                         int64_t N, int64_t K, const int64_t* sa, const int64_t* sb,
+                         const int64_t* sc, hipStream_t st, rocblas_status* status) {
+  const int64_t lim = 0x7fffffff;
+  if (M > lim || N > lim || K > lim || batch > lim) return false;
+  // Normalise the strides of size-1 dims (free) towards a usable layout.
+  int64_t sam = sa[1], sak = sa[2], sbk = sb[1], sbn = sb[2], scm = sc[1], scn = sc[2];
+  if (N == 1) scn = 1;
+  if (M == 1) { scm = std::max<int64_t>(N, 1); if (sak == 1) sam = std::max<int64_t>(sam, K); }
+  if (K == 1) { sak = 1; sbk = std::max<int64_t>(N, sbk); }
+  if (sc[0] < 0 || scn != 1 || scm < N) return false;
+  // first operand: our B as an N x K column-major matrix (op N) or its K x N transpose
+  rocblas_operation opb;
+  int64_t ldb;
+  if (sbn == 1 && sbk >= N) { opb = rocblas_operation_none; ldb = sbk; }
+  else if (sbk == 1 && sbn >= K) { opb = rocblas_operation_transpose; ldb = sbn; }
+  else return false;
+  // second operand: our A as a K x M column-major matrix (op N) or its M x K transpose
+  rocblas_operation opa;
+  int64_t lda;
+  if (sak == 1 && sam >= K) { opa = rocblas_operation_none; lda = sam; }
+  else if (sam == 1 && sak >= M) { opa = rocblas_operation_transpose; lda = sak; }
+  else return false;
+  if (lda > lim || ldb > lim || scm > lim || sa[0] < 0 || sb[0] < 0) return false;
+  rocblas_handle h = blas_handle();
+  if (!h) return false;
+  rocblas_set_stream(h, st);
+  const float alpha = 1.f, beta = 0.f;
+  *status = rocblas_sgemm_strided_batched(h, opb, opa, (rocblas_int)N, (rocblas_int)M, (rocblas_int)K,
+                                          &alpha, b, (rocblas_int)ldb, sb[0], a, (rocblas_int)lda, sa[0],
+                                          &beta, c, (rocblas_int)scm, sc[0], (rocblas_int)batch);
+  return true;
+}
+
 int mt_matmul_f32(float* c, const float* a, const float* b, int64_t batch, int64_t M, int64_t N,
                   int64_t K, const int64_t* a_strides, const int64_t* b_strides,
                   const int64_t* c_strides, void* stream) {
   if (batch <= 0 || M <= 0 || N <= 0 || K <= 0)
     return set_error("mt_matmul_f32: bad sizes %lld %lld %lld %lld", (long long)batch,
                      (long long)M, (long long)N, (long long)K);
+  if (g_gemm_backend == 0) {
+    rocblas_status rs = rocblas_status_success;
+    if (gemm_rocblas(c, a, b, batch, M, N, K, a_strides, b_strides, c_strides, (hipStream_t)stream, &rs)) {
+      if (rs != rocblas_status_success)
+        return set_error("mt_matmul_f32: rocblas_sgemm_strided_batched: %s", rocblas_status_to_string(rs));
+      return check_hip(hipGetLastError(), "mt_matmul_f32(rocblas)");
+    }
+  }
   if (batch > 65535) return set_error("mt_matmul_f32: batch %lld > 65535", (long long)batch);
   GemmArgs g;
   g.a = a; g.b = b; g.c = c; g.M = M; g.N = N; g.K = K;

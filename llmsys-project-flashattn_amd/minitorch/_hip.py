@@ -51,6 +51,7 @@ _PROTOS = {
                                 ctypes.c_float, _vp]),
     "mt_matmul_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _i64p, _i64p, _vp]),
     "mt_rand_uniform": (_int, [_vp, _i64, ctypes.c_uint64, _vp]),
+    "mt_set_gemm_backend": (None, [_int]),
     "launch_attn_softmax": (None, [_fp, _fp, _int, _int, _int, _int, ctypes.c_bool, _vp]),
     "launch_attn_softmax_bw": (None, [_fp, _fp, _int, _int, _vp]),
     "launch_layernorm": (None, [_fp] * 6 + [_int, _int, _vp]),

@@ -90,7 +90,19 @@ def test_device_rand_and_dropout(mt):
 
 @pytest.mark.parametrize("shapes", [((5, 7), (7, 3)), ((4, 33, 65), (4, 65, 70)),
                                     ((2, 3, 17, 8), (2, 3, 8, 40)), ((1, 64, 96), (3, 96, 5))])
-def test_matmul(mt, shapes):
+@pytest.mark.parametrize("gemm_backend", [0, 1])
+def test_matmul(mt, shapes, gemm_backend):
+    """Batched matmul on both GEMM back ends (0: rocBLAS for plain layouts with the own
+    kernel for the rest, 1: own kernel only), plain, transposed and fully strided operands."""
+    from minitorch import _hip
+    _hip.lib().mt_set_gemm_backend(gemm_backend)
+    try:
+        _matmul_case(mt, shapes)
+    finally:
+        _hip.lib().mt_set_gemm_backend(0)
+
+
+def _matmul_case(mt, shapes):
     minitorch, B = mt
     rng = np.random.default_rng(1)
     x = rng.standard_normal(shapes[0]).astype(np.float32)
@@ -104,6 +116,11 @@ def test_matmul(mt, shapes):
     order[-1], order[-2] = order[-2], order[-1]
     out2 = xt.permute(*order) @ minitorch.tensor_from_numpy(w, B)
     np.testing.assert_allclose(out2.to_numpy(), ref, rtol=1e-5, atol=1e-5)
+    if x.ndim == 3:
+        # no unit stride in either matrix dim: (M, K, batch) storage viewed as (batch, M, K)
+        xs = minitorch.tensor_from_numpy(np.ascontiguousarray(np.moveaxis(x, 0, -1)), B)
+        out3 = xs.permute(2, 0, 1) @ minitorch.tensor_from_numpy(w, B)
+        np.testing.assert_allclose(out3.to_numpy(), ref, rtol=1e-5, atol=1e-5)
 
 
 def _mha_case(minitorch, backend, batch_size, queries_len, n_embd, num_heads, causal, use_flash,
