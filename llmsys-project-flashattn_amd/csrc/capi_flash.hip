@@ -27,7 +27,7 @@ hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
                          bool* handled);
 hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled);
-hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, bool pipe, hipStream_t st, bool* handled);
+hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
 
@@ -195,8 +195,14 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
     bool handled = false;
     // 40: software-pipelined dK/dV (A/B variant). An in-wave interleaved dQ tile was
     // measured 1.7 % slower than the plain tile and removed (profiles/r1_ab_bwd_dq.txt).
-    const hipError_t e = launch_bwd_bf16(a, causal != 0, g_kernel_policy == 40, (hipStream_t)stream,
-                                         &handled);
+    // dK/dV variants: 0 32-query steps, 1 software-pipelined (policy 40), 2 64-query steps
+    // (policy 42). Default: 2 non-causal (1.912 vs 1.952 ms at C3), 0 causal (1.12 vs
+    // 1.31 ms: the masked diagonal steps spill in the 64-query form); policy 43 forces 0.
+    const int variant = g_kernel_policy == 40   ? 1
+                        : g_kernel_policy == 42 ? 2
+                        : g_kernel_policy == 43 ? 0
+                                                : (causal ? 0 : 2);
+    const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }
   return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream),

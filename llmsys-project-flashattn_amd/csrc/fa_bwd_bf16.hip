@@ -549,6 +549,147 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16(AttnArgs p, int nkb) {
   }
 }
 
+// dK/dV with 64-query steps: each barrier-to-barrier step stages two 32-query sub-tiles
+// (two ring sub-slots) and runs dkv_tile on both, halving the barriers and global-load
+// round trips per MFMA against the 32-query kernel above (A/B variant).
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16_q64(AttnArgs p, int nkb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = logical / nkb, kb = logical % nkb;
+  const int b = bh / p.H, hh = bh % p.H;
+  const int k0 = kb * 128;
+  const int my_k = k0 + wave * 32 + c32;
+  const int wk_lo = k0 + wave * 32;
+
+  DkvCtx c;
+  {
+    const int kr = min(my_k, N - 1);
+    const bf16* krow = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1] + (int64_t)kr * p.sk[2];
+    const bf16* vrow = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1] + (int64_t)kr * p.sv[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      c.kf[ks] = *(const bf16x8*)(krow + 16 * ks + 8 * hf);
+      c.vf[ks] = *(const bf16x8*)(vrow + 16 * ks + 8 * hf);
+      c.roff[ks] = k_swz<D>(c32, 2 * ks + hf);
+    }
+    c.toff[0] = tr_off(lane, 0);
+    c.toff[1] = tr_off(lane, 1);
+  }
+
+  // Staging: thread -> (row, chunk) of each 32 x 64 sub-tile of Q and dO (one chunk per
+  // sub-tile per tensor); 128 threads move the row constants of both sub-tiles.
+  const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* Og = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int sqn = (int)p.sq[2], son = (int)p.sdo[2];
+  const __amdgpu_buffer_rsrc_t rq = head_rsrc(Qg, N, sqn), ro = head_rsrc(Og, N, son);
+  const int st_r = tid >> 3, st_c = tid & 7;
+  const int goq = (st_r * sqn + st_c * 8) * 2, goo = (st_r * son + st_c * 8) * 2;
+  const int srow = k_swz<D>(st_r, st_c), stri = v_swz<D>(st_r, st_c);
+  const float* nlse = p.lse2 + (int64_t)bh * N;
+  const float* ndel = p.delta + (int64_t)bh * N;
+
+  constexpr int kStep = 2 * kQT;
+  const int qt0 = CAUSAL ? k0 : 0;
+  const int nstep = N > qt0 ? (N - qt0 + kStep - 1) / kStep : 0;
+
+  uint4 sq[2], so[2];
+  float sv = 0.f;
+#define DKV2_LOAD(T_)                                                                    \
+  {                                                                                      \
+    const int qs_ = qt0 + (T_) * kStep;                                                  \
+    _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
+      sq[u] = bload(rq, goq + (qs_ + u * kQT) * sqn * 2);                                \
+      so[u] = bload(ro, goo + (qs_ + u * kQT) * son * 2);                                \
+    }                                                                                    \
+    if (tid < 4 * kQT) {                                                                 \
+      const int q_ = qs_ + (tid >> 6) * kQT + (tid & (kQT - 1));                         \
+      sv = q_ < N ? ((tid & kQT) == 0 ? nlse[q_] : ndel[q_]) : 0.f;                      \
+    }                                                                                    \
+  }
+#define DKV2_STORE(SLOT_)                                                                \
+  {                                                                                      \
+    _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
+      bf16* img = (bf16*)(smem + (2 * (SLOT_) + u) * kBufQ);                             \
+      *(uint4*)(img + srow) = sq[u];                                                     \
+      *(uint4*)(img + kImgQ + stri) = sq[u];                                             \
+      *(uint4*)(img + 2 * kImgQ + srow) = so[u];                                         \
+      *(uint4*)(img + 3 * kImgQ + stri) = so[u];                                         \
+    }                                                                                    \
+    if (tid < 4 * kQT)                                                                   \
+      ((float*)((bf16*)(smem + (2 * (SLOT_) + (tid >> 6)) * kBufQ) + 4 * kImgQ))[tid & 63] = sv; \
+  }
+
+  f32x16 dK[2], dV[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
+  const float c2 = p.scale_log2;
+
+  if (nstep > 0) {
+    DKV2_LOAD(0)
+    DKV2_STORE(0)
+  }
+  __syncthreads();
+  // steps: [0, nhead) causal diagonal (masked), [nhead, nfull) mask-free, [nfull, nstep)
+  // ragged tail (masked)
+  const int nhead = CAUSAL ? min(nstep, 128 / kStep) : 0;
+  const int nfull = max(nhead, (N - qt0) / kStep);
+#define DKV2_STEP(MASK_, SLOT_, T_)                                                      \
+  {                                                                                      \
+    const int t_ = (T_);                                                                 \
+    const bool more_ = t_ + 1 < nstep;                                                   \
+    if (more_) DKV2_LOAD(t_ + 1)                                                         \
+    _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
+      const int qt_ = qt0 + t_ * kStep + u * kQT;                                        \
+      if (!(MASK_) || (qt_ < N && (!CAUSAL || qt_ + kQT - 1 >= wk_lo)))                 \
+        dkv_tile<CAUSAL, MASK_>(smem + (2 * (SLOT_) + u) * kBufQ, c, dK, dV, c2, qt_, N, \
+                                my_k, hf);                                               \
+    }                                                                                    \
+    if (more_) DKV2_STORE((SLOT_) ^ 1)                                                   \
+    __syncthreads();                                                                     \
+  }
+  int t = 0;
+  for (; t < nhead; ++t) {
+    if (t & 1) DKV2_STEP(true, 1, t) else DKV2_STEP(true, 0, t)
+  }
+  if ((t & 1) && t < nfull) {
+    DKV2_STEP(false, 1, t)
+    ++t;
+  }
+  for (; t + 1 < nfull; t += 2) {
+    DKV2_STEP(false, 0, t)
+    DKV2_STEP(false, 1, t + 1)
+  }
+  for (; t < nstep; ++t) {
+    if (t < nfull) {
+      if (t & 1) DKV2_STEP(false, 1, t) else DKV2_STEP(false, 0, t)
+    } else {
+      if (t & 1) DKV2_STEP(true, 1, t) else DKV2_STEP(true, 0, t)
+    }
+  }
+#undef DKV2_STEP
+#undef DKV2_LOAD
+#undef DKV2_STORE
+
+  if (my_k < N) {
+    bf16* dKg = (bf16*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
+    bf16* dVg = (bf16*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
+    const float sc = p.scale;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = db * 32 + 8 * g + 4 * hf;
+        store4(dKg + col, dK[db][4 * g] * sc, dK[db][4 * g + 1] * sc, dK[db][4 * g + 2] * sc,
+               dK[db][4 * g + 3] * sc, true);
+        store4(dVg + col, dV[db][4 * g], dV[db][4 * g + 1], dV[db][4 * g + 2], dV[db][4 * g + 3], true);
+      }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // dQ. Workgroup = 4 waves = 128 queries; 64-key tiles.
 namespace {
@@ -729,7 +870,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
 
 // ---------------------------------------------------------------------------------------
 template <bool CAUSAL>
-static hipError_t launch_bwd_bf16_t(const AttnArgs& a, bool pipe, hipStream_t st) {
+static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.H * a.N;
   hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
@@ -738,8 +879,10 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, bool pipe, hipStream_t st
     const int nkb = (a.N + 127) / 128;
     const int64_t nblk = (int64_t)nkb * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-    const size_t smem = (pipe ? 3 : 2) * (size_t)kBufQ;
-    auto kfn = pipe ? fa_bwd_dkv_bf16_p<CAUSAL> : fa_bwd_dkv_bf16<CAUSAL>;
+    const size_t smem = (variant == 1 ? 3 : variant == 2 ? 4 : 2) * (size_t)kBufQ;
+    auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
+               : variant == 2 ? fa_bwd_dkv_bf16_q64<CAUSAL>
+                              : fa_bwd_dkv_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(256), smem, st, a, nkb);
@@ -760,14 +903,14 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, bool pipe, hipStream_t st
 
 // bf16, d = 64, every per-head row offset of Q/K/V/dO (plus one tile past N) inside the
 // 31-bit buffer range; otherwise the caller falls back to the generic kernels.
-hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, bool pipe, hipStream_t st, bool* handled) {
+hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled) {
   *handled = false;
   if (a.d != 64) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   for (const int64_t s : {a.sq[2], a.sk[2], a.sv[2], a.sdo[2]})
     if (((int64_t)a.N + 64) * s * 2 >= lim) return hipSuccess;
   *handled = true;
-  return causal ? launch_bwd_bf16_t<true>(a, pipe, st) : launch_bwd_bf16_t<false>(a, pipe, st);
+  return causal ? launch_bwd_bf16_t<true>(a, variant, st) : launch_bwd_bf16_t<false>(a, variant, st);
 }
 
 }  // namespace mt
