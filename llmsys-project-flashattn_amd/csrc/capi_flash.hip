@@ -136,6 +136,11 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       e = launch_fwd_v5(a, causal != 0, 2, 0, st, &handled);
     if (g_kernel_policy == 97)  // diagnostics only (wrong results): no scale-and-shift
       e = launch_fwd_v5(a, causal != 0, 2, 2, st, &handled);
+    if (g_kernel_policy >= 80 && g_kernel_policy <= 86 && !causal) {
+      // diagnostics only (wrong results): unrolled v5 minus one component (fa_fwd_v5.hip)
+      static const int kAbl[7] = {12, 28, 4, 68, 132, 260, 6};  // 82 = the default (see v5)
+      e = launch_fwd_v5(a, false, 2, kAbl[g_kernel_policy - 80], st, &handled);
+    }
     if (g_kernel_policy >= 91 && g_kernel_policy <= 96 && d == 64 && !causal) {
       e = launch_fwd_v4_ablation(a, g_kernel_policy - 90, st);  // diagnostics only
       handled = true;

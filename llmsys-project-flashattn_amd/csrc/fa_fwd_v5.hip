@@ -50,6 +50,10 @@ struct Ctx5 {
 // (A v_dot2c_f32_bf16 row sum of the bf16-rounded pair was tried as VAR bit 0: slower,
 // 962 vs 978 TF/s, and it failed the 150x spike test; removed.)
 // VAR bit 2: the tile loop unrolled by 4 (see iter in the kernel).
+// Diagnostic ablation bits (timing only, wrong results; policies 80-86): 8 no K/V staging,
+// 16 no barrier either, 64 no Vᵀ operand reads, 128 no exponential, 256 no row-sum add.
+// (Replacing the K operand reads with Q fragments is not a valid ablation: the QKᵀ
+// products become loop-invariant and the compiler hoists them out of the loop.)
 template <int VAR>
 __device__ __forceinline__ void sm_pair(const f32x16& s, int i, float c2, float nmc, f32x2& acc,
                                         bf16x8 (&pf)[2]) {
@@ -59,9 +63,9 @@ __device__ __forceinline__ void sm_pair(const f32x16& s, int i, float c2, float 
     x = f32x2{s[j], s[j + 1]};
   else
     x = f32x2{s[j], s[j + 1]} * f32x2{c2, c2} + f32x2{nmc, nmc};
-  const float e0 = __builtin_amdgcn_exp2f(x[0]);
-  const float e1 = __builtin_amdgcn_exp2f(x[1]);
-  acc += f32x2{e0, e1};
+  const float e0 = (VAR & 128) ? x[0] : __builtin_amdgcn_exp2f(x[0]);
+  const float e1 = (VAR & 128) ? x[1] : __builtin_amdgcn_exp2f(x[1]);
+  if (!(VAR & 256)) acc += f32x2{e0, e1};
   pf[j >> 3][j & 7] = (bf16)e0;
   pf[j >> 3][(j & 7) + 1] = (bf16)e1;
 }
@@ -108,10 +112,10 @@ __device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32
                                          bf16x8 (&pf)[2]) {
   bf16x8 vf[8];
 #pragma unroll
-  for (int n = 0; n < kAhead; ++n) vf[n] = vread(sv, vo, n);
+  for (int n = 0; n < kAhead; ++n) vf[n] = (VAR & 64) ? p_lo[n & 1] : vread(sv, vo, n);
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
-    if (n + kAhead < 8) vf[n + kAhead] = vread(sv, vo, n + kAhead);
+    if (n + kAhead < 8) vf[n + kAhead] = (VAR & 64) ? p_hi[n & 1] : vread(sv, vo, n + kAhead);
     const bf16x8& p = (n >> 2) ? p_hi[(n >> 1) & 1] : p_lo[(n >> 1) & 1];
     O[n & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[n], p, O[n & 1], 0, 0, 0);
     if (SOFT) sm_pair<VAR>(s_in, n, c2, nmc, acc, pf);
@@ -252,8 +256,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
     // immediate offsets instead of per-iteration address VALU).
     auto iter = [&](int t, int s0) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
-      load5(rK, rk, c.kgo, (t + 2) * ktile_b);
-      load5(rV, rv, c.vgo, (t + 1) * vtile_b);
+      if (!(VAR & 8)) {
+        load5(rK, rk, c.kgo, (t + 2) * ktile_b);
+        load5(rV, rv, c.vgo, (t + 1) * vtile_b);
+      }
       int koA[4], koB[4], vo[2];
       const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & 1) * TILE;
 #pragma unroll
@@ -267,9 +273,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
       phase_pv<true, AHEAD, VAR>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);         // P2
       phase_qk<true, AHEAD, VAR>(sK, koB, qfB, SB, SA[1], c2, nmcA, accA, pA1);             // P3
       phase_pv<true, AHEAD, VAR>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0);         // P4
-      store5(sK + ((s0 + 2) & 3) * TILE, rK, c.kso);
-      store5(sV + ((s0 + 1) & 1) * TILE, rV, c.vso);
-      __syncthreads();
+      if (!(VAR & 8)) {
+        store5(sK + ((s0 + 2) & 3) * TILE, rK, c.kso);
+        store5(sV + ((s0 + 1) & 1) * TILE, rV, c.vso);
+      }
+      if (!(VAR & 16)) __syncthreads();
     };
     int t = 0;
     if (VAR & 4)
@@ -406,6 +414,13 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
   void (*kfn)(AttnArgs, int);
   if (causal)
     kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;
+  else if (var >= 8)  // diagnostic ablations
+    kfn = var == 12    ? fa_fwd_bf16_v5<2, 12, false>
+          : var == 28  ? fa_fwd_bf16_v5<2, 28, false>
+          : var == 68  ? fa_fwd_bf16_v5<2, 68, false>
+          : var == 132 ? fa_fwd_bf16_v5<2, 132, false>
+          : var == 260 ? fa_fwd_bf16_v5<2, 260, false>
+                       : fa_fwd_bf16_v5<2, 6, false>;
   else
     kfn = var == 4   ? fa_fwd_bf16_v5<2, 4, false>
           : var == 2 ? fa_fwd_bf16_v5<2, 2, false>
