@@ -132,8 +132,14 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
     if (g_kernel_policy >= 27 && g_kernel_policy <= 29)
       e = launch_fwd_v5(a, causal != 0, 2 * (g_kernel_policy - 26), g_kernel_policy == 27 ? 4 : 0, st,
                         &handled);
+    if (g_kernel_policy == 38 && !causal)  // 4 waves, register staging (the previous default)
+      e = launch_fwd_v5(a, false, 2, 4, st, &handled);
     if (g_kernel_policy == 31)  // tile loop not unrolled (the pre-unroll default)
       e = launch_fwd_v5(a, causal != 0, 2, 0, st, &handled);
+    if (g_kernel_policy == 35 && !causal)  // LDS-DMA staging
+      e = launch_fwd_v5(a, false, 2, 1028, st, &handled);
+    if ((g_kernel_policy == 36 || g_kernel_policy == 37) && !causal)  // 8 waves (37: + LDS-DMA)
+      e = launch_fwd_v5(a, false, 2, g_kernel_policy == 36 ? 2048 + 4 : 2048 + 1028, st, &handled);
     if (g_kernel_policy == 97)  // diagnostics only (wrong results): no scale-and-shift
       e = launch_fwd_v5(a, causal != 0, 2, 2, st, &handled);
     if (g_kernel_policy >= 80 && g_kernel_policy <= 86 && !causal) {
@@ -149,7 +155,9 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       // v5 for non-causal N % 64 == 0. Causal v5 (policies 27-31) is correct but slower
       // than the 4-wave v4 (790 vs 811 TF/s at C3, 813 vs 836 at (1,16,16384,64)):
       // 256-query workgroups balance the triangle worse and its diagonal tiles run serially.
-      if (!causal) e = launch_fwd_v5(a, false, 2, 4, st, &handled);
+      // Non-causal default: 8 waves per workgroup with LDS-DMA K/V staging (policy 37:
+      // 993 vs 967 TF/s for the 4-wave register-staged form, profiles/r1_ab_v5_nw8.txt).
+      if (!causal) e = launch_fwd_v5(a, false, 2, 2048 + 1028, st, &handled);
       if (!handled) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
     }
     // d = 128: the pipelined frozen-reference kernel (fa_fwd_d128.hip). Default: 8 waves for

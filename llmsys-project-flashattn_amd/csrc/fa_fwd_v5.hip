@@ -28,10 +28,9 @@ using namespace fwdbf16;
 constexpr int D = 64;
 constexpr int kBK = 64;
 constexpr int TILE = kBK * D;              // elements per K or V tile
-constexpr int NWV = 4;                     // waves per workgroup
-constexpr int kBQ = 64 * NWV;              // queries per workgroup
 constexpr int kKSlots = 4, kVSlots = 2;
-constexpr int LPT = kBK * (D / 8) / (64 * NWV);  // 16-B staging chunks per thread per tile
+template <int NW>
+constexpr int lpt() { return kBK * (D / 8) / (64 * NW); }  // 16-B staging chunks per thread per tile
 constexpr float kLimit = 1.8446744e19f;   // 2^64
 constexpr float kThr = 8.0f;
 
@@ -39,10 +38,12 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
+template <int LPT>
 struct Ctx5 {
   int koff[4];  // per-lane K row-image offsets per k-step (slot 0, key block 0)
   int voff[2];  // per-lane Vᵀ transpose-read offsets per d block (slot 0, row block 0)
   int kgo[LPT], vgo[LPT], kso[LPT], vso[LPT];
+  int kdo[LPT], vdo[LPT];  // LDS-DMA per-lane source offsets (rows R0(i) + lane / 8)
 };
 
 // Softmax of one 32-key half of a block: pair i (0..7) of the 16 scores of S_half.
@@ -50,6 +51,7 @@ struct Ctx5 {
 // (A v_dot2c_f32_bf16 row sum of the bf16-rounded pair was tried as VAR bit 0: slower,
 // 962 vs 978 TF/s, and it failed the 150x spike test; removed.)
 // VAR bit 2: the tile loop unrolled by 4 (see iter in the kernel).
+// VAR bit 1024: K/V staged by LDS-DMA (dma5) instead of through registers.
 // Diagnostic ablation bits (timing only, wrong results; policies 80-86): 8 no K/V staging,
 // 16 no barrier either, 64 no Vᵀ operand reads, 128 no exponential, 256 no row-sum add.
 // (Replacing the K operand reads with Q fragments is not a valid ablation: the QKᵀ
@@ -123,6 +125,7 @@ __device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32
   }
 }
 
+template <int LPT>
 __device__ __forceinline__ void load5(uint4 (&r)[LPT], __amdgpu_buffer_rsrc_t rs, const int (&go)[LPT],
                                       int step) {
 #pragma unroll
@@ -130,9 +133,20 @@ __device__ __forceinline__ void load5(uint4 (&r)[LPT], __amdgpu_buffer_rsrc_t rs
     r[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, go[i] + step, 0, 0));
 }
 
+template <int LPT>
 __device__ __forceinline__ void store5(bf16* dst, const uint4 (&r)[LPT], const int (&so)[LPT]) {
 #pragma unroll
   for (int i = 0; i < LPT; ++i) *(uint4*)(dst + so[i]) = r[i];
+}
+
+// LDS-DMA staging (VAR bit 1024): buffer_load_dwordx4 ... lds writes each lane's 16 B at
+// (wave-uniform base + lane * 16), so a wave instruction fills 8 consecutive 128-B rows of
+// the image in lane order; the swizzle moves to the per-lane global source (lane l of
+// rows R0..R0+7 fetches chunk (l % 8) ^ swz(row) of row R0 + l / 8). No VGPRs hold the
+// tile and there are no ds_write instructions. dst: the slot image + R0 rows.
+__device__ __forceinline__ void dma5(bf16* dst_rows, __amdgpu_buffer_rsrc_t rs, int go, int step) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst_rows, 16,
+                                           go + step, 0, 0, 0);
 }
 
 __device__ __forceinline__ float lane_pair_sum(float x) {
@@ -143,8 +157,10 @@ __device__ __forceinline__ float lane_pair_sum(float x) {
 }  // namespace
 
 // AHEAD: LDS operand reads are issued this many MFMAs ahead of their use. VAR: see sm_pair.
-template <int AHEAD, int VAR, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
+template <int AHEAD, int VAR, bool CAUSAL, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
+  constexpr int LPT = lpt<NW>();
+  constexpr int kBQ = 64 * NW;  // queries per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* const sK = (bf16*)smem_raw;          // [kKSlots][TILE]
   bf16* const sV = sK + kKSlots * TILE;      // [kVSlots][TILE]
@@ -182,7 +198,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
       qfB[ks] = *(const bf16x8*)(rb + ks * 16 + 8 * hf);
     }
   }
-  Ctx5 c;
+  Ctx5<LPT> c;
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) c.koff[ks] = k_swz<D>(c32, 2 * ks + hf);
   {
@@ -195,11 +211,15 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
     const int st_r = tid / (D / 8), st_c = tid % (D / 8);
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int r = st_r + i * (256 / (D / 8));
+      const int r = st_r + i * (64 * NW / (D / 8));
       c.kgo[i] = (r * skn + st_c * 8) * 2;
       c.vgo[i] = (r * svn + st_c * 8) * 2;
       c.kso[i] = k_swz<D>(r, st_c);
       c.vso[i] = v_swz<D>(r, st_c);
+      // DMA: wave w's instruction i fills rows 8 * (LPT * w + i) .. + 7
+      const int dr = 8 * (LPT * wave + i) + (lane >> 3), dc = lane & 7;
+      c.kdo[i] = (dr * skn + (dc ^ ((dr >> 1) & 7)) * 8) * 2;
+      c.vdo[i] = (dr * svn + (dc ^ (((dr >> 1) & 1) << 2)) * 8) * 2;
     }
   }
   const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
@@ -216,16 +236,31 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
 
+  auto dma_k = [&](bf16* slot, int step) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) dma5(slot + 8 * (LPT * wave + i) * D, rk, c.kdo[i], step);
+  };
+  auto dma_v = [&](bf16* slot, int step) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) dma5(slot + 8 * (LPT * wave + i) * D, rv, c.vdo[i], step);
+  };
+
   // ---- pass 0: the pipelined loop with the frozen first-tile reference over the tiles
   //      [0, nbulk), mask-free for every query of the workgroup ---------------------------
   if (!CAUSAL || nbulk >= 2) {  // non-causal: the launcher guarantees N >= 128
     uint4 rK[LPT], rV[LPT];
-    load5(rK, rk, c.kgo, 0);
-    load5(rV, rv, c.vgo, 0);
-    store5(sK, rK, c.kso);
-    store5(sV, rV, c.vso);
-    load5(rK, rk, c.kgo, ktile_b);
-    store5(sK + TILE, rK, c.kso);
+    if (VAR & 1024) {
+      dma_k(sK, 0);
+      dma_v(sV, 0);
+      dma_k(sK + TILE, ktile_b);
+    } else {
+      load5(rK, rk, c.kgo, 0);
+      load5(rV, rv, c.vgo, 0);
+      store5(sK, rK, c.kso);
+      store5(sV, rV, c.vso);
+      load5(rK, rk, c.kgo, ktile_b);
+      store5(sK + TILE, rK, c.kso);
+    }
     __syncthreads();
 
     // reference maxima from tile 0; S_B(0) kept for the pipeline, P_B(0) keys 0-31 computed
@@ -256,7 +291,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
     // immediate offsets instead of per-iteration address VALU).
     auto iter = [&](int t, int s0) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
-      if (!(VAR & 8)) {
+      if (VAR & 1024) {
+        // K(t+2) -> slot (t+2)%4 and V(t+1) -> slot (t+1)%2, both free since the last barrier
+        dma_k(sK + ((s0 + 2) & 3) * TILE, (t + 2) * ktile_b);
+        dma_v(sV + ((s0 + 1) & 1) * TILE, (t + 1) * vtile_b);
+      } else if (!(VAR & 8)) {
         load5(rK, rk, c.kgo, (t + 2) * ktile_b);
         load5(rV, rv, c.vgo, (t + 1) * vtile_b);
       }
@@ -273,10 +312,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
       phase_pv<true, AHEAD, VAR>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);         // P2
       phase_qk<true, AHEAD, VAR>(sK, koB, qfB, SB, SA[1], c2, nmcA, accA, pA1);             // P3
       phase_pv<true, AHEAD, VAR>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0);         // P4
-      if (!(VAR & 8)) {
+      if (!(VAR & 8) && !(VAR & 1024)) {
         store5(sK + ((s0 + 2) & 3) * TILE, rK, c.kso);
         store5(sV + ((s0 + 1) & 1) * TILE, rV, c.vso);
       }
+      if (VAR & 1024) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA has landed
       if (!(VAR & 16)) __syncthreads();
     };
     int t = 0;
@@ -412,8 +452,14 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
   *handled = true;
   const size_t smem = (size_t)(kKSlots + kVSlots) * TILE * sizeof(bf16);
   void (*kfn)(AttnArgs, int);
-  if (causal)
+  const int nw = (var & 2048) ? 8 : 4;  // VAR bit 2048 (launcher only): 8 waves per workgroup
+  var &= ~2048;
+  if (nw == 8)
+    kfn = var == 1028 ? fa_fwd_bf16_v5<2, 1028, false, 8> : fa_fwd_bf16_v5<2, 4, false, 8>;
+  else if (causal)
     kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;
+  else if (var == 1028)
+    kfn = fa_fwd_bf16_v5<2, 1028, false>;
   else if (var >= 8)  // diagnostic ablations
     kfn = var == 12    ? fa_fwd_bf16_v5<2, 12, false>
           : var == 28  ? fa_fwd_bf16_v5<2, 28, false>
@@ -429,10 +475,11 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
                        : fa_fwd_bf16_v5<2, 0, false>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
+  const int kBQ = 64 * nw;
   const int nqb = (a.N + kBQ - 1) / kBQ;
   const int64_t nblk = (int64_t)nqb * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(256), smem, st, a, nqb);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(64 * nw), smem, st, a, nqb);
   return hipGetLastError();
 }
 
