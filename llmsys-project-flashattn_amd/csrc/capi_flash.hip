@@ -132,6 +132,8 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
     if (g_kernel_policy >= 27 && g_kernel_policy <= 29)
       e = launch_fwd_v5(a, causal != 0, 2 * (g_kernel_policy - 26), g_kernel_policy == 27 ? 4 : 0, st,
                         &handled);
+    if (g_kernel_policy == 39 && !causal)  // 37 + static priority for the younger 4 waves
+      e = launch_fwd_v5(a, false, 2, 2048 + 1028 + 4096, st, &handled);
     if (g_kernel_policy == 38 && !causal)  // 4 waves, register staging (the previous default)
       e = launch_fwd_v5(a, false, 2, 4, st, &handled);
     if (g_kernel_policy == 31)  // tile loop not unrolled (the pre-unroll default)

@@ -245,6 +245,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
     for (int i = 0; i < LPT; ++i) dma5(slot + 8 * (LPT * wave + i) * D, rv, c.vdo[i], step);
   };
 
+  // VAR bit 4096 (8 waves): the younger half of the workgroup (waves 4-7) runs at issue
+  // priority 1 for the whole kernel, so it does not lose VALU arbitration to the older
+  // half at every phase start (cdna_hip_programming.md T5, static form).
+  if (NW == 8 && (VAR & 4096) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
+    __builtin_amdgcn_s_setprio(1);
+
   // ---- pass 0: the pipelined loop with the frozen first-tile reference over the tiles
   //      [0, nbulk), mask-free for every query of the workgroup ---------------------------
   if (!CAUSAL || nbulk >= 2) {  // non-causal: the launcher guarantees N >= 128
@@ -422,14 +428,30 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
     const float l = blk ? lB : lA, m = blk ? mB : mA;
     const f32x16(&O)[2] = blk ? OB : OA;
     const float inv = 1.f / l;
+    // Widened store: lane (c32, hf) holds columns 8g + 4hf .. +3 of each 32-column block;
+    // one v_permlane32_swap per dword pairs groups (g, g+1) so lanes 0-31 hold the 16
+    // contiguous bytes of group g and lanes 32-63 those of group g+1: 4 dwordx4 stores
+    // per block instead of 8 dwordx2 (every lane takes part in the swap; stores are guarded).
+    bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)min(q, N - 1) * p.so[2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      uint2 u[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        const bf16x4 v = {(bf16)(O[db][4 * g] * inv), (bf16)(O[db][4 * g + 1] * inv),
+                          (bf16)(O[db][4 * g + 2] * inv), (bf16)(O[db][4 * g + 3] * inv)};
+        u[g] = __builtin_bit_cast(uint2, v);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k += 2) {
+        const auto rx = __builtin_amdgcn_permlane32_swap(u[k].x, u[k + 1].x, false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(u[k].y, u[k + 1].y, false, false);
+        if (q < N)
+          *(uint4*)(Og + db * 32 + 8 * k + 8 * hf) = uint4{rx[0], ry[0], rx[1], ry[1]};
+      }
+    }
     if (q < N) {
-      bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)q * p.so[2];
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          store4(Og + db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv, O[db][4 * g + 1] * inv,
-                 O[db][4 * g + 2] * inv, O[db][4 * g + 3] * inv, true);
       if (hf == 0) {
         const int64_t row = (int64_t)bh * N + q;
         if (p.m) p.m[row] = m * p.scale;
@@ -455,7 +477,9 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
   const int nw = (var & 2048) ? 8 : 4;  // VAR bit 2048 (launcher only): 8 waves per workgroup
   var &= ~2048;
   if (nw == 8)
-    kfn = var == 1028 ? fa_fwd_bf16_v5<2, 1028, false, 8> : fa_fwd_bf16_v5<2, 4, false, 8>;
+    kfn = var == 1028   ? fa_fwd_bf16_v5<2, 1028, false, 8>
+          : var == 5124 ? fa_fwd_bf16_v5<2, 5124, false, 8>
+                        : fa_fwd_bf16_v5<2, 4, false, 8>;
   else if (causal)
     kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;
   else if (var == 1028)
