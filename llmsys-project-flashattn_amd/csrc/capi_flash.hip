@@ -26,7 +26,8 @@ hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
                          bool* handled);
-hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled);
+hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
+                           bool* handled);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
@@ -162,12 +163,17 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       if (!causal) e = launch_fwd_v5(a, false, 2, 2048 + 1028, st, &handled);
       if (!handled) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
     }
-    // d = 128: the pipelined frozen-reference kernel (fa_fwd_d128.hip). Default: 8 waves for
-    // long non-causal heads, else 4 (1214 vs 1125 TF/s at (8,16,16384,128); 948 vs 892 at
-    // (8,16,4096,128); causal 774 vs 701). 32 / 33 force 8 / 4 waves.
-    if (!handled && (g_kernel_policy == 0 || g_kernel_policy == 32 || g_kernel_policy == 33)) {
-      const int nw = g_kernel_policy == 32 ? 8 : g_kernel_policy == 33 ? 4 : (!causal && N >= 8192) ? 8 : 4;
-      e = launch_fwd_d128(a, causal != 0, nw, st, &handled);
+    // d = 128: the pipelined frozen-reference kernel (fa_fwd_d128.hip). Default: 8 waves
+    // non-causal, 4 causal (warm-clock A/B, profiles/r1_ab_d128_warm.txt: non-causal 1085 vs
+    // 1001 TF/s at (8,16,4096,128), 1143 vs 1046 at (1,16,16384,128); causal 846 vs 819).
+    // 32 / 33 force 8 / 4 waves; 44 / 45 the same with LDS-DMA staging (neutral to -3 %).
+    if (!handled && (g_kernel_policy == 0 || (g_kernel_policy >= 32 && g_kernel_policy <= 33) ||
+                     (g_kernel_policy >= 44 && g_kernel_policy <= 45))) {
+      // 44 / 45: 8 / 4 waves with LDS-DMA staging
+      const int nw = (g_kernel_policy == 32 || g_kernel_policy == 44) ? 8
+                     : (g_kernel_policy == 33 || g_kernel_policy == 45) ? 4
+                     : causal ? 4 : 8;
+      e = launch_fwd_d128(a, causal != 0, nw, g_kernel_policy >= 44, st, &handled);
     }
     // any shape the kernels above decline: the single-phase kernel, 8 waves by default
     // (faster than 4 at d = 128: 959 vs 802 TF/s at (1,16,16384,128))

@@ -46,6 +46,7 @@ struct Ctx6 {
   int koff[8];   // K row-image offset of this lane's A fragment per k-step (key block 0)
   int voff[4];   // Vᵀ transpose-read offset per 32-wide d block (16-key step 0)
   int kgo[LPT], vgo[LPT], kso[LPT], vso[LPT];
+  int kdo[LPT], vdo[LPT];  // LDS-DMA per-lane source offsets
 };
 
 __device__ __forceinline__ bf16x8 vt_read(const bf16* a1) {
@@ -133,6 +134,14 @@ __device__ __forceinline__ void store6(bf16* dst, const uint4 (&r)[LPT], const i
   for (int i = 0; i < LPT; ++i) *(uint4*)(dst + so[i]) = r[i];
 }
 
+// LDS-DMA (DMA = true): one buffer_load_dwordx4 ... lds writes 1 KiB = 4 rows of 256 B in
+// lane order; lane l of rows R0..R0+3 fetches the chunk the swizzle puts at slot l % 16 of
+// row R0 + l / 16 (the XOR swizzles are involutions).
+__device__ __forceinline__ void dma6(bf16* dst_rows, __amdgpu_buffer_rsrc_t rs, int go, int step) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst_rows, 16,
+                                           go + step, 0, 0, 0);
+}
+
 __device__ __forceinline__ bf16 exp1(float s, float c2, float nmc, float& l) {
   const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(s, c2, nmc));
   l += e;
@@ -194,7 +203,7 @@ __device__ __forceinline__ void bulk6(const bf16* sk, const bf16* sv, const Ctx6
 
 }  // namespace
 
-template <bool CAUSAL, int NW>
+template <bool CAUSAL, int NW, bool DMA = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, int nqb) {
   using C = C6<NW>;
   constexpr int LPT = C::LPT;
@@ -255,6 +264,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
       c.vgo[i] = (r * svn + st_c * 8) * 2;
       c.kso[i] = k_swz<D>(r, st_c);
       c.vso[i] = v_swz<D>(r, st_c);
+      // DMA: wave w's instruction i fills rows 4 * (LPT * w + i) .. + 3
+      const int dr = 4 * (LPT * wave + i) + (lane >> 4), dc = lane & 15;
+      c.kdo[i] = (dr * skn + (dc ^ (dr & 15)) * 8) * 2;
+      c.vdo[i] = (dr * svn + (dc ^ ((dr & 3) << 2)) * 8) * 2;
     }
   }
   const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
@@ -264,6 +277,24 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
   const int ntiles = (kend + kBK - 1) / kBK;
   const int nfull = CAUSAL ? min(N / kBK, q0 / kBK) : N / kBK;  // mask-free tiles
 
+  // staging: issue (global -> registers, or LDS-DMA straight into the slot) and write
+  // (registers -> slot; nothing with DMA, whose writes land by the barrier's vmcnt(0))
+#define D6_ISSUE_K(SLOT_, STEP_)                                                             \
+  {                                                                                          \
+    if (DMA) {                                                                               \
+      _Pragma("unroll") for (int i = 0; i < LPT; ++i)                                        \
+        dma6((SLOT_) + 4 * (LPT * wave + i) * D, rk, c.kdo[i], (STEP_));                     \
+    } else load6(rK, rk, c.kgo, (STEP_));                                                    \
+  }
+#define D6_ISSUE_V(SLOT_, STEP_)                                                             \
+  {                                                                                          \
+    if (DMA) {                                                                               \
+      _Pragma("unroll") for (int i = 0; i < LPT; ++i)                                        \
+        dma6((SLOT_) + 4 * (LPT * wave + i) * D, rv, c.vdo[i], (STEP_));                     \
+    } else load6(rV, rv, c.vgo, (STEP_));                                                    \
+  }
+#define D6_WRITE_K(SLOT_) { if (!DMA) store6((SLOT_), rK, c.kso); }
+#define D6_WRITE_V(SLOT_) { if (!DMA) store6((SLOT_), rV, c.vso); }
   f32x16 O[4];
   float l_part, m_run;
   uint4 rK[LPT], rV[LPT];
@@ -276,12 +307,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
     for (int i = 0; i < 4; ++i) O[i] = f32x16{};
     l_part = 0.f;
     m_run = -INFINITY;
-    load6(rK, rk, c.kgo, 0);
-    load6(rV, rv, c.vgo, 0);
-    store6(sK0, rK, c.kso);
-    store6(sV0, rV, c.vso);
-    load6(rK, rk, c.kgo, ktile_b);
-    store6(sK1, rK, c.kso);
+    D6_ISSUE_K(sK0, 0)
+    D6_ISSUE_V(sV0, 0)
+    D6_WRITE_K(sK0)
+    D6_WRITE_V(sV0)
+    D6_ISSUE_K(sK1, ktile_b)
+    D6_WRITE_K(sK1)
     __syncthreads();
     qk6(sK0, c, qf, SA);
     __syncthreads();  // iteration 0 overwrites K slot 0, which every wave just read
@@ -293,8 +324,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
     const int t_ = (T_);                                                                     \
     const int par = t_ & 1;                                                                  \
     const bool next = t_ + 1 < ntiles;                                                       \
-    if (t_ + 2 < ntiles) load6(rK, rk, c.kgo, (t_ + 2) * ktile_b);                           \
-    if (next) load6(rV, rv, c.vgo, (t_ + 1) * vtile_b);                                      \
+    if (t_ + 2 < ntiles) D6_ISSUE_K(par ? sK1 : sK0, (t_ + 2) * ktile_b)                     \
+    if (next) D6_ISSUE_V(par ? sV0 : sV1, (t_ + 1) * vtile_b)                                \
     if (!CAUSAL || t_ * kBK <= wq_hi) {                                                      \
       if (t_ >= nfull) mask6<CAUSAL>(SA, t_ * kBK, N, my_q, hf);                             \
       const float nmc = max6(SA, O, l_part, m_run, c2);                                      \
@@ -306,8 +337,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
       pv6<1>(sv, c, p2, p3, O);                                                              \
     }                                                                                        \
     if (next && (!CAUSAL || (t_ + 1) * kBK <= wq_hi)) qk6(par ? sK0 : sK1, c, qf, SA);       \
-    if (t_ + 2 < ntiles) store6(par ? sK1 : sK0, rK, c.kso);                                 \
-    if (next) store6(par ? sV0 : sV1, rV, c.vso);                                            \
+    if (t_ + 2 < ntiles) D6_WRITE_K(par ? sK1 : sK0)                                         \
+    if (next) D6_WRITE_V(par ? sV0 : sV1)                                                    \
     __syncthreads();                                                                         \
   }
 
@@ -320,11 +351,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
       // into a slot nobody reads).
 #define D6_BULK(SC_, SN_, SKN_, SVC_, SKW_, SVW_, T_)                                        \
   {                                                                                         \
-    load6(rK, rk, c.kgo, ((T_) + 2) * ktile_b);                                             \
-    load6(rV, rv, c.vgo, ((T_) + 1) * vtile_b);                                             \
+    D6_ISSUE_K(SKW_, ((T_) + 2) * ktile_b)                                                  \
+    D6_ISSUE_V(SVW_, ((T_) + 1) * vtile_b)                                                  \
     bulk6(SKN_, SVC_, c, qf, SC_, SN_, O, l_part, c2, nmc);                                 \
-    store6(SKW_, rK, c.kso);                                                                \
-    store6(SVW_, rV, c.vso);                                                                \
+    D6_WRITE_K(SKW_)                                                                        \
+    D6_WRITE_V(SVW_)                                                                        \
     __syncthreads();                                                                        \
   }
       // t odd: S(t) in SA, K(t+1) in slot 0, V(t) in slot 1; writes K(t+2) -> slot 1,
@@ -337,6 +368,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
     }
     for (; t < ntiles; ++t) D6_GENERAL(t)
 #undef D6_GENERAL
+#undef D6_ISSUE_K
+#undef D6_ISSUE_V
+#undef D6_WRITE_K
+#undef D6_WRITE_V
     const bool bad = !(l_part <= kBulkLimit);
     if (pass == 1 || !__syncthreads_or(bad)) break;
   }
@@ -361,10 +396,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
   }
 }
 
-template <bool CAUSAL, int NW>
+template <bool CAUSAL, int NW, bool DMA = false>
 static hipError_t launch_d128_t(const AttnArgs& a, hipStream_t st) {
   const size_t smem = 4 * (size_t)TILE * sizeof(bf16);
-  auto kfn = fa_fwd_bf16_d128<CAUSAL, NW>;
+  auto kfn = fa_fwd_bf16_d128<CAUSAL, NW, DMA>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)smem);
   if (e != hipSuccess) return e;
@@ -378,13 +413,18 @@ static hipError_t launch_d128_t(const AttnArgs& a, hipStream_t st) {
 // d = 128, bf16, unit d-stride (the caller's vec check); every per-head K/V byte offset up
 // to two tiles past N must fit the 31-bit buffer offset (the bulk loop stages one tile
 // ahead of the last one it needs).
-hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, hipStream_t st, bool* handled) {
+hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
+                           bool* handled) {
   *handled = false;
   if (a.d != D) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
+  if (dma) {
+    if (nw == 8) return causal ? launch_d128_t<true, 8, true>(a, st) : launch_d128_t<false, 8, true>(a, st);
+    return causal ? launch_d128_t<true, 4, true>(a, st) : launch_d128_t<false, 4, true>(a, st);
+  }
   if (nw == 8) return causal ? launch_d128_t<true, 8>(a, st) : launch_d128_t<false, 8>(a, st);
   return causal ? launch_d128_t<true, 4>(a, st) : launch_d128_t<false, 4>(a, st);
 }

@@ -11,6 +11,13 @@ g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
 o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
 flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
+# untimed clock ramp (~0.3 s of kernels) so the first policy is not measured on a cold GPU
+import time
+_hip.lib().mt_flash_set_kernel_policy(pols[0])
+t_ramp = time.perf_counter()
+while time.perf_counter() - t_ramp < 0.3:
+    _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
+    torch.cuda.synchronize()
 for p in pols:
     _hip.lib().mt_flash_set_kernel_policy(p)
     for _ in range(2): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)

@@ -269,7 +269,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # 8 / 4 waves; the d = 128 default), 35 v5 with LDS-DMA staging, 36 / 37 v5 with 8 waves
 # per workgroup (37 also LDS-DMA: the d = 64 non-causal default), 38 the 4-wave
 # register-staged v5
-FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
+FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39, 44, 45,
                  33)
 
 
