@@ -21,13 +21,13 @@ hipError_t launch_fwd_v2(const AttnArgs& a, bool causal, int nw, int resc, hipSt
                          bool* handled);
 hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
-                         bool* handled);
+                         bool* handled, bool pair = false);
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
                          bool* handled);
 hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
-                           bool* handled);
+                           bool* handled, bool pair = false);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
@@ -143,6 +143,14 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       e = launch_fwd_v5(a, false, 2, 1028, st, &handled);
     if ((g_kernel_policy == 36 || g_kernel_policy == 37) && !causal)  // 8 waves (37: + LDS-DMA)
       e = launch_fwd_v5(a, false, 2, g_kernel_policy == 36 ? 2048 + 4 : 2048 + 1028, st, &handled);
+    if (g_kernel_policy == 50 || g_kernel_policy == 51)  // causal v4, heavy + light block pairs
+      e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 50 ? 4 : 8, !causal, st, &handled, true);
+    if (g_kernel_policy >= 46 && g_kernel_policy <= 49 && !causal) {
+      // 37 (+ static priority at 49) with: 46 single-issue f32 softmax VALU (no v_pk_*),
+      // 47 waves 4-7 staggered half a tile behind waves 0-3, 48 both
+      static const int kVar[4] = {9220, 17412, 25604, 21508};
+      e = launch_fwd_v5(a, false, 2, 2048 + kVar[g_kernel_policy - 46], st, &handled);
+    }
     if (g_kernel_policy == 97)  // diagnostics only (wrong results): no scale-and-shift
       e = launch_fwd_v5(a, causal != 0, 2, 2, st, &handled);
     if (g_kernel_policy >= 80 && g_kernel_policy <= 86 && !causal) {
@@ -161,19 +169,30 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       // Non-causal default: 8 waves per workgroup with LDS-DMA K/V staging (policy 37:
       // 993 vs 967 TF/s for the 4-wave register-staged form, profiles/r1_ab_v5_nw8.txt).
       if (!causal) e = launch_fwd_v5(a, false, 2, 2048 + 1028, st, &handled);
-      if (!handled) e = launch_fwd_v4(a, causal != 0, 4, !causal, st, &handled);
+      // Causal: v4 with heavy + light query blocks paired per workgroup
+      // (profiles/r1_ab_causal_pair.txt): 4 waves (policy 50) below N = 8192 (860 vs 806
+      // TF/s unpaired at C3, 824 for 8 waves), 8 waves (policy 51) from there (934 vs 898
+      // for 4 waves at (1,16,16384,64)).
+      if (!handled)
+        e = launch_fwd_v4(a, causal != 0, causal && N >= 8192 ? 8 : 4, !causal, st, &handled,
+                          causal != 0);
     }
     // d = 128: the pipelined frozen-reference kernel (fa_fwd_d128.hip). Default: 8 waves
     // non-causal, 4 causal (warm-clock A/B, profiles/r1_ab_d128_warm.txt: non-causal 1085 vs
     // 1001 TF/s at (8,16,4096,128), 1143 vs 1046 at (1,16,16384,128); causal 846 vs 819).
     // 32 / 33 force 8 / 4 waves; 44 / 45 the same with LDS-DMA staging (neutral to -3 %).
     if (!handled && (g_kernel_policy == 0 || (g_kernel_policy >= 32 && g_kernel_policy <= 33) ||
-                     (g_kernel_policy >= 44 && g_kernel_policy <= 45))) {
-      // 44 / 45: 8 / 4 waves with LDS-DMA staging
-      const int nw = (g_kernel_policy == 32 || g_kernel_policy == 44) ? 8
-                     : (g_kernel_policy == 33 || g_kernel_policy == 45) ? 4
-                     : causal ? 4 : 8;
-      e = launch_fwd_d128(a, causal != 0, nw, g_kernel_policy >= 44, st, &handled);
+                     (g_kernel_policy >= 44 && g_kernel_policy <= 45) || g_kernel_policy == 52 ||
+                     g_kernel_policy == 53)) {
+      // 44 / 45: 8 / 4 waves with LDS-DMA staging; 52 / 53: causal heavy + light block
+      // pairs per workgroup, 4 / 8 waves
+      const int nw = (g_kernel_policy == 32 || g_kernel_policy == 44 || g_kernel_policy == 53) ? 8
+                     : (g_kernel_policy == 33 || g_kernel_policy == 45 || g_kernel_policy == 52) ? 4
+                     : 8;
+      // causal default: 8 waves with paired query blocks (policy 53: 944 vs 866 TF/s for
+      // unpaired 4 waves at (8,16,4096,128), 1101 vs 1020 at (1,16,16384,128))
+      e = launch_fwd_d128(a, causal != 0, nw, g_kernel_policy == 44 || g_kernel_policy == 45, st,
+                          &handled, g_kernel_policy >= 52 || (g_kernel_policy == 0 && causal));
     }
     // any shape the kernels above decline: the single-phase kernel, 8 waves by default
     // (faster than 4 at d = 128: 959 vs 802 TF/s at (1,16,16384,128))

@@ -203,7 +203,9 @@ __device__ __forceinline__ void bulk6(const bf16* sk, const bf16* sv, const Ctx6
 
 }  // namespace
 
-template <bool CAUSAL, int NW, bool DMA = false>
+// PAIR (causal): a workgroup owns query blocks nqb-1-u and u of one head (heaviest, then
+// lightest), so every workgroup walks nqb + 1 key tiles (fa_fwd_v4.hip, same scheme).
+template <bool CAUSAL, int NW, bool DMA = false, bool PAIR = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, int nqb) {
   using C = C6<NW>;
   constexpr int LPT = C::LPT;
@@ -221,10 +223,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
   const int nblk = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
   const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  const int bh = logical / nqb;
-  int qb = logical % nqb;
-  if (CAUSAL) qb = nqb - 1 - qb;  // heaviest first
+  const int nunit = PAIR ? (nqb + 1) / 2 : nqb;  // work units per head
+  const int bh = logical / nunit;
+  const int unit = logical % nunit;
   const int b = bh / p.H, hh = bh % p.H;
+  for (int rep = 0; rep < (PAIR ? 2 : 1); ++rep) {
+  int qb = unit;
+  if (PAIR) {
+    qb = rep ? unit : nqb - 1 - unit;
+    if (rep && qb == nqb - 1 - unit) break;  // odd nqb: the middle block has no partner
+  } else if (CAUSAL) {
+    qb = nqb - 1 - qb;  // heaviest first
+  }
   const int q0 = qb * C::kBQ;
 
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
@@ -394,17 +404,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
       if (p.l) p.l[row] = l_tot;
     }
   }
+  }  // rep
 }
 
-template <bool CAUSAL, int NW, bool DMA = false>
+template <bool CAUSAL, int NW, bool DMA = false, bool PAIR = false>
 static hipError_t launch_d128_t(const AttnArgs& a, hipStream_t st) {
   const size_t smem = 4 * (size_t)TILE * sizeof(bf16);
-  auto kfn = fa_fwd_bf16_d128<CAUSAL, NW, DMA>;
+  auto kfn = fa_fwd_bf16_d128<CAUSAL, NW, DMA, PAIR>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)smem);
   if (e != hipSuccess) return e;
   const int nqb = (a.N + 32 * NW - 1) / (32 * NW);
-  const int64_t nblk = (int64_t)nqb * a.B * a.H;
+  const int64_t nblk = (int64_t)(PAIR ? (nqb + 1) / 2 : nqb) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(64 * NW), smem, st, a, nqb);
   return hipGetLastError();
@@ -414,13 +425,15 @@ static hipError_t launch_d128_t(const AttnArgs& a, hipStream_t st) {
 // to two tiles past N must fit the 31-bit buffer offset (the bulk loop stages one tile
 // ahead of the last one it needs).
 hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
-                           bool* handled) {
+                           bool* handled, bool pair) {
   *handled = false;
   if (a.d != D) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
+  if (causal && pair)
+    return nw == 8 ? launch_d128_t<true, 8, false, true>(a, st) : launch_d128_t<true, 4, false, true>(a, st);
   if (dma) {
     if (nw == 8) return causal ? launch_d128_t<true, 8, true>(a, st) : launch_d128_t<false, 8, true>(a, st);
     return causal ? launch_d128_t<true, 4, true>(a, st) : launch_d128_t<false, 4, true>(a, st);

@@ -225,7 +225,10 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
 
 }  // namespace
 
-template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false>
+// PAIR (causal only): a workgroup owns the query blocks nqb-1-u and u of one head (the
+// heaviest block, then the lightest), so every workgroup walks nqb + 1 key tiles and
+// the grid has no tail of heavy blocks dispatched last.
+template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false, bool PAIR = false>
 __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb) {
   using C = V4<NW>;
   constexpr int D = 64;
@@ -242,10 +245,18 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb
   const int xcd = hw & 7, slot = hw >> 3;
   const int qd = nblk >> 3, rm = nblk & 7;
   const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  const int bh = logical / nqb;
-  int qb = logical % nqb;
-  if (CAUSAL) qb = nqb - 1 - qb;  // heaviest first
+  const int nunit = PAIR ? (nqb + 1) / 2 : nqb;  // work units per head
+  const int bh = logical / nunit;
+  const int unit = logical % nunit;
   const int b = bh / p.H, hh = bh % p.H;
+  for (int rep = 0; rep < (PAIR ? 2 : 1); ++rep) {
+  int qb = unit;
+  if (PAIR) {
+    qb = rep ? unit : nqb - 1 - unit;
+    if (rep && qb == nqb - 1 - unit) break;  // odd nqb: the middle block has no partner
+  } else if (CAUSAL) {
+    qb = nqb - 1 - qb;  // heaviest first
+  }
   const int q0 = qb * C::kBQ;
 
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
@@ -420,17 +431,18 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb
       if (p.l) p.l[row] = l_tot;
     }
   }
+  }  // rep
 }
 
-template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false>
+template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false, bool PAIR = false>
 static hipError_t launch_v4_t(const AttnArgs& a, hipStream_t st) {
   const size_t smem = 4 * (size_t)kBK * 64 * sizeof(bf16);
-  auto kfn = fa_fwd_bf16_v4<CAUSAL, NW, PK, ABL, DEEP>;
+  auto kfn = fa_fwd_bf16_v4<CAUSAL, NW, PK, ABL, DEEP, PAIR>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)smem);
   if (e != hipSuccess) return e;
   const int nqb = (a.N + 32 * NW - 1) / (32 * NW);
-  const int64_t nblk = (int64_t)nqb * a.B * a.H;
+  const int64_t nblk = (int64_t)(PAIR ? (nqb + 1) / 2 : nqb) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(64 * NW), smem, st, a, nqb);
   return hipGetLastError();
@@ -456,13 +468,16 @@ hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream
 }
 
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
-                         bool* handled) {
+                         bool* handled, bool pair) {
   *handled = false;
   if (a.d != 64) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
+  if (causal && pair)
+    return nw == 8 ? launch_v4_t<true, 8, false, 0, false, true>(a, st)
+                   : launch_v4_t<true, 4, false, 0, false, true>(a, st);
   if (pk) {
     if (nw == 8) return causal ? launch_v4_t<true, 8, true>(a, st) : launch_v4_t<false, 8, true>(a, st);
     return causal ? launch_v4_t<true, 4, true>(a, st) : launch_v4_t<false, 4, true>(a, st);

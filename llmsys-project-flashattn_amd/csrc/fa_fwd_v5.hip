@@ -18,6 +18,8 @@
 // and writes K(t+2)), V a 2-slot ring; one barrier per iteration.
 // Softmax: v4's frozen first-tile reference (row max of tile 0 per block); a lane whose
 // row-sum share leaves 2^64 sends its workgroup through a serial deferred-max recompute.
+#include <type_traits>
+
 #include "fa_fwd_bf16.h"
 
 namespace mt {
@@ -56,10 +58,32 @@ struct Ctx5 {
 // 16 no barrier either, 64 no Vᵀ operand reads, 128 no exponential, 256 no row-sum add.
 // (Replacing the K operand reads with Q fragments is not a valid ablation: the QKᵀ
 // products become loop-invariant and the compiler hoists them out of the loop.)
+// VAR bit 8192: single-issue f32 VALU only (v_fma_f32 / v_add_f32 pinned by inline asm, so
+// neither SLP nor the vector types form v_pk_fma_f32 / v_pk_add_f32 beside the MFMAs).
+__device__ __forceinline__ float fma1(float a, float b, float c) {
+  float r;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float add1(float a, float b) {
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 template <int VAR>
 __device__ __forceinline__ void sm_pair(const f32x16& s, int i, float c2, float nmc, f32x2& acc,
                                         bf16x8 (&pf)[2]) {
   const int j = 2 * i;
+  if (VAR & 8192) {
+    const float e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j], c2, nmc));
+    const float e1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j + 1], c2, nmc));
+    acc[0] += e0;
+    acc[1] += e1;
+    pf[j >> 3][j & 7] = (bf16)e0;
+    pf[j >> 3][(j & 7) + 1] = (bf16)e1;
+    return;
+  }
   f32x2 x;
   if (VAR & 2)
     x = f32x2{s[j], s[j + 1]};
@@ -163,11 +187,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   constexpr int kBQ = 64 * NW;  // queries per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* const sK = (bf16*)smem_raw;          // [kKSlots][TILE]
-  bf16* const sV = sK + kKSlots * TILE;      // [kVSlots][TILE]
+  bf16* const sV = sK + kKSlots * TILE;      // [kVS][TILE]
+  // VAR bit 16384 (8 waves): waves 4-7 (the second wave of each SIMD) take the tile barrier
+  // after P2 instead of after P4, so they run half a tile behind waves 0-3 and the two
+  // waves of a SIMD stop reaching their MFMA / VALU bursts in lockstep
+  // (MI355X_MICROARCH.md, two waves per SIMD, item 9). V then needs a 4-slot ring: a
+  // lagging wave still reads V(t) in P4 while the others stage V(t+2).
+  constexpr int kVS = (VAR & 16384) ? 4 : kVSlots;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N;
+  const bool late = (VAR & 16384) && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= 4;
 
   const int nblk = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
@@ -295,18 +326,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
     // One iteration; s0 = t & 3. With VAR bit 2 the loop is unrolled by the K ring size so
     // that every slot offset is a compile-time constant (folded into the LDS instructions'
     // immediate offsets instead of per-iteration address VALU).
-    auto iter = [&](int t, int s0) __attribute__((always_inline)) {
+    auto iter = [&](int t, int s0, auto late_tag) __attribute__((always_inline)) {
+      constexpr bool kLate = decltype(late_tag)::value;
       __builtin_amdgcn_sched_barrier(0);
       if (VAR & 1024) {
         // K(t+2) -> slot (t+2)%4 and V(t+1) -> slot (t+1)%2, both free since the last barrier
         dma_k(sK + ((s0 + 2) & 3) * TILE, (t + 2) * ktile_b);
-        dma_v(sV + ((s0 + 1) & 1) * TILE, (t + 1) * vtile_b);
+        dma_v(sV + ((s0 + 1) & (kVS - 1)) * TILE, (t + 1) * vtile_b);
       } else if (!(VAR & 8)) {
         load5(rK, rk, c.kgo, (t + 2) * ktile_b);
         load5(rV, rv, c.vgo, (t + 1) * vtile_b);
       }
       int koA[4], koB[4], vo[2];
-      const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & 1) * TILE;
+      const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & (kVS - 1)) * TILE;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         koA[ks] = c.koff[ks] + kslA;
@@ -316,31 +348,45 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       vo[1] = c.voff[1] + vsl;
       phase_qk<true, AHEAD, VAR>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);             // P1
       phase_pv<true, AHEAD, VAR>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);         // P2
+      if (kLate) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+      }
       phase_qk<true, AHEAD, VAR>(sK, koB, qfB, SB, SA[1], c2, nmcA, accA, pA1);             // P3
       phase_pv<true, AHEAD, VAR>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0);         // P4
       if (!(VAR & 8) && !(VAR & 1024)) {
         store5(sK + ((s0 + 2) & 3) * TILE, rK, c.kso);
         store5(sV + ((s0 + 1) & 1) * TILE, rV, c.vso);
       }
-      if (VAR & 1024) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA has landed
-      if (!(VAR & 16)) __syncthreads();
-    };
-    int t = 0;
-    if (VAR & 4)
-      for (; t + 4 < nbulk; t += 4) {
-        iter(t, 0);
-        iter(t + 1, 1);
-        iter(t + 2, 2);
-        iter(t + 3, 3);
+      if (!kLate) {
+        if (VAR & 1024) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA has landed
+        if (!(VAR & 16)) __syncthreads();
       }
-    for (; t + 1 < nbulk; ++t) iter(t, t & 3);
+    };
+    // The staggered half runs its own copy of the loop (straight-line bodies; a branch on
+    // `late` inside the body splits it and the register allocator then spills).
+    auto loop = [&](auto late_tag) __attribute__((always_inline)) {
+      int t = 0;
+      if (VAR & 4)
+        for (; t + 4 < nbulk; t += 4) {
+          iter(t, 0, late_tag);
+          iter(t + 1, 1, late_tag);
+          iter(t + 2, 2, late_tag);
+          iter(t + 3, 3, late_tag);
+        }
+      for (; t + 1 < nbulk; ++t) iter(t, t & 3, late_tag);
+    };
+    if ((VAR & 16384) && late)
+      loop(std::integral_constant<bool, true>{});
+    else
+      loop(std::integral_constant<bool, false>{});
     {
       const int t = nbulk - 1;
       int koA[4], vo[2];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) koA[ks] = c.koff[ks] + (t & 3) * TILE;
-      vo[0] = c.voff[0] + (t & 1) * TILE;
-      vo[1] = c.voff[1] + (t & 1) * TILE;
+      vo[0] = c.voff[0] + (t & (kVS - 1)) * TILE;
+      vo[1] = c.voff[1] + (t & (kVS - 1)) * TILE;
       phase_qk<true, AHEAD, VAR>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);
       phase_pv<true, AHEAD, VAR>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);
 #pragma unroll
@@ -472,13 +518,17 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
-  const size_t smem = (size_t)(kKSlots + kVSlots) * TILE * sizeof(bf16);
+  const size_t smem = (size_t)(kKSlots + ((var & 16384) ? 4 : kVSlots)) * TILE * sizeof(bf16);
   void (*kfn)(AttnArgs, int);
   const int nw = (var & 2048) ? 8 : 4;  // VAR bit 2048 (launcher only): 8 waves per workgroup
   var &= ~2048;
   if (nw == 8)
     kfn = var == 1028   ? fa_fwd_bf16_v5<2, 1028, false, 8>
           : var == 5124 ? fa_fwd_bf16_v5<2, 5124, false, 8>
+          : var == 9220 ? fa_fwd_bf16_v5<2, 9220, false, 8>
+          : var == 17412 ? fa_fwd_bf16_v5<2, 17412, false, 8>
+          : var == 25604 ? fa_fwd_bf16_v5<2, 25604, false, 8>
+          : var == 21508 ? fa_fwd_bf16_v5<2, 21508, false, 8>
                         : fa_fwd_bf16_v5<2, 4, false, 8>;
   else if (causal)
     kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;

@@ -217,6 +217,22 @@ def test_config3_bf16_full_size(torch_dev, causal):
             assert err <= tol, f"{name} (b,h)=({b},{h}) max-abs {err:.3e} > {tol:.3e}"
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_long_causal_paired_default(torch_dev, d):
+    """Causal default at long N (d = 64: 8-wave v4 from N = 8192; d = 128: 8-wave d128),
+    both with heavy + light query blocks paired per workgroup: rows from every block of a
+    head checked against the C oracle, the first and last blocks included."""
+    from minitorch import _hip
+    torch = torch_dev
+    g = torch.Generator(device="cuda").manual_seed(11)
+    q, k, v = (torch.randn((1, 3, 8192, d), device="cuda", generator=g).to(torch.bfloat16)
+               for _ in range(3))
+    o, m, l = _hip.flash_fwd(q, k, v, True)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o.float()).all()
+    _subset_check_fwd(torch, q, k, v, o, True, [(0, 0), (0, 2)], 1e-3, 2.0 ** -7)
+
+
 def test_deterministic(torch_dev):
     """No atomics: two runs are bitwise identical."""
     from minitorch import _hip
@@ -268,9 +284,13 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # default unroll the tile loop by 4, 31 does not), 32/33 the d = 128 kernel (fa_fwd_d128.hip,
 # 8 / 4 waves; the d = 128 default), 35 v5 with LDS-DMA staging, 36 / 37 v5 with 8 waves
 # per workgroup (37 also LDS-DMA: the d = 64 non-causal default), 38 the 4-wave
-# register-staged v5
+# register-staged v5, 39 = 37 + static priority for waves 4-7, 44/45 the d = 128 kernel with
+# LDS-DMA staging (8 / 4 waves), 46 = 37 with single-issue f32 softmax VALU, 47 = 37 with
+# waves 4-7 staggered half a tile behind (4-slot V ring), 48 = 46 + 47, 49 = 47 + priority,
+# 50 / 51 causal v4 (4 / 8 waves) with query blocks paired heavy + light per workgroup,
+# 52 / 53 the same pairing in the d = 128 kernel (4 / 8 waves); the causal defaults pair
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39, 44, 45,
-                 33)
+                 33, 46, 47, 48, 49, 50, 51, 52, 53)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
