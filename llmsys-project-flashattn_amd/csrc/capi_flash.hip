@@ -145,6 +145,12 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       e = launch_fwd_v5(a, false, 2, g_kernel_policy == 36 ? 2048 + 4 : 2048 + 1028, st, &handled);
     if (g_kernel_policy == 50 || g_kernel_policy == 51)  // causal v4, heavy + light block pairs
       e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 50 ? 4 : 8, !causal, st, &handled, true);
+    if (g_kernel_policy >= 56 && g_kernel_policy <= 58 && !causal)  // 54 + exp-to-use distance
+      // of one MFMA slot (57 / 58: LDS operand reads 3 / 4 MFMAs ahead instead of 2)
+      e = launch_fwd_v5(a, false, g_kernel_policy - 54, 2048 + 99332, st, &handled);
+    if ((g_kernel_policy == 54 || g_kernel_policy == 55) && !causal)  // 37 (55: + priority) with
+      // the Vᵀ fragments of P2 kept in registers for P4 (half the V LDS reads)
+      e = launch_fwd_v5(a, false, 2, 2048 + (g_kernel_policy == 54 ? 33796 : 37892), st, &handled);
     if (g_kernel_policy >= 46 && g_kernel_policy <= 49 && !causal) {
       // 37 (+ static priority at 49) with: 46 single-issue f32 softmax VALU (no v_pk_*),
       // 47 waves 4-7 staggered half a tile behind waves 0-3, 48 both
@@ -168,7 +174,10 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       // 256-query workgroups balance the triangle worse and its diagonal tiles run serially.
       // Non-causal default: 8 waves per workgroup with LDS-DMA K/V staging (policy 37:
       // 993 vs 967 TF/s for the 4-wave register-staged form, profiles/r1_ab_v5_nw8.txt).
-      if (!causal) e = launch_fwd_v5(a, false, 2, 2048 + 1028, st, &handled);
+      // Then (policy 56): the Vᵀ fragments of P2 kept in registers for P4 (+1.8 %,
+      // profiles/r1_ab_v5_vkeep.txt) and each pair's row-sum add / bf16 pack one MFMA slot
+      // after its exponentials (no trans-use s_nop; +2.2 % more, profiles/r1_ab_v5_defer.txt).
+      if (!causal) e = launch_fwd_v5(a, false, 2, 2048 + 99332, st, &handled);
       // Causal: v4 with heavy + light query blocks paired per workgroup
       // (profiles/r1_ab_causal_pair.txt): 4 waves (policy 50) below N = 8192 (860 vs 806
       // TF/s unpaired at C3, 824 for 8 waves), 8 waves (policy 51) from there (934 vs 898

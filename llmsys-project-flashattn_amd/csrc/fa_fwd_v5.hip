@@ -96,6 +96,21 @@ __device__ __forceinline__ void sm_pair(const f32x16& s, int i, float c2, float 
   pf[j >> 3][(j & 7) + 1] = (bf16)e1;
 }
 
+// VAR bit 65536: the softmax of pair i is split in two: its scale-and-shift and
+// exponentials in MFMA slot i, its row-sum add and bf16 pack in slot i + 1 (the last pair's
+// after the phase's last MFMA). A v_exp_f32 result read by the very next VALU instruction
+// costs an s_nop (trans-use hazard); one slot of distance removes it.
+__device__ __forceinline__ f32x2 sm_exp(const f32x16& s, int i, float c2, float nmc) {
+  const f32x2 x = f32x2{s[2 * i], s[2 * i + 1]} * f32x2{c2, c2} + f32x2{nmc, nmc};
+  return f32x2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+}
+__device__ __forceinline__ void sm_fin(const f32x2& e, int i, f32x2& acc, bf16x8 (&pf)[2]) {
+  const int j = 2 * i;
+  acc += e;
+  pf[j >> 3][j & 7] = (bf16)e[0];
+  pf[j >> 3][(j & 7) + 1] = (bf16)e[1];
+}
+
 __device__ __forceinline__ bf16x8 kread(const bf16* sk, const int (&ko)[4], int i) {
   // MFMA i of a QKᵀ phase: key block i/4, k-step i%4 (block 0's chain completes first)
   return *(const bf16x8*)(sk + (i >> 2) * 32 * D + ko[i & 3]);
@@ -117,6 +132,7 @@ __device__ __forceinline__ void phase_qk(const bf16* sk, const int (&ko)[4], con
                                          f32x16 (&S)[2], const f32x16& s_in, float c2, float nmc,
                                          f32x2& acc, bf16x8 (&pf)[2]) {
   bf16x8 kf[8];
+  f32x2 ep;
 #pragma unroll
   for (int i = 0; i < kAhead; ++i) kf[i] = kread(sk, ko, i);
 #pragma unroll
@@ -124,29 +140,49 @@ __device__ __forceinline__ void phase_qk(const bf16* sk, const int (&ko)[4], con
     if (i + kAhead < 8) kf[i + kAhead] = kread(sk, ko, i + kAhead);
     S[i >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i & 3], (i & 3) ? S[i >> 2] : f32x16{},
                                                        0, 0, 0);
-    if (SOFT) sm_pair<VAR>(s_in, i, c2, nmc, acc, pf);
+    if (SOFT && (VAR & 65536)) {
+      const f32x2 e = sm_exp(s_in, i, c2, nmc);
+      if (i) sm_fin(ep, i - 1, acc, pf);
+      ep = e;
+    } else if (SOFT) {
+      sm_pair<VAR>(s_in, i, c2, nmc, acc, pf);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (SOFT && (VAR & 65536)) sm_fin(ep, 7, acc, pf);
 }
 
 // PV phase (8 MFMAs into O with P fragments p_lo (keys 0-31) and p_hi (keys 32-63))
 // interleaved with the softmax of s_in (8 pairs) -> pf.
-template <bool SOFT, int kAhead, int VAR>
+// KEEP (VAR bit 32768): 1 = read the Vᵀ fragments and leave them in vk, 2 = take them from
+// vk (P2 and P4 of an iteration multiply the same V(t): the second phase reads no LDS).
+template <bool SOFT, int kAhead, int VAR, int KEEP = 0>
 __device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32x16 (&O)[2],
                                          const bf16x8 (&p_lo)[2], const bf16x8 (&p_hi)[2],
                                          const f32x16& s_in, float c2, float nmc, f32x2& acc,
-                                         bf16x8 (&pf)[2]) {
-  bf16x8 vf[8];
+                                         bf16x8 (&pf)[2], bf16x8 (&vk)[8]) {
+  bf16x8 vf_own[8];
+  f32x2 ep;
+  bf16x8 (&vf)[8] = KEEP ? vk : vf_own;
+  if (KEEP != 2) {
 #pragma unroll
-  for (int n = 0; n < kAhead; ++n) vf[n] = (VAR & 64) ? p_lo[n & 1] : vread(sv, vo, n);
+    for (int n = 0; n < kAhead; ++n) vf[n] = (VAR & 64) ? p_lo[n & 1] : vread(sv, vo, n);
+  }
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
-    if (n + kAhead < 8) vf[n + kAhead] = (VAR & 64) ? p_hi[n & 1] : vread(sv, vo, n + kAhead);
+    if (KEEP != 2 && n + kAhead < 8) vf[n + kAhead] = (VAR & 64) ? p_hi[n & 1] : vread(sv, vo, n + kAhead);
     const bf16x8& p = (n >> 2) ? p_hi[(n >> 1) & 1] : p_lo[(n >> 1) & 1];
     O[n & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[n], p, O[n & 1], 0, 0, 0);
-    if (SOFT) sm_pair<VAR>(s_in, n, c2, nmc, acc, pf);
+    if (SOFT && (VAR & 65536)) {
+      const f32x2 e = sm_exp(s_in, n, c2, nmc);
+      if (n) sm_fin(ep, n - 1, acc, pf);
+      ep = e;
+    } else if (SOFT) {
+      sm_pair<VAR>(s_in, n, c2, nmc, acc, pf);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (SOFT && (VAR & 65536)) sm_fin(ep, 7, acc, pf);
 }
 
 template <int LPT>
@@ -262,6 +298,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   const float c2 = p.scale_log2;
 
   f32x16 OA[2], OB[2];
+  bf16x8 vk[8];  // Vᵀ fragments kept from P2 to P4 (VAR bit 32768)
+  constexpr int kKeep = (VAR & 32768) ? 1 : 0;
   float mA = -INFINITY, mB = -INFINITY;
   float pA = 0.f, pB = 0.f;  // this lane's share of each block's row sum
 #pragma unroll
@@ -347,13 +385,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       vo[0] = c.voff[0] + vsl;
       vo[1] = c.voff[1] + vsl;
       phase_qk<true, AHEAD, VAR>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);             // P1
-      phase_pv<true, AHEAD, VAR>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);         // P2
+      phase_pv<true, AHEAD, VAR, kKeep>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0, vk);  // P2
       if (kLate) {
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
       phase_qk<true, AHEAD, VAR>(sK, koB, qfB, SB, SA[1], c2, nmcA, accA, pA1);             // P3
-      phase_pv<true, AHEAD, VAR>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0);         // P4
+      phase_pv<true, AHEAD, VAR, 2 * kKeep>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0, vk);  // P4
       if (!(VAR & 8) && !(VAR & 1024)) {
         store5(sK + ((s0 + 2) & 3) * TILE, rK, c.kso);
         store5(sV + ((s0 + 1) & 1) * TILE, rV, c.vso);
@@ -388,12 +426,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       vo[0] = c.voff[0] + (t & (kVS - 1)) * TILE;
       vo[1] = c.voff[1] + (t & (kVS - 1)) * TILE;
       phase_qk<true, AHEAD, VAR>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);
-      phase_pv<true, AHEAD, VAR>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0);
+      phase_pv<true, AHEAD, VAR, kKeep>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0, vk);
 #pragma unroll
       for (int i = 0; i < 8; ++i) sm_pair<VAR>(SA[1], i, c2, nmcA, accA, pA1);
       f32x2 d2 = {0.f, 0.f};
       bf16x8 dpf[2];
-      phase_pv<false, AHEAD, VAR>(sV, vo, OA, pA0, pA1, SA[0], c2, 0.f, d2, dpf);
+      phase_pv<false, AHEAD, VAR, 2 * kKeep>(sV, vo, OA, pA0, pA1, SA[0], c2, 0.f, d2, dpf, vk);
     }
     pA = accA[0] + accA[1];
     pB = accB[0] + accB[1];
@@ -452,7 +490,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
 #pragma unroll
         for (int i = 0; i < 8; ++i) sm_pair<VAR>(S[1], i, c2, nmc, acc, phi);
         l += acc[0] + acc[1];
-        phase_pv<false, AHEAD, VAR>(sV, vo, O, plo, phi, S[0], c2, 0.f, acc, dpf);
+        phase_pv<false, AHEAD, VAR>(sV, vo, O, plo, phi, S[0], c2, 0.f, acc, dpf, vk);
       }
     }
   };
@@ -522,13 +560,20 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
   void (*kfn)(AttnArgs, int);
   const int nw = (var & 2048) ? 8 : 4;  // VAR bit 2048 (launcher only): 8 waves per workgroup
   var &= ~2048;
-  if (nw == 8)
+  if (nw == 8 && ahead == 3)  // LDS operand reads 3 / 4 MFMAs ahead (policies 57 / 58)
+    kfn = fa_fwd_bf16_v5<3, 99332, false, 8>;
+  else if (nw == 8 && ahead == 4)
+    kfn = fa_fwd_bf16_v5<4, 99332, false, 8>;
+  else if (nw == 8)
     kfn = var == 1028   ? fa_fwd_bf16_v5<2, 1028, false, 8>
           : var == 5124 ? fa_fwd_bf16_v5<2, 5124, false, 8>
           : var == 9220 ? fa_fwd_bf16_v5<2, 9220, false, 8>
           : var == 17412 ? fa_fwd_bf16_v5<2, 17412, false, 8>
           : var == 25604 ? fa_fwd_bf16_v5<2, 25604, false, 8>
           : var == 21508 ? fa_fwd_bf16_v5<2, 21508, false, 8>
+          : var == 33796 ? fa_fwd_bf16_v5<2, 33796, false, 8>
+          : var == 37892 ? fa_fwd_bf16_v5<2, 37892, false, 8>
+          : var == 99332 ? fa_fwd_bf16_v5<2, 99332, false, 8>
                         : fa_fwd_bf16_v5<2, 4, false, 8>;
   else if (causal)
     kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;
