@@ -145,6 +145,8 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       e = launch_fwd_v5(a, false, 2, g_kernel_policy == 36 ? 2048 + 4 : 2048 + 1028, st, &handled);
     if (g_kernel_policy == 50 || g_kernel_policy == 51)  // causal v4, heavy + light block pairs
       e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 50 ? 4 : 8, !causal, st, &handled, true);
+    if (g_kernel_policy == 61 && !causal)  // 56 with the LDS-DMA issued from inline asm
+      e = launch_fwd_v5(a, false, 2, 2048 + 623620, st, &handled);
     if (g_kernel_policy >= 56 && g_kernel_policy <= 58 && !causal)  // 54 + exp-to-use distance
       // of one MFMA slot (57 / 58: LDS operand reads 3 / 4 MFMAs ahead instead of 2)
       e = launch_fwd_v5(a, false, g_kernel_policy - 54, 2048 + 99332, st, &handled);

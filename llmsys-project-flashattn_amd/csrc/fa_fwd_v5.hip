@@ -204,9 +204,27 @@ __device__ __forceinline__ void store5(bf16* dst, const uint4 (&r)[LPT], const i
 // the image in lane order; the swizzle moves to the per-lane global source (lane l of
 // rows R0..R0+7 fetches chunk (l % 8) ^ swz(row) of row R0 + l / 8). No VGPRs hold the
 // tile and there are no ds_write instructions. dst: the slot image + R0 rows.
+// VAR bit 524288: the same instruction from inline asm. hipcc tracks builtin LDS-DMA as an
+// LDS store of unknown address and puts an s_waitcnt vmcnt(0) before the first Vᵀ read of
+// every tile (the DMA then has to land within P1); the asm form is invisible to its waitcnt
+// pass, and the explicit vmcnt(0) before each tile barrier is the only wait. M0 is
+// compiler-reserved: saved and restored inside the statement (cdna_hip_programming.md §5.7).
+template <int VAR>
 __device__ __forceinline__ void dma5(bf16* dst_rows, __amdgpu_buffer_rsrc_t rs, int go, int step) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst_rows, 16,
-                                           go + step, 0, 0, 0);
+  if (VAR & 524288) {
+    const unsigned lds = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)dst_rows);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(go + step), "s"(lds), "s"(rs)
+        : "memory");
+  } else {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst_rows, 16,
+                                             go + step, 0, 0, 0);
+  }
 }
 
 __device__ __forceinline__ float lane_pair_sum(float x) {
@@ -307,11 +325,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
 
   auto dma_k = [&](bf16* slot, int step) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma5(slot + 8 * (LPT * wave + i) * D, rk, c.kdo[i], step);
+    for (int i = 0; i < LPT; ++i) dma5<VAR>(slot + 8 * (LPT * wave + i) * D, rk, c.kdo[i], step);
   };
   auto dma_v = [&](bf16* slot, int step) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma5(slot + 8 * (LPT * wave + i) * D, rv, c.vdo[i], step);
+    for (int i = 0; i < LPT; ++i) dma5<VAR>(slot + 8 * (LPT * wave + i) * D, rv, c.vdo[i], step);
   };
 
   // VAR bit 4096 (8 waves): the younger half of the workgroup (waves 4-7) runs at issue
@@ -328,6 +346,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       dma_k(sK, 0);
       dma_v(sV, 0);
       dma_k(sK + TILE, ktile_b);
+      if (VAR & 524288) __builtin_amdgcn_s_waitcnt(0x0F70);  // asm DMA: hipcc does not wait
     } else {
       load5(rK, rk, c.kgo, 0);
       load5(rV, rv, c.vgo, 0);
@@ -574,6 +593,7 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
           : var == 33796 ? fa_fwd_bf16_v5<2, 33796, false, 8>
           : var == 37892 ? fa_fwd_bf16_v5<2, 37892, false, 8>
           : var == 99332 ? fa_fwd_bf16_v5<2, 99332, false, 8>
+          : var == 623620 ? fa_fwd_bf16_v5<2, 623620, false, 8>
                         : fa_fwd_bf16_v5<2, 4, false, 8>;
   else if (causal)
     kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;

@@ -290,7 +290,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # 50 / 51 causal v4 (4 / 8 waves) with query blocks paired heavy + light per workgroup,
 # 52 / 53 the same pairing in the d = 128 kernel (4 / 8 waves); the causal defaults pair
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39, 44, 45,
-                 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58)
+                 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
