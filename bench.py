@@ -117,15 +117,18 @@ def cpu_baseline(shape, seconds=12.0):
 
 
 def load_pmc_traffic(tag):
+    """HBM bytes per launch (and MFMA-busy fraction, effective clock) of the forward kernel
+    from the committed rocprofv3 PMC capture (profiles/pmc_<tag>.json)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
     if not os.path.exists(path):
-        return None, None
+        return None, None, {}
     try:
         with open(path) as f:
             j = json.load(f)
-        return j.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+        extra = {k: j[k] for k in ("mfma_busy_frac", "effective_clock_ghz") if k in j}
+        return j.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT), extra
     except Exception:
-        return None, None
+        return None, None, {}
 
 
 def main():
@@ -205,7 +208,7 @@ def main():
     ms_per_step = wall * 1e3 / args.steps
     achieved = flops_rank / (kern_ms * 1e-3) / 1e12
     alg_bytes = fwd_bytes(B, H, N, d)
-    traffic, traffic_src = load_pmc_traffic("fwd_bf16_c3" + ("_causal" if args.causal else ""))
+    traffic, traffic_src, pmc_extra = load_pmc_traffic("fwd_bf16_c3" + ("_causal" if args.causal else ""))
 
     result = {
         "metric": "FlashAttn fwd TFLOP/s (+ HBM GB/s) at (B,H,N,d)=(8,16,4096,64) per GPU",
@@ -233,6 +236,8 @@ def main():
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "pmc_mfma_busy_frac": pmc_extra.get("mfma_busy_frac"),
+            "pmc_effective_clock_ghz": pmc_extra.get("effective_clock_ghz"),
             "algorithmic_bytes": alg_bytes,
             "algorithmic_flops": flops_rank,
             "kernel_ms": round(kern_ms, 5),
