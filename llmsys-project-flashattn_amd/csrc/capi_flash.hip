@@ -251,6 +251,7 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
     // 1.31 ms: the masked diagonal steps spill in the 64-query form); policy 43 forces 0.
     const int variant = g_kernel_policy == 40   ? 1
                         : g_kernel_policy == 42 ? 2
+                        : g_kernel_policy == 62 ? 3  // 64-query steps, one wave per SIMD
                         : g_kernel_policy == 43 ? 0
                                                 : (causal ? 0 : 2);
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);

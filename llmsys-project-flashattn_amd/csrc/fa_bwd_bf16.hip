@@ -552,8 +552,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16(AttnArgs p, int nkb) {
 // dK/dV with 64-query steps: each barrier-to-barrier step stages two 32-query sub-tiles
 // (two ring sub-slots) and runs dkv_tile on both, halving the barriers and global-load
 // round trips per MFMA against the 32-query kernel above (A/B variant).
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16_q64(AttnArgs p, int nkb) {
+// MINB = workgroups per CU the register budget targets: 2 (two waves per SIMD, 256 VGPRs,
+// the compiler spills ~38 values into scratch inside the loop) or 1 (one wave per SIMD,
+// 512 VGPR+AGPR, no spills, no second wave to overlap with).
+template <bool CAUSAL, int MINB = 2>
+__global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int nkb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
@@ -879,9 +882,10 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     const int nkb = (a.N + 127) / 128;
     const int64_t nblk = (int64_t)nkb * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-    const size_t smem = (variant == 1 ? 3 : variant == 2 ? 4 : 2) * (size_t)kBufQ;
+    const size_t smem = (variant == 1 ? 3 : variant >= 2 ? 4 : 2) * (size_t)kBufQ;
     auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
                : variant == 2 ? fa_bwd_dkv_bf16_q64<CAUSAL>
+               : variant == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
                               : fa_bwd_dkv_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
