@@ -21,13 +21,13 @@ hipError_t launch_fwd_v2(const AttnArgs& a, bool causal, int nw, int resc, hipSt
                          bool* handled);
 hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
-                         bool* handled, bool pair = false);
+                         bool* handled, int pair = 0);
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
                          bool* handled);
 hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
-                           bool* handled, bool pair = false);
+                           bool* handled, int pair = 0);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
@@ -145,6 +145,8 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       e = launch_fwd_v5(a, false, 2, g_kernel_policy == 36 ? 2048 + 4 : 2048 + 1028, st, &handled);
     if (g_kernel_policy == 50 || g_kernel_policy == 51)  // causal v4, heavy + light block pairs
       e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 50 ? 4 : 8, !causal, st, &handled, true);
+    if (g_kernel_policy == 63 || g_kernel_policy == 64)  // 50 / 51 with the light block first
+      e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 63 ? 4 : 8, !causal, st, &handled, 2);
     if (g_kernel_policy == 61 && !causal)  // 56 with the LDS-DMA issued from inline asm
       e = launch_fwd_v5(a, false, 2, 2048 + 623620, st, &handled);
     if (g_kernel_policy >= 56 && g_kernel_policy <= 58 && !causal)  // 54 + exp-to-use distance
@@ -183,10 +185,13 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
       // Causal: v4 with heavy + light query blocks paired per workgroup
       // (profiles/r1_ab_causal_pair.txt): 4 waves (policy 50) below N = 8192 (860 vs 806
       // TF/s unpaired at C3, 824 for 8 waves), 8 waves (policy 51) from there (934 vs 898
-      // for 4 waves at (1,16,16384,64)).
+      // for 4 waves at (1,16,16384,64)). The light block of each pair runs first
+      // (policies 63 / 64, profiles/r1_ab_causal_lightfirst.txt): same time (±1 %), and
+      // the heavy block finds the light block's K/V tiles still in L2, so HBM traffic at C3
+      // drops from 321 to 273 MB per launch (algorithmic 270 MB).
       if (!handled)
         e = launch_fwd_v4(a, causal != 0, causal && N >= 8192 ? 8 : 4, !causal, st, &handled,
-                          causal != 0);
+                          causal ? 2 : 0);
     }
     // d = 128: the pipelined frozen-reference kernel (fa_fwd_d128.hip). Default: 8 waves
     // non-causal, 4 causal (warm-clock A/B, profiles/r1_ab_d128_warm.txt: non-causal 1085 vs
@@ -194,16 +199,20 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
     // 32 / 33 force 8 / 4 waves; 44 / 45 the same with LDS-DMA staging (neutral to -3 %).
     if (!handled && (g_kernel_policy == 0 || (g_kernel_policy >= 32 && g_kernel_policy <= 33) ||
                      (g_kernel_policy >= 44 && g_kernel_policy <= 45) || g_kernel_policy == 52 ||
-                     g_kernel_policy == 53)) {
+                     g_kernel_policy == 53 || (g_kernel_policy >= 63 && g_kernel_policy <= 65))) {
       // 44 / 45: 8 / 4 waves with LDS-DMA staging; 52 / 53: causal heavy + light block
       // pairs per workgroup, 4 / 8 waves
       const int nw = (g_kernel_policy == 32 || g_kernel_policy == 44 || g_kernel_policy == 53) ? 8
-                     : (g_kernel_policy == 33 || g_kernel_policy == 45 || g_kernel_policy == 52) ? 4
+                     : (g_kernel_policy == 33 || g_kernel_policy == 45 || g_kernel_policy == 52 ||
+                        g_kernel_policy == 63) ? 4
                      : 8;
       // causal default: 8 waves with paired query blocks (policy 53: 944 vs 866 TF/s for
       // unpaired 4 waves at (8,16,4096,128), 1101 vs 1020 at (1,16,16384,128))
       e = launch_fwd_d128(a, causal != 0, nw, g_kernel_policy == 44 || g_kernel_policy == 45, st,
-                          &handled, g_kernel_policy >= 52 || (g_kernel_policy == 0 && causal));
+                          &handled,
+                          g_kernel_policy >= 63 || (g_kernel_policy == 0 && causal) ? 2  // light first
+                          : g_kernel_policy >= 52                                    ? 1
+                                                                                     : 0);
     }
     // any shape the kernels above decline: the single-phase kernel, 8 waves by default
     // (faster than 4 at d = 128: 959 vs 802 TF/s at (1,16,16384,128))

@@ -204,8 +204,9 @@ __device__ __forceinline__ void bulk6(const bf16* sk, const bf16* sv, const Ctx6
 }  // namespace
 
 // PAIR (causal): a workgroup owns query blocks nqb-1-u and u of one head (heaviest, then
-// lightest), so every workgroup walks nqb + 1 key tiles (fa_fwd_v4.hip, same scheme).
-template <bool CAUSAL, int NW, bool DMA = false, bool PAIR = false>
+// lightest; PAIR = 2: lightest first), so every workgroup walks nqb + 1 key tiles
+// (fa_fwd_v4.hip, same scheme).
+template <bool CAUSAL, int NW, bool DMA = false, int PAIR = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, int nqb) {
   using C = C6<NW>;
   constexpr int LPT = C::LPT;
@@ -230,8 +231,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
   for (int rep = 0; rep < (PAIR ? 2 : 1); ++rep) {
   int qb = unit;
   if (PAIR) {
-    qb = rep ? unit : nqb - 1 - unit;
-    if (rep && qb == nqb - 1 - unit) break;  // odd nqb: the middle block has no partner
+    qb = (rep == (PAIR == 2 ? 0 : 1)) ? unit : nqb - 1 - unit;
+    if (rep && unit == nqb - 1 - unit) break;  // odd nqb: the middle block has no partner
   } else if (CAUSAL) {
     qb = nqb - 1 - qb;  // heaviest first
   }
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
   }  // rep
 }
 
-template <bool CAUSAL, int NW, bool DMA = false, bool PAIR = false>
+template <bool CAUSAL, int NW, bool DMA = false, int PAIR = 0>
 static hipError_t launch_d128_t(const AttnArgs& a, hipStream_t st) {
   const size_t smem = 4 * (size_t)TILE * sizeof(bf16);
   auto kfn = fa_fwd_bf16_d128<CAUSAL, NW, DMA, PAIR>;
@@ -425,15 +426,17 @@ static hipError_t launch_d128_t(const AttnArgs& a, hipStream_t st) {
 // to two tiles past N must fit the 31-bit buffer offset (the bulk loop stages one tile
 // ahead of the last one it needs).
 hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
-                           bool* handled, bool pair) {
+                           bool* handled, int pair) {
   *handled = false;
   if (a.d != D) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
+  if (causal && pair == 2)
+    return nw == 8 ? launch_d128_t<true, 8, false, 2>(a, st) : launch_d128_t<true, 4, false, 2>(a, st);
   if (causal && pair)
-    return nw == 8 ? launch_d128_t<true, 8, false, true>(a, st) : launch_d128_t<true, 4, false, true>(a, st);
+    return nw == 8 ? launch_d128_t<true, 8, false, 1>(a, st) : launch_d128_t<true, 4, false, 1>(a, st);
   if (dma) {
     if (nw == 8) return causal ? launch_d128_t<true, 8, true>(a, st) : launch_d128_t<false, 8, true>(a, st);
     return causal ? launch_d128_t<true, 4, true>(a, st) : launch_d128_t<false, 4, true>(a, st);

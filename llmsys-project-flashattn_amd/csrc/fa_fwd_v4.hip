@@ -227,8 +227,10 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
 
 // PAIR (causal only): a workgroup owns the query blocks nqb-1-u and u of one head (the
 // heaviest block, then the lightest), so every workgroup walks nqb + 1 key tiles and
-// the grid has no tail of heavy blocks dispatched last.
-template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false, bool PAIR = false>
+// the grid has no tail of heavy blocks dispatched last. PAIR = 2 walks the light block
+// first: the heavy block then re-reads the light block's key tiles while they are still in
+// the XCD's L2 (heavy-first re-reads them after nqb - 1 - u other tiles have passed).
+template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false, int PAIR = 0>
 __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb) {
   using C = V4<NW>;
   constexpr int D = 64;
@@ -252,8 +254,8 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb
   for (int rep = 0; rep < (PAIR ? 2 : 1); ++rep) {
   int qb = unit;
   if (PAIR) {
-    qb = rep ? unit : nqb - 1 - unit;
-    if (rep && qb == nqb - 1 - unit) break;  // odd nqb: the middle block has no partner
+    qb = (rep == (PAIR == 2 ? 0 : 1)) ? unit : nqb - 1 - unit;
+    if (rep && unit == nqb - 1 - unit) break;  // odd nqb: the middle block has no partner
   } else if (CAUSAL) {
     qb = nqb - 1 - qb;  // heaviest first
   }
@@ -434,7 +436,7 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb
   }  // rep
 }
 
-template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false, bool PAIR = false>
+template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false, int PAIR = 0>
 static hipError_t launch_v4_t(const AttnArgs& a, hipStream_t st) {
   const size_t smem = 4 * (size_t)kBK * 64 * sizeof(bf16);
   auto kfn = fa_fwd_bf16_v4<CAUSAL, NW, PK, ABL, DEEP, PAIR>;
@@ -468,16 +470,19 @@ hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream
 }
 
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
-                         bool* handled, bool pair) {
+                         bool* handled, int pair) {
   *handled = false;
   if (a.d != 64) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
+  if (causal && pair == 2)
+    return nw == 8 ? launch_v4_t<true, 8, false, 0, false, 2>(a, st)
+                   : launch_v4_t<true, 4, false, 0, false, 2>(a, st);
   if (causal && pair)
-    return nw == 8 ? launch_v4_t<true, 8, false, 0, false, true>(a, st)
-                   : launch_v4_t<true, 4, false, 0, false, true>(a, st);
+    return nw == 8 ? launch_v4_t<true, 8, false, 0, false, 1>(a, st)
+                   : launch_v4_t<true, 4, false, 0, false, 1>(a, st);
   if (pk) {
     if (nw == 8) return causal ? launch_v4_t<true, 8, true>(a, st) : launch_v4_t<false, 8, true>(a, st);
     return causal ? launch_v4_t<true, 4, true>(a, st) : launch_v4_t<false, 4, true>(a, st);

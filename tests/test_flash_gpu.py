@@ -288,9 +288,10 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # LDS-DMA staging (8 / 4 waves), 46 = 37 with single-issue f32 softmax VALU, 47 = 37 with
 # waves 4-7 staggered half a tile behind (4-slot V ring), 48 = 46 + 47, 49 = 47 + priority,
 # 50 / 51 causal v4 (4 / 8 waves) with query blocks paired heavy + light per workgroup,
-# 52 / 53 the same pairing in the d = 128 kernel (4 / 8 waves); the causal defaults pair
+# 52 / 53 the same pairing in the d = 128 kernel (4 / 8 waves); the causal defaults pair;
+# 63 / 64 = 50 / 51 and 65 = 53 with the light block of each pair walked first
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 7, 8, 9, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39, 44, 45,
-                 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61)
+                 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
