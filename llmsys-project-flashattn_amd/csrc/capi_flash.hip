@@ -261,6 +261,7 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
     const int variant = g_kernel_policy == 40   ? 1
                         : g_kernel_policy == 42 ? 2
                         : g_kernel_policy == 62 ? 3  // 64-query steps, one wave per SIMD
+                        : g_kernel_policy == 66 ? 4  // 64-query steps, Q / dO by LDS-DMA
                         : g_kernel_policy == 43 ? 0
                                                 : (causal ? 0 : 2);
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);

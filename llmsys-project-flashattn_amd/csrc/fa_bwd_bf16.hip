@@ -67,6 +67,23 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+// LDS-DMA: one wave instruction moves 64 x 16 B from per-lane buffer offsets (go) to 1 KiB
+// of LDS at dst in lane order (8 rows of a [rows][64] bf16 image); the image swizzle is
+// applied on the per-lane source. Issued from inline asm so hipcc's waitcnt pass does not
+// put a vmcnt(0) in front of the next LDS read (fa_fwd_v5.hip dma5, VAR bit 524288); the
+// caller waits vmcnt(0) before the barrier that publishes the slot. M0 is saved/restored.
+__device__ __forceinline__ void dma_rows(void* dst, __amdgpu_buffer_rsrc_t rs, int go) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)dst);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(go), "s"(lds), "s"(rs)
+      : "memory");
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
@@ -555,7 +572,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16(AttnArgs p, int nkb) {
 // MINB = workgroups per CU the register budget targets: 2 (two waves per SIMD, 256 VGPRs,
 // the compiler spills ~38 values into scratch inside the loop) or 1 (one wave per SIMD,
 // 512 VGPR+AGPR, no spills, no second wave to overlap with).
-template <bool CAUSAL, int MINB = 2>
+// DMA: the Q / dO images arrive by LDS-DMA (dma_rows) instead of buffer loads into VGPRs
+// plus ds_writes: no staging registers live across the step (policy 66, A/B variant).
+template <bool CAUSAL, int MINB = 2, bool DMA = false>
 __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int nkb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -594,6 +613,17 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
   const int srow = k_swz<D>(st_r, st_c), stri = v_swz<D>(st_r, st_c);
   const float* nlse = p.lse2 + (int64_t)bh * N;
   const float* ndel = p.delta + (int64_t)bh * N;
+  // DMA: wave w fills rows 8w..8w+7 of each image; lane l -> row 8w + l/8, LDS chunk l%8,
+  // which holds source chunk (l%8) ^ swz(row) (the swizzles are XOR, self-inverse)
+  int gdq[2] = {0, 0}, gdo[2] = {0, 0};
+  if (DMA) {
+    const int r = 8 * wave + (lane >> 3), pc = lane & 7;
+    const int ck = pc ^ ((r >> 1) & 7), cv = pc ^ (((r >> 1) & 1) << 2);
+    gdq[0] = (r * sqn + ck * 8) * 2;
+    gdq[1] = (r * sqn + cv * 8) * 2;
+    gdo[0] = (r * son + ck * 8) * 2;
+    gdo[1] = (r * son + cv * 8) * 2;
+  }
 
   constexpr int kStep = 2 * kQT;
   const int qt0 = CAUSAL ? k0 : 0;
@@ -601,12 +631,21 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
 
   uint4 sq[2], so[2];
   float sv = 0.f;
-#define DKV2_LOAD(T_)                                                                    \
+#define DKV2_LOAD(T_, SLOT_)                                                             \
   {                                                                                      \
     const int qs_ = qt0 + (T_) * kStep;                                                  \
     _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
-      sq[u] = bload(rq, goq + (qs_ + u * kQT) * sqn * 2);                                \
-      so[u] = bload(ro, goo + (qs_ + u * kQT) * son * 2);                                \
+      if (DMA) {                                                                         \
+        char* img_ = smem + (2 * (SLOT_) + u) * kBufQ + wave * 8 * D * 2;                \
+        const int oq_ = (qs_ + u * kQT) * sqn * 2, oo_ = (qs_ + u * kQT) * son * 2;      \
+        dma_rows(img_, rq, gdq[0] + oq_);                                                \
+        dma_rows(img_ + kImgQ * 2, rq, gdq[1] + oq_);                                    \
+        dma_rows(img_ + 2 * kImgQ * 2, ro, gdo[0] + oo_);                                \
+        dma_rows(img_ + 3 * kImgQ * 2, ro, gdo[1] + oo_);                                \
+      } else {                                                                           \
+        sq[u] = bload(rq, goq + (qs_ + u * kQT) * sqn * 2);                              \
+        so[u] = bload(ro, goo + (qs_ + u * kQT) * son * 2);                              \
+      }                                                                                  \
     }                                                                                    \
     if (tid < 4 * kQT) {                                                                 \
       const int q_ = qs_ + (tid >> 6) * kQT + (tid & (kQT - 1));                         \
@@ -615,15 +654,18 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
   }
 #define DKV2_STORE(SLOT_)                                                                \
   {                                                                                      \
-    _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
-      bf16* img = (bf16*)(smem + (2 * (SLOT_) + u) * kBufQ);                             \
-      *(uint4*)(img + srow) = sq[u];                                                     \
-      *(uint4*)(img + kImgQ + stri) = sq[u];                                             \
-      *(uint4*)(img + 2 * kImgQ + srow) = so[u];                                         \
-      *(uint4*)(img + 3 * kImgQ + stri) = so[u];                                         \
+    if (!DMA) {                                                                          \
+      _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                    \
+        bf16* img = (bf16*)(smem + (2 * (SLOT_) + u) * kBufQ);                           \
+        *(uint4*)(img + srow) = sq[u];                                                   \
+        *(uint4*)(img + kImgQ + stri) = sq[u];                                           \
+        *(uint4*)(img + 2 * kImgQ + srow) = so[u];                                       \
+        *(uint4*)(img + 3 * kImgQ + stri) = so[u];                                       \
+      }                                                                                  \
     }                                                                                    \
     if (tid < 4 * kQT)                                                                   \
       ((float*)((bf16*)(smem + (2 * (SLOT_) + (tid >> 6)) * kBufQ) + 4 * kImgQ))[tid & 63] = sv; \
+    if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                            \
   }
 
   f32x16 dK[2], dV[2];
@@ -632,7 +674,7 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
   const float c2 = p.scale_log2;
 
   if (nstep > 0) {
-    DKV2_LOAD(0)
+    DKV2_LOAD(0, 0)
     DKV2_STORE(0)
   }
   __syncthreads();
@@ -644,7 +686,7 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
   {                                                                                      \
     const int t_ = (T_);                                                                 \
     const bool more_ = t_ + 1 < nstep;                                                   \
-    if (more_) DKV2_LOAD(t_ + 1)                                                         \
+    if (more_) DKV2_LOAD(t_ + 1, (SLOT_) ^ 1)                                            \
     _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
       const int qt_ = qt0 + t_ * kStep + u * kQT;                                        \
       if (!(MASK_) || (qt_ < N && (!CAUSAL || qt_ + kQT - 1 >= wk_lo)))                 \
@@ -886,6 +928,7 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
                : variant == 2 ? fa_bwd_dkv_bf16_q64<CAUSAL>
                : variant == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
+               : variant == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
                               : fa_bwd_dkv_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
