@@ -1,25 +1,41 @@
 #!/usr/bin/env python3
-"""Headline benchmark: FlashAttention forward TFLOP/s + HBM GB/s at
-(B,H,N,d) = (8,16,4096,64) bf16 per GPU (BASELINE.json metric, configs[2]).
+"""Headline benchmark: FlashAttention forward TFLOP/s + HBM GB/s at (B,H,N,d) =
+(8,16,4096,64) bf16 (BASELINE.json metric, configs[2]), on 1, 2, 4 or 8 GPUs.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W [--config c3|c4] [--split strong|weak]
 
-One "step" = one pass of the hot path (the bf16 MFMA forward kernel) over one
-(8,16,4096,64) batch of synthetic Q/K/V already resident in HBM. Multi-GPU: one
-process per GPU (torch.distributed.run); the batch x heads axis is sharded, each
-rank owns its own (8,16,4096,64) slice of a global (8N,16,4096,64) problem
-(weak scaling, no collective inside the timed region). An RCCL all-gather of the
-output shards over xGMI (BASELINE config 4's exchange step) is timed separately
-and reported under "allgather".
+One "step" = one pass of the hot path (the bf16 MFMA forward kernel) over this rank's
+shard of the workload, with synthetic Q/K/V already resident in HBM. Multi-GPU: one
+process per GPU (torch.distributed.run, RCCL). The flattened batch x heads axis is
+sharded into contiguous per-rank ranges (every (b,h) head is
+independent, so there is no collective on the data path):
+
+  --config c3 (default)  the global problem is (8,16,4096,64).
+      --split strong (default): rank r owns heads [r*128/N, (r+1)*128/N): the total work
+                         is fixed, "scaling": "strong".
+      --split weak:      every rank owns a full (8,16,4096,64) slice of a global
+                         (8N,16,4096,64) problem: "scaling": "weak".
+  --config c4            BASELINE config 4: global (64,16,16384,128), strong split
+                         (1024/N heads per rank; at N = 1 the whole 2^31-element-per-tensor
+                         problem runs on one GPU).
+
+`value` = the global problem's flops per step x steps / the max-over-ranks wall time of
+the timed region (compute only: the forward kernel on every rank). With N > 1 the line
+also carries "end_to_end": the same steps with the RCCL all-gather of every rank's O
+shard (all_gather_into_tensor over xGMI) inside the timed region, max over ranks.
 
 rank 0 prints ONE JSON line with the contract fields plus:
-  roofline     : achieved TFLOP/s of the forward kernel (algorithmic flops / mean
-                 kernel duration from HIP events on the launch stream) vs the dense
-                 bf16 MFMA peak; "traffic" = HBM bytes per launch from the committed
-                 rocprofv3 PMC capture (profiles/), or null.
+  roofline     : achieved TFLOP/s of the forward kernel (algorithmic flops / mean kernel
+                 duration from HIP events on the launch stream) vs the dense bf16 MFMA
+                 peak; "traffic" = HBM bytes per launch from the committed rocprofv3 PMC
+                 capture (profiles/pmc_*.json), or null.
   cpu_baseline : the C restatement of the reference's CPU fast_ops attention
                  (oracle/attn_ref.c), timed on a bounded sample of heads of the same
-                 workload on this host (rank 0, N=1 only).
+                 workload on this host's cores (rank 0, N = 1 only).
+
+The orchestration (`run`) takes the attention function, the device and the process group
+as arguments, so tests/test_bench_dist.py drives the N > 1 code path on CPU with gloo
+and an injected attention.
 """
 from __future__ import annotations
 
@@ -36,10 +52,15 @@ sys.path.insert(0, ROOT)
 PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 4096 flop/clk x 2.4 GHz (MI355X_MICROARCH.md, dense)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBPS = 8000.0
-WORKLOAD = (8, 16, 4096, 64)
-
-
+CONFIGS = {"c3": (8, 16, 4096, 64), "c4": (64, 16, 16384, 128)}
+WORKLOAD = CONFIGS["c3"]
 PREWARM_S = 0.3  # untimed steady-clock ramp before the timed region (seconds)
+METRIC = "FlashAttn fwd TFLOP/s (+ HBM GB/s) at (B,H,N,d)=(8,16,4096,64); 1/2/4/8 GPU"
+
+
+def _sig(x, n=6):
+    """x to n significant digits (tiny CPU-test throughputs must not round to 0)."""
+    return float(f"{x:.{n}g}")
 
 
 def fwd_flops(B, H, N, d, causal=False):
@@ -52,43 +73,236 @@ def fwd_bytes(B, H, N, d, esize=2):
     return 4.0 * B * H * N * d * esize + 2.0 * B * H * N * 4
 
 
-def make_inputs(torch, shape, dtype, seed, rank):
-    """Synthetic N(0,1) inputs; shard r of the global tensor = global batch rows
-    [r*B, (r+1)*B), generated from (seed, global batch index)."""
-    B, H, N, d = shape
-    out = torch.empty(shape, dtype=dtype, device="cuda")
-    g = torch.Generator(device="cuda")
-    for b in range(B):
-        g.manual_seed(seed * 1000003 + rank * B + b)
-        out[b].copy_(torch.randn((H, N, d), generator=g, device="cuda", dtype=torch.float32))
+# ---- sharding plan -------------------------------------------------------------------
+def shard_plan(global_shape, world, rank, split="strong"):
+    """Per-rank slice of the flattened B*H axis.
+
+    strong: the global problem is fixed and rank r owns heads [r*BH/W, (r+1)*BH/W); the
+    shard is (B/W, H, N, d) when W divides B, else (1, BH/W, N, d) (both are one
+    contiguous block of the [B,H,N,d] layout). weak: every rank owns a full copy-shaped
+    slice, global = (W*B, H, N, d). Returns dict(global_shape, shard_shape, bh_lo, bh_hi)."""
+    B, H, N, d = global_shape
+    if split == "weak":
+        return {"global_shape": (B * world, H, N, d), "shard_shape": (B, H, N, d),
+                "bh_lo": rank * B * H, "bh_hi": (rank + 1) * B * H}
+    if split != "strong":
+        raise ValueError(f"unknown split {split!r}")
+    BH = B * H
+    if BH % world:
+        raise ValueError(f"B*H = {BH} heads do not split evenly over {world} ranks")
+    per = BH // world
+    shard = (B // world, H, N, d) if B % world == 0 else (1, per, N, d)
+    return {"global_shape": (B, H, N, d), "shard_shape": shard, "bh_lo": rank * per,
+            "bh_hi": (rank + 1) * per}
+
+
+def make_shard(torch, shard_shape, bh_lo, dtype, seed, device):
+    """Synthetic N(0,1) inputs from a generator keyed by (seed, global head index), so the
+    shard of rank r equals heads [bh_lo, bh_lo + rows) of the global tensor whatever W is."""
+    Bs, Hs, N, d = shard_shape
+    out = torch.empty(shard_shape, dtype=dtype, device=device)
+    flat = out.view(Bs * Hs, N, d)
+    g = torch.Generator(device=device)
+    for i in range(Bs * Hs):
+        g.manual_seed(seed * 1000003 + bh_lo + i)
+        flat[i].copy_(torch.randn((N, d), generator=g, device=device, dtype=torch.float32))
     return out
 
 
-def time_kernel(torch, fn, steps, warmup):
-    for _ in range(warmup):
-        fn()
-    torch.cuda.synchronize()
-    st = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(steps):
-        fn()
-    e1.record(st)
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / steps  # ms per launch
+class Clock:
+    """Device timing: HIP events on the launch stream on a GPU, perf_counter on CPU."""
+
+    def __init__(self, torch, device):
+        self.torch = torch
+        self.gpu = device != "cpu"
+
+    def sync(self):
+        if self.gpu:
+            self.torch.cuda.synchronize()
+
+    def span(self, fn, steps):
+        """(mean ms per call of fn over `steps` calls, measured on the device)."""
+        if self.gpu:
+            st = self.torch.cuda.current_stream()
+            e0 = self.torch.cuda.Event(enable_timing=True)
+            e1 = self.torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(steps):
+                fn()
+            e1.record(st)
+            self.torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / steps
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        return (time.perf_counter() - t0) * 1e3 / steps
 
 
-def cpu_baseline(shape, seconds=12.0):
-    """Time the C oracle on a bounded sample of (b,h) heads at full N and d."""
-    import numpy as np
-    from oracle import cref
-    B, H, N, d = shape
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+def _timed_region(torch, clock, dist, world, fn, steps):
+    """Barrier + sync on both sides of exactly `steps` calls; returns (wall s and device ms
+    per call, both the MAX over ranks; this rank's own device ms per call)."""
+    if world > 1:
+        dist.barrier()
+    clock.sync()
+    t0 = time.perf_counter()
+    dev_ms = clock.span(fn, steps)
+    clock.sync()
+    if world > 1:
+        dist.barrier()
+    clock.sync()
+    wall = time.perf_counter() - t0
+    own_ms = dev_ms
+    if world > 1:
+        t = torch.tensor([wall, dev_ms], dtype=torch.float64)
+        if clock.gpu:
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, dev_ms = float(t[0]), float(t[1])
+    return wall, dev_ms, own_ms
+
+
+def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2):
+    """The bench's timed legs for this rank. attn_fwd(q, k, v, causal, out) runs the hot
+    path on a shard. Returns the result dict (rank 0 prints it) and, for tests, the
+    gathered output (N > 1) or this rank's output."""
+    base = CONFIGS[args.config] if args.shape is None else tuple(args.shape)
+    split = "strong" if args.config == "c4" else args.split
+    plan = shard_plan(base, world, rank, split)
+    gshape, sshape = plan["global_shape"], plan["shard_shape"]
+    q, k, v = (make_shard(torch, sshape, plan["bh_lo"], dtype, s, device) for s in (1, 2, 3))
+    o = torch.empty_like(q)
+    clock = Clock(torch, device)
+
+    def step():
+        attn_fwd(q, k, v, args.causal, o)
+
+    for _ in range(args.warmup):
+        step()
+    clock.sync()
+    # untimed clock ramp: keep stepping until PREWARM_S of device work has run, so the
+    # timed region starts at the steady-state clock whatever W the caller passes (the
+    # first launches on a cold GPU run up to 30 % slower: profiles/r1e_kernel_stats.csv)
+    t_ramp = time.perf_counter()
+    while clock.gpu and time.perf_counter() - t_ramp < PREWARM_S:
+        for _ in range(10):
+            step()
+        clock.sync()
+
+    # kern_ms: this rank's mean kernel time from HIP events on the launch stream over the
+    # timed region (the roofline's denominator)
+    wall, kern_ms_max, kern_ms = _timed_region(torch, clock, dist, world, step, args.steps)
+    B, H, N, d = gshape
+    total_flops = fwd_flops(B, H, N, d, args.causal) * args.steps
+    value = total_flops / wall / 1e12
+    flops_rank = fwd_flops(*sshape, args.causal)
+    achieved = flops_rank / (kern_ms * 1e-3) / 1e12
+    alg_bytes = fwd_bytes(*sshape, esize=esize)
+    tag = ("fwd_bf16_c4" if args.config == "c4" else "fwd_bf16_c3") + ("_causal" if args.causal else "")
+    traffic, traffic_src, pmc_extra = load_pmc_traffic(tag) if world == 1 else (None, None, {})
+
+    result = {
+        "metric": METRIC,
+        "value": _sig(value),
+        "unit": "TFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "prewarm_s": PREWARM_S,
+        "ms_per_step": round(wall * 1e3 / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": split,
+        "vs_baseline": None,
+        "dtype": "bf16" if esize == 2 else "f32",
+        "data": "synthetic N(0,1) Q/K/V (counter-seeded per global head), resident in HBM",
+        "config": {"workload": f"flash_attention_fwd {args.config}", "B": B, "H": H, "N": N,
+                   "d": d, "per_gpu_shape": list(sshape), "causal": bool(args.causal),
+                   "parallelism": f"bh-shard x{world} ({split})"},
+        "hbm_gbps": round(fwd_bytes(B, H, N, d, esize) * args.steps / wall / 1e9, 2),
+        "roofline": {
+            "bound": "mfma",
+            "achieved": round(achieved, 2),
+            "peak": PEAK_BF16_TFLOPS if esize == 2 else PEAK_F32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / (PEAK_BF16_TFLOPS if esize == 2 else PEAK_F32_TFLOPS), 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "pmc_mfma_busy_frac": pmc_extra.get("mfma_busy_frac"),
+            "pmc_effective_clock_ghz": pmc_extra.get("effective_clock_ghz"),
+            "algorithmic_bytes": alg_bytes,
+            "algorithmic_flops": flops_rank,
+            "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_max_over_ranks_timed": round(kern_ms_max, 5),
+        },
+    }
+
+    gathered = None
+    if world > 1:
+        # end to end: the forward plus the RCCL all-gather of the O shards, both inside the
+        # timed region (SURVEY.md §8(e) leg (ii))
+        # concatenated along the leading axis: rank order = global head order
+        gathered = torch.empty((world * o.shape[0],) + tuple(o.shape[1:]), dtype=o.dtype,
+                               device=o.device)
+
+        def step_gather():
+            step()
+            dist.all_gather_into_tensor(gathered, o)
+
+        for _ in range(2):
+            step_gather()
+        clock.sync()
+        tg, _, _ = _timed_region(torch, clock, dist, world, step_gather, args.steps)
+        result["end_to_end"] = {
+            "what": "forward + all_gather_into_tensor of every rank's O shard, per step",
+            "ms_per_step": round(tg * 1e3 / args.steps, 4),
+            "tflops": _sig(total_flops / tg / 1e12),
+            "gathered_bytes_per_rank": int(o.numel() * o.element_size() * world),
+            "allgather_gbps_per_rank": round(o.numel() * o.element_size() * (world - 1) * args.steps
+                                             / max(tg - wall, 1e-9) / 1e9, 2),
+        }
+    return result, (gathered if gathered is not None else o), (q, k, v)
+
+
+def _cpu_cores():
+    """Cores this process may use: the affinity mask, capped by a cgroup CPU quota when
+    one is set (the GPU boxes show the whole machine in the mask)."""
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    threads = min(threads or avail, avail, 16)
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    cores = avail if quota is None else max(1, min(avail, int(quota + 0.5)))
+    return cores, avail, quota
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(shape, seconds=12.0):
+    """Time the C oracle on a bounded sample of (b,h) heads at full N and d, on every
+    core this process may use."""
+    import numpy as np
+    from oracle import cref
+    B, H, N, d = shape
+    threads, avail, quota = _cpu_cores()
     rng = np.random.default_rng(0)
     one = [rng.standard_normal((1, N, d)).astype(np.float32) for _ in range(3)]
     t0 = time.perf_counter()
@@ -108,10 +322,13 @@ def cpu_baseline(shape, seconds=12.0):
         "value": round(flops / dt / 1e12, 6),
         "unit": "TFLOP/s",
         "cores": threads,
+        "cores_in_affinity_mask": avail,
+        "cgroup_cpu_quota": quota,
+        "cpu_model": _cpu_model(),
         "kind": "port",
         "sample": f"{reps} pass(es) over {heads} of {B*H} (b,h) heads at N={N}, d={d}, fp32 "
-                  f"(C restatement of the reference fast_ops attention, oracle/attn_ref.c), "
-                  f"{dt:.1f} s",
+                  f"(C restatement of the reference fast_ops attention, oracle/attn_ref.c, "
+                  f"OpenMP over (head,row) on {threads} threads), {dt:.1f} s",
         "seconds": round(dt, 2),
     }
 
@@ -131,185 +348,113 @@ def load_pmc_traffic(tag):
         return None, None, {}
 
 
-def main():
+def extra_legs(torch, _hip, time_fn):
+    """Single-GPU side legs (rank 0, N = 1): causal forward, bf16 backward, config 2 fp32,
+    and the config-4 per-GPU shard at 8 GPUs."""
+    extra = {}
+    B, H, N, d = WORKLOAD
+    q, k, v, do = (make_shard(torch, WORKLOAD, 0, torch.bfloat16, s, "cuda") for s in (1, 2, 3, 4))
+    o = torch.empty_like(q)
+    m = torch.empty((B, H, N), dtype=torch.float32, device="cuda")
+    l = torch.empty_like(m)
+    extra["fwd_causal_tflops"] = round(fwd_flops(B, H, N, d, True) / (time_fn(
+        lambda: _hip.flash_fwd(q, k, v, True, out=o, m=m, l=l), 20, 3) * 1e-3) / 1e12, 2)
+    # backward (bf16), FA-2 flop convention 2.5 x fwd
+    _hip.flash_fwd(q, k, v, False, out=o, m=m, l=l)
+    ws = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(B, H, N, d) // 4,
+                     dtype=torch.float32, device="cuda")
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
+    bwd_ms = time_fn(lambda: _hip.flash_bwd(q, k, v, o, do, m, l, False, dq=dq, dk=dk, dv=dv,
+                                            workspace=ws), 10, 2)
+    extra["bwd_ms"] = round(bwd_ms, 4)
+    extra["bwd_tflops"] = round(2.5 * fwd_flops(B, H, N, d) / (bwd_ms * 1e-3) / 1e12, 2)
+    _hip.flash_fwd(q, k, v, True, out=o, m=m, l=l)
+    bwdc_ms = time_fn(lambda: _hip.flash_bwd(q, k, v, o, do, m, l, True, dq=dq, dk=dk, dv=dv,
+                                             workspace=ws), 10, 2)
+    extra["bwd_causal_ms"] = round(bwdc_ms, 4)
+    extra["bwd_causal_tflops"] = round(2.5 * fwd_flops(B, H, N, d, True) / (bwdc_ms * 1e-3) / 1e12, 2)
+    del q, k, v, do, o, m, l, dq, dk, dv, ws
+    # config 2: (8,16,1024,64) fp32 forward
+    c2 = (8, 16, 1024, 64)
+    q2, k2, v2 = (make_shard(torch, c2, 0, torch.float32, s, "cuda") for s in (5, 6, 7))
+    c2_ms = time_fn(lambda: _hip.flash_fwd(q2, k2, v2, False), 20, 3)
+    extra["c2_fp32_fwd_ms"] = round(c2_ms, 4)
+    extra["c2_fp32_fwd_tflops"] = round(fwd_flops(*c2) / (c2_ms * 1e-3) / 1e12, 2)
+    extra["c2_fp32_frac_of_f32_peak"] = round(extra["c2_fp32_fwd_tflops"] / PEAK_F32_TFLOPS, 4)
+    del q2, k2, v2
+    # config 4's per-GPU shard at 8 GPUs: (8,16,16384,128) bf16 forward (1/8 of B = 64)
+    c4 = (8, 16, 16384, 128)
+    q4, k4, v4 = (make_shard(torch, c4, 0, torch.bfloat16, s, "cuda") for s in (8, 9, 10))
+    o4 = torch.empty_like(q4)
+    m4 = torch.empty(c4[:3], dtype=torch.float32, device="cuda")
+    l4 = torch.empty_like(m4)
+    c4_ms = time_fn(lambda: _hip.flash_fwd(q4, k4, v4, False, out=o4, m=m4, l=l4), 5, 1)
+    extra["c4_shard_bf16_fwd_ms"] = round(c4_ms, 3)
+    extra["c4_shard_bf16_fwd_tflops"] = round(fwd_flops(*c4) / (c4_ms * 1e-3) / 1e12, 2)
+    return extra
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
+    ap.add_argument("--split", choices=("strong", "weak"), default="strong")
     ap.add_argument("--causal", action="store_true")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra (bwd, fp32) legs")
-    ap.add_argument("--policy", type=int, default=0, help="0 auto, 1 generic kernels only")
-    args = ap.parse_args()
+    ap.add_argument("--policy", type=int, default=0, help="kernel policy (0 default)")
+    ap.add_argument("--shape", type=int, nargs=4, default=None, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N processes with "
+              f"torch.distributed.run --nproc-per-node N and pass --gpus N", file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
     from minitorch import _hip
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes",
-                  file=sys.stderr)
-            sys.exit(2)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    _hip.lib().mt_flash_set_kernel_policy(args.policy)
+    _hip.set_policy(args.policy)
 
-    B, H, N, d = WORKLOAD
-    q, k, v = (make_inputs(torch, WORKLOAD, torch.bfloat16, s, rank) for s in (1, 2, 3))
-    o = torch.empty_like(q)
-    m = torch.empty((B, H, N), dtype=torch.float32, device="cuda")
-    l = torch.empty_like(m)
+    # m / l outputs are part of the forward's contract: keep them written every step
+    ml = {}
 
-    def step():
-        _hip.flash_fwd(q, k, v, args.causal, out=o, m=m, l=l)
+    def attn_ml(q, k, v, causal, out):
+        key = tuple(q.shape[:3])
+        if key not in ml:
+            ml[key] = (torch.empty(key, dtype=torch.float32, device=q.device),
+                       torch.empty(key, dtype=torch.float32, device=q.device))
+        m, l = ml[key]
+        _hip.flash_fwd(q, k, v, causal, out=out, m=m, l=l)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    # untimed clock ramp: keep stepping until PREWARM_S of GPU work has run, so the timed
-    # region starts at the steady-state clock whatever W the caller passes (the first
-    # launches on a cold GPU run up to 30 % slower: profiles/r1e_kernel_stats.csv max)
-    t_ramp = time.perf_counter()
-    while time.perf_counter() - t_ramp < PREWARM_S:
-        for _ in range(10):
-            step()
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    st = torch.cuda.current_stream()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(st)
-    for _ in range(args.steps):
-        step()
-    ev1.record(st)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        t = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, kern_ms_max = float(t[0]), float(t[1])
-    else:
-        kern_ms_max = kern_ms
+    result, _, _ = run(args, attn_ml, torch, dist, world, rank, f"cuda:{local}", torch.bfloat16)
 
-    flops_rank = fwd_flops(B, H, N, d, args.causal)
-    total_flops = flops_rank * world * args.steps
-    value = total_flops / wall / 1e12
-    ms_per_step = wall * 1e3 / args.steps
-    achieved = flops_rank / (kern_ms * 1e-3) / 1e12
-    alg_bytes = fwd_bytes(B, H, N, d)
-    traffic, traffic_src, pmc_extra = load_pmc_traffic("fwd_bf16_c3" + ("_causal" if args.causal else ""))
+    if rank == 0 and world == 1 and not args.no_extra and args.config == "c3":
+        clock = Clock(torch, "cuda")
 
-    result = {
-        "metric": "FlashAttn fwd TFLOP/s (+ HBM GB/s) at (B,H,N,d)=(8,16,4096,64) per GPU",
-        "value": round(value, 3),
-        "unit": "TFLOP/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "prewarm_s": PREWARM_S,
-        "ms_per_step": round(ms_per_step, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16",
-        "data": "synthetic N(0,1) Q/K/V, resident in HBM",
-        "config": {"workload": "flash_attention_fwd", "B": B * world, "H": H, "N": N, "d": d,
-                   "per_gpu_shape": [B, H, N, d], "causal": bool(args.causal),
-                   "parallelism": f"bh-shard x{world}"},
-        "hbm_gbps": round(alg_bytes * world * args.steps / wall / 1e9, 2),
-        "roofline": {
-            "bound": "mfma",
-            "achieved": round(achieved, 2),
-            "peak": PEAK_BF16_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "pmc_mfma_busy_frac": pmc_extra.get("mfma_busy_frac"),
-            "pmc_effective_clock_ghz": pmc_extra.get("effective_clock_ghz"),
-            "algorithmic_bytes": alg_bytes,
-            "algorithmic_flops": flops_rank,
-            "kernel_ms": round(kern_ms, 5),
-        },
-    }
+        def time_fn(fn, steps, warmup):
+            for _ in range(warmup):
+                fn()
+            clock.sync()
+            return clock.span(fn, steps)
 
-    # RCCL all-gather of the output shards (BASELINE config 4's exchange step).
-    if world > 1:
-        gathered = torch.empty((world,) + tuple(o.shape), dtype=o.dtype, device="cuda")
-
-        def step_gather():
-            step()
-            dist.all_gather_into_tensor(gathered, o)
-
-        for _ in range(3):
-            step_gather()
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step_gather()
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-        tg = float(tg[0])
-        result["allgather"] = {
-            "ms_per_step_fwd_plus_allgather": round(tg * 1e3 / args.steps, 4),
-            "tflops_fwd_plus_allgather": round(total_flops / tg / 1e12, 3),
-            "gathered_bytes_per_rank": int(o.numel() * o.element_size() * world),
-        }
-
-    if rank == 0 and world == 1 and not args.no_extra:
-        extra = {}
-        # causal forward, same workload
-        extra["fwd_causal_tflops"] = round(
-            fwd_flops(B, H, N, d, True) / (time_kernel(
-                torch, lambda: _hip.flash_fwd(q, k, v, True, out=o, m=m, l=l), 20, 3) * 1e-3) / 1e12, 2)
-        # backward (bf16), FA-2 flop convention 2.5 x fwd
-        do = make_inputs(torch, WORKLOAD, torch.bfloat16, 4, rank)
-        _hip.flash_fwd(q, k, v, False, out=o, m=m, l=l)
-        ws = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(B, H, N, d) // 4,
-                         dtype=torch.float32, device="cuda")
-        dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
-        bwd_ms = time_kernel(torch, lambda: _hip.flash_bwd(q, k, v, o, do, m, l, False, dq=dq, dk=dk,
-                                                          dv=dv, workspace=ws), 10, 2)
-        extra["bwd_ms"] = round(bwd_ms, 4)
-        extra["bwd_tflops"] = round(2.5 * fwd_flops(B, H, N, d) / (bwd_ms * 1e-3) / 1e12, 2)
-        del do, dq, dk, dv, ws
-        # config 2: (8,16,1024,64) fp32 forward
-        c2 = (8, 16, 1024, 64)
-        q2, k2, v2 = (make_inputs(torch, c2, torch.float32, s, 0) for s in (5, 6, 7))
-        c2_ms = time_kernel(torch, lambda: _hip.flash_fwd(q2, k2, v2, False), 20, 3)
-        extra["c2_fp32_fwd_ms"] = round(c2_ms, 4)
-        extra["c2_fp32_fwd_tflops"] = round(fwd_flops(*c2) / (c2_ms * 1e-3) / 1e12, 2)
-        extra["c2_fp32_frac_of_f32_peak"] = round(extra["c2_fp32_fwd_tflops"] / PEAK_F32_TFLOPS, 4)
-        del q2, k2, v2
-        # config 4's per-GPU shard at 8 GPUs: (8,16,16384,128) bf16 forward (1/8 of B=64)
-        c4 = (8, 16, 16384, 128)
-        q4, k4, v4 = (make_inputs(torch, c4, torch.bfloat16, s, 0) for s in (8, 9, 10))
-        o4 = torch.empty_like(q4)
-        m4 = torch.empty(c4[:3], dtype=torch.float32, device="cuda")
-        l4 = torch.empty_like(m4)
-        c4_ms = time_kernel(torch, lambda: _hip.flash_fwd(q4, k4, v4, False, out=o4, m=m4, l=l4), 5, 1)
-        extra["c4_shard_bf16_fwd_ms"] = round(c4_ms, 3)
-        extra["c4_shard_bf16_fwd_tflops"] = round(fwd_flops(*c4) / (c4_ms * 1e-3) / 1e12, 2)
-        del q4, k4, v4, o4, m4, l4
-        result["extra"] = extra
+        result["extra"] = extra_legs(torch, _hip, time_fn)
 
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(WORKLOAD)
-        cpu["gpu_over_cpu"] = round(value / cpu["value"], 1) if cpu["value"] > 0 else None
+        cpu = cpu_baseline(CONFIGS[args.config])
+        cpu["gpu_over_cpu"] = round(result["value"] / cpu["value"], 1) if cpu["value"] > 0 else None
         result["cpu_baseline"] = cpu
 
     if rank == 0:

@@ -36,10 +36,14 @@ enum { MT_F32 = 0, MT_BF16 = 1 };
 /* ---- status ------------------------------------------------------------- */
 const char* mt_last_error(void);
 int mt_abi_version(void);
-/* Forward kernel selection (A/B testing). 0 (default): the bf16 MFMA kernel specialised
- * for d in {64, 128} when the layout allows it, else the generic kernel; 1: always the
- * generic tiled kernels; 2, 4, 5, 6: alternative bf16 schedules (see fa_fwd_fast.hip). */
-void mt_flash_set_kernel_policy(int policy);
+/* Kernel selection for A/B timing. 0 (default): the bf16 MFMA kernels specialised for
+ * d in {64, 128} where the layout allows, else the generic kernels; 1: the generic tiled
+ * kernels only; other ids: alternative bf16 schedules, each computing the same attention
+ * (the list and what each id selects: csrc/capi_flash.hip, enum kPol*). Returns 0, or 1
+ * for an id the library does not know (the policy is then unchanged). Process-wide,
+ * read atomically at each launch. */
+int mt_flash_set_kernel_policy(int policy);
+int mt_flash_get_kernel_policy(void);
 
 /* ---- FlashAttention, device pointers ------------------------------------- */
 /* O = softmax(Q Kᵀ/√d [causal]) V;  m[b,h,n] = row max of the scaled logits,

@@ -11,18 +11,15 @@
 #include "../../include/minitorch_hip.h"
 #include "fa_common.h"
 #include <algorithm>
+#include <atomic>
 
 namespace mt {
 hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
 hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStream_t st,
                            bool* handled);
-hipError_t launch_fwd_v2(const AttnArgs& a, bool causal, int nw, int resc, hipStream_t st,
-                         bool* handled);
-hipError_t launch_fwd_v3(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
                          bool* handled, int pair = 0);
-hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
                          bool* handled);
@@ -31,11 +28,80 @@ hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hip
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st);
+#ifdef MT_DIAGNOSTICS
+hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
+#endif
 
 static thread_local char g_err[512] = "";
-static int g_kernel_policy = 0;  // 0: default bf16 MFMA kernels, 1: generic kernels only,
-                                 // other values: A/B variants (fa_fwd_fast/v2/v3/v4.hip,
-                                 // listed in tests/test_flash_gpu.py FAST_POLICIES)
+
+// ---- kernel policies (A/B selection) ------------------------------------------------
+// Every id below computes the same attention as the default; each has its own parity
+// tests (tests/test_flash_gpu.py FAST_POLICIES / test_bf16_bwd_policies_vs_oracle). The
+// ids are the ones the round-1 A/B records under profiles/ cite. mt_flash_set_kernel_policy
+// rejects anything else with a status. Timing-only ablations that compute WRONG results
+// exist only in a diagnostics build (make DIAG=1 -> libminitorch_hip_diag.so, compiled with
+// -DMT_DIAGNOSTICS), never in the product library.
+enum : int {
+  kPolDefault = 0,
+  kPolGeneric = 1,  // generic tiled kernels only (fa_fwd.hip / fa_bwd.hip)
+  // fa_fwd_fast.hip: 2 single-phase 8-wave, 3 single-phase 4-wave, 4 / 5 software-pipelined
+  // 8 / 4-wave, 6 ping-pong 8-wave
+  kPolFast8 = 2, kPolFast4 = 3, kPolFastSp8 = 4, kPolFastSp4 = 5, kPolFastPp = 6,
+  // fa_fwd_v4.hip: 21 / 22 4 / 8 waves, 23 / 24 packed-f32 softmax 8 / 4 waves, 25 / 26
+  // 4 waves with staging one iteration deeper (packed / scalar)
+  kPolV4w4 = 21, kPolV4w8 = 22, kPolV4Pk8 = 23, kPolV4Pk4 = 24, kPolV4DeepPk = 25,
+  kPolV4Deep = 26,
+  // causal v4 with heavy + light query blocks per workgroup (50 / 51: 4 / 8 waves, heavy
+  // first; 63 / 64: light first); d = 128: 52 / 53 heavy first (4 / 8 waves), 65 light first
+  kPolV4Pair4 = 50, kPolV4Pair8 = 51, kPolD128Pair4 = 52, kPolD128Pair8 = 53,
+  kPolV4PairLF4 = 63, kPolV4PairLF8 = 64, kPolD128PairLF8 = 65,
+  // fa_fwd_v5.hip: 27 / 28 / 29 LDS reads 2 / 4 / 6 MFMAs ahead (27 unrolled), 31 not
+  // unrolled, 35 LDS-DMA, 36 / 37 8 waves (37 + LDS-DMA), 38 4-wave register-staged,
+  // 39 = 37 + static priority, 46 single-issue softmax VALU, 47 waves 4-7 staggered,
+  // 48 = 46 + 47, 49 = 47 + priority, 54 / 55 Vᵀ reuse (55 + priority), 56 = 54 + exp-to-use
+  // distance (the d = 64 default), 57 / 58 = 56 with reads 3 / 4 ahead, 61 = 56 with the DMA
+  // from inline asm
+  kPolV5a2 = 27, kPolV5a4 = 28, kPolV5a6 = 29, kPolV5NoUnroll = 31, kPolV5Dma = 35,
+  kPolV5w8 = 36, kPolV5w8Dma = 37, kPolV5w4Reg = 38, kPolV5Prio = 39, kPolV5Scalar = 46,
+  kPolV5Stagger = 47, kPolV5ScalarStagger = 48, kPolV5StaggerPrio = 49, kPolV5VKeep = 54,
+  kPolV5VKeepPrio = 55, kPolV5Defer = 56, kPolV5Defer3 = 57, kPolV5Defer4 = 58,
+  kPolV5AsmDma = 61,
+  // fa_fwd_d128.hip: 32 / 33 8 / 4 waves, 44 / 45 the same with LDS-DMA staging
+  kPolD128w8 = 32, kPolD128w4 = 33, kPolD128Dma8 = 44, kPolD128Dma4 = 45,
+  // fa_bwd_bf16.hip dK/dV forms: 40 software-pipelined, 42 64-query steps, 43 32-query
+  // steps, 62 64-query steps at one wave per SIMD, 66 64-query steps with LDS-DMA Q/dO
+  kPolBwdPipe = 40, kPolBwdQ64 = 42, kPolBwdQ32 = 43, kPolBwdQ64OneWave = 62,
+  kPolBwdQ64Dma = 66,
+};
+static const int kValidPolicies[] = {
+    kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
+    kPolV4w4, kPolV4w8, kPolV4Pk8, kPolV4Pk4, kPolV4DeepPk, kPolV4Deep, kPolV4Pair4,
+    kPolV4Pair8, kPolD128Pair4, kPolD128Pair8, kPolV4PairLF4, kPolV4PairLF8, kPolD128PairLF8,
+    kPolV5a2, kPolV5a4, kPolV5a6, kPolV5NoUnroll, kPolV5Dma, kPolV5w8, kPolV5w8Dma,
+    kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
+    kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
+    kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
+    kPolBwdQ64, kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma};
+static std::atomic<int> g_kernel_policy{kPolDefault};
+
+static bool policy_valid(int p) {
+  for (int v : kValidPolicies)
+    if (v == p) return true;
+#ifdef MT_DIAGNOSTICS
+  // wrong-result ablations (timing only): v5 80-86 / 97, v4 91-96, fast 10-15
+  if ((p >= 80 && p <= 86) || p == 97 || (p >= 91 && p <= 96) || (p >= 10 && p <= 15)) return true;
+#endif
+  return false;
+}
+
+// v5 template variants (VAR bits, fa_fwd_v5.hip): unrolled tile loop, LDS-DMA staging,
+// 8 waves (launcher only), static priority for waves 4-7, single-issue softmax VALU,
+// staggered waves, Vᵀ fragment reuse, exp-to-use distance, DMA from inline asm.
+namespace v5 {
+constexpr int kUnroll = 4, kDma = 1024, kW8 = 2048, kPrio = 4096, kScalar = 8192,
+              kStagger = 16384, kVKeep = 32768, kDefer = 65536, kAsmDma = 524288;
+constexpr int kDefault = kW8 | kDefer | kVKeep | kDma | kUnroll;
+}  // namespace v5
 
 int set_error(const char* fmt, ...) {
   va_list ap;
@@ -82,6 +148,120 @@ static int check_sizes(int dtype, int64_t B, int64_t H, int64_t N, int64_t d) {
   return 0;
 }
 
+// bf16 forward with 16-B rows: pick the MFMA kernel for policy `pol`. Returns with
+// *handled = false when no bf16 MFMA kernel takes the shape (the caller then runs the
+// generic kernel).
+static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hipStream_t st,
+                                    bool* handled) {
+  *handled = false;
+  hipError_t e = hipSuccess;
+  const int N = a.N;
+  switch (pol) {
+    case kPolV4w4: case kPolV4w8: case kPolV4Pk8: case kPolV4Pk4:
+      e = launch_fwd_v4(a, causal, (pol == kPolV4w8 || pol == kPolV4Pk8) ? 8 : 4,
+                        pol == kPolV4Pk8 || pol == kPolV4Pk4, st, handled);
+      break;
+    case kPolV4DeepPk: case kPolV4Deep:
+      if (a.d == 64 && ((int64_t)N + 128) * std::max(a.sk[2], a.sv[2]) * 2 < ((int64_t)1 << 31)) {
+        e = launch_fwd_v4_deep(a, causal, pol == kPolV4DeepPk, st);
+        *handled = true;
+      }
+      break;
+    case kPolV4Pair4: case kPolV4Pair8:  // heavy + light block pairs, heavy first
+      e = launch_fwd_v4(a, causal, pol == kPolV4Pair4 ? 4 : 8, !causal, st, handled, 1);
+      break;
+    case kPolV4PairLF4: case kPolV4PairLF8:  // light first
+      e = launch_fwd_v4(a, causal, pol == kPolV4PairLF4 ? 4 : 8, !causal, st, handled, 2);
+      break;
+    case kPolV5a2: case kPolV5a4: case kPolV5a6:
+      e = launch_fwd_v5(a, causal, 2 * (pol - kPolV5a2 + 1), pol == kPolV5a2 ? v5::kUnroll : 0,
+                        st, handled);
+      break;
+    case kPolV5NoUnroll: e = launch_fwd_v5(a, causal, 2, 0, st, handled); break;
+    default: break;
+  }
+  if (!causal && !*handled) {  // non-causal-only v5 forms
+    int var = -1, ahead = 2;
+    switch (pol) {
+      case kPolV5Dma: var = v5::kDma | v5::kUnroll; break;
+      case kPolV5w8: var = v5::kW8 | v5::kUnroll; break;
+      case kPolV5w8Dma: var = v5::kW8 | v5::kDma | v5::kUnroll; break;
+      case kPolV5w4Reg: var = v5::kUnroll; break;
+      case kPolV5Prio: var = v5::kW8 | v5::kPrio | v5::kDma | v5::kUnroll; break;
+      case kPolV5Scalar: var = v5::kW8 | v5::kScalar | v5::kDma | v5::kUnroll; break;
+      case kPolV5Stagger: var = v5::kW8 | v5::kStagger | v5::kDma | v5::kUnroll; break;
+      case kPolV5ScalarStagger:
+        var = v5::kW8 | v5::kScalar | v5::kStagger | v5::kDma | v5::kUnroll;
+        break;
+      case kPolV5StaggerPrio:
+        var = v5::kW8 | v5::kStagger | v5::kPrio | v5::kDma | v5::kUnroll;
+        break;
+      case kPolV5VKeep: var = v5::kW8 | v5::kVKeep | v5::kDma | v5::kUnroll; break;
+      case kPolV5VKeepPrio: var = v5::kW8 | v5::kVKeep | v5::kPrio | v5::kDma | v5::kUnroll; break;
+      case kPolV5Defer: case kPolV5Defer3: case kPolV5Defer4:
+        var = v5::kDefault;
+        ahead = pol - kPolV5Defer + 2;
+        break;
+      case kPolV5AsmDma: var = v5::kDefault | v5::kAsmDma; break;
+      case kPolDefault:
+        // d = 64, N % 64 == 0: v5 with 8 waves, LDS-DMA K/V staging, Vᵀ reuse and the
+        // exp-to-use distance (policy 56; A/B history in DESIGN.md §3, profiles/r1_ab_v5_*).
+        var = v5::kDefault;
+        break;
+      default: break;
+    }
+#ifdef MT_DIAGNOSTICS
+    if (pol >= 80 && pol <= 86) {  // wrong results: unrolled v5 minus one component
+      static const int kAbl[7] = {12, 28, 4, 68, 132, 260, 6};
+      var = kAbl[pol - 80];
+    }
+    if (pol == 97) var = 2;  // wrong results: no scale-and-shift
+    if (pol >= 91 && pol <= 96 && a.d == 64) {
+      *handled = true;
+      return launch_fwd_v4_ablation(a, pol - 90, st);
+    }
+#endif
+    if (var >= 0) e = launch_fwd_v5(a, false, ahead, var, st, handled);
+  }
+  if (!*handled && pol == kPolDefault && a.d == 64)
+    // causal, ragged N or short N: v4. Causal pairs a heavy and a light query block per
+    // workgroup, light block first (860 vs 806 TF/s unpaired at C3; 4 waves below
+    // N = 8192, 8 from there: profiles/r1_ab_causal_pair.txt, r1_ab_causal_lightfirst.txt).
+    e = launch_fwd_v4(a, causal, causal && N >= 8192 ? 8 : 4, !causal, st, handled,
+                      causal ? 2 : 0);
+  if (!*handled && a.d == 128) {
+    // d = 128: the pipelined frozen-reference kernel. Non-causal 8 waves; causal 8 waves
+    // with paired query blocks, light block first (profiles/r1_ab_d128_warm.txt,
+    // r1_ab_causal_pair.txt).
+    int nw = -1, pair = 0;
+    bool dma = false;
+    switch (pol) {
+      case kPolDefault: nw = 8; pair = causal ? 2 : 0; break;
+      case kPolD128w8: nw = 8; break;
+      case kPolD128w4: nw = 4; break;
+      case kPolD128Dma8: nw = 8; dma = true; break;
+      case kPolD128Dma4: nw = 4; dma = true; break;
+      case kPolD128Pair4: nw = 4; pair = 1; break;
+      case kPolD128Pair8: nw = 8; pair = 1; break;
+      case kPolV4PairLF4: nw = 4; pair = 2; break;
+      case kPolV4PairLF8: case kPolD128PairLF8: nw = 8; pair = 2; break;
+      default: break;
+    }
+    if (nw > 0) e = launch_fwd_d128(a, causal, nw, dma, st, handled, pair);
+  }
+  // any shape the kernels above decline: the single-phase kernel (d = 64 / 128), 8 waves
+  // by default (959 vs 802 TF/s for 4 waves at (1,16,16384,128))
+  if (!*handled) {
+    int var = 2;
+    if (pol >= kPolFast8 && pol <= kPolFastPp) var = pol;
+#ifdef MT_DIAGNOSTICS
+    if (pol >= 10 && pol <= 15) var = pol;
+#endif
+    e = launch_fwd_fast(a, causal, var, st, handled);
+  }
+  return e;
+}
+
 }  // namespace mt
 
 using namespace mt;
@@ -89,8 +269,14 @@ using namespace mt;
 extern "C" {
 
 const char* mt_last_error(void) { return g_err; }
-void mt_flash_set_kernel_policy(int policy) { g_kernel_policy = policy; }
-int mt_abi_version(void) { return 1; }
+int mt_flash_set_kernel_policy(int policy) {
+  if (!policy_valid(policy))
+    return set_error("mt_flash_set_kernel_policy: unknown policy %d", policy);
+  g_kernel_policy.store(policy, std::memory_order_relaxed);
+  return 0;
+}
+int mt_flash_get_kernel_policy(void) { return g_kernel_policy.load(std::memory_order_relaxed); }
+int mt_abi_version(void) { return 2; }
 
 int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const void* v,
                       void* o, float* m, float* l, int64_t B, int64_t H, int64_t N, int64_t d,
@@ -111,114 +297,11 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
   const int es = dtype == MT_BF16 ? 2 : 4;
   const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so}, {q, k, v, o});
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MT_BF16 && vec && g_kernel_policy != 1) {
+  const int pol = g_kernel_policy.load(std::memory_order_relaxed);
+  if (dtype == MT_BF16 && vec && pol != kPolGeneric) {
     bool handled = false;
-    hipError_t e = hipSuccess;
-    if (g_kernel_policy >= 7 && g_kernel_policy <= 9)
-      e = launch_fwd_v2(a, causal != 0, g_kernel_policy == 8 ? 8 : 4, g_kernel_policy == 9, st,
-                        &handled);
-    if (g_kernel_policy >= 16 && g_kernel_policy <= 20)
-      e = launch_fwd_v3(a, causal != 0, g_kernel_policy - 16, st, &handled);
-    if (g_kernel_policy >= 21 && g_kernel_policy <= 24)
-      e = launch_fwd_v4(a, causal != 0, (g_kernel_policy & 1) ? 4 : 8, g_kernel_policy >= 23, st,
-                        &handled);
-    // default at d = 64: v5 (two query blocks per wave) for non-causal N % 64 == 0, else
-    // 4-wave v4 (packed-f32 softmax arithmetic when non-causal, scalar when causal: the
-    // faster of each in the A/B, profiles/r1_ab_*)
-    if ((g_kernel_policy == 25 || g_kernel_policy == 26) && d == 64 &&
-        ((int64_t)N + 128) * std::max(a.sk[2], a.sv[2]) * 2 < ((int64_t)1 << 31)) {
-      e = launch_fwd_v4_deep(a, causal != 0, g_kernel_policy == 25, st);  // 4-wave, deep staging
-      handled = true;
-    }
-    if (g_kernel_policy >= 27 && g_kernel_policy <= 29)
-      e = launch_fwd_v5(a, causal != 0, 2 * (g_kernel_policy - 26), g_kernel_policy == 27 ? 4 : 0, st,
-                        &handled);
-    if (g_kernel_policy == 39 && !causal)  // 37 + static priority for the younger 4 waves
-      e = launch_fwd_v5(a, false, 2, 2048 + 1028 + 4096, st, &handled);
-    if (g_kernel_policy == 38 && !causal)  // 4 waves, register staging (the previous default)
-      e = launch_fwd_v5(a, false, 2, 4, st, &handled);
-    if (g_kernel_policy == 31)  // tile loop not unrolled (the pre-unroll default)
-      e = launch_fwd_v5(a, causal != 0, 2, 0, st, &handled);
-    if (g_kernel_policy == 35 && !causal)  // LDS-DMA staging
-      e = launch_fwd_v5(a, false, 2, 1028, st, &handled);
-    if ((g_kernel_policy == 36 || g_kernel_policy == 37) && !causal)  // 8 waves (37: + LDS-DMA)
-      e = launch_fwd_v5(a, false, 2, g_kernel_policy == 36 ? 2048 + 4 : 2048 + 1028, st, &handled);
-    if (g_kernel_policy == 50 || g_kernel_policy == 51)  // causal v4, heavy + light block pairs
-      e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 50 ? 4 : 8, !causal, st, &handled, true);
-    if (g_kernel_policy == 63 || g_kernel_policy == 64)  // 50 / 51 with the light block first
-      e = launch_fwd_v4(a, causal != 0, g_kernel_policy == 63 ? 4 : 8, !causal, st, &handled, 2);
-    if (g_kernel_policy == 61 && !causal)  // 56 with the LDS-DMA issued from inline asm
-      e = launch_fwd_v5(a, false, 2, 2048 + 623620, st, &handled);
-    if (g_kernel_policy >= 56 && g_kernel_policy <= 58 && !causal)  // 54 + exp-to-use distance
-      // of one MFMA slot (57 / 58: LDS operand reads 3 / 4 MFMAs ahead instead of 2)
-      e = launch_fwd_v5(a, false, g_kernel_policy - 54, 2048 + 99332, st, &handled);
-    if ((g_kernel_policy == 54 || g_kernel_policy == 55) && !causal)  // 37 (55: + priority) with
-      // the Vᵀ fragments of P2 kept in registers for P4 (half the V LDS reads)
-      e = launch_fwd_v5(a, false, 2, 2048 + (g_kernel_policy == 54 ? 33796 : 37892), st, &handled);
-    if (g_kernel_policy >= 46 && g_kernel_policy <= 49 && !causal) {
-      // 37 (+ static priority at 49) with: 46 single-issue f32 softmax VALU (no v_pk_*),
-      // 47 waves 4-7 staggered half a tile behind waves 0-3, 48 both
-      static const int kVar[4] = {9220, 17412, 25604, 21508};
-      e = launch_fwd_v5(a, false, 2, 2048 + kVar[g_kernel_policy - 46], st, &handled);
-    }
-    if (g_kernel_policy == 97)  // diagnostics only (wrong results): no scale-and-shift
-      e = launch_fwd_v5(a, causal != 0, 2, 2, st, &handled);
-    if (g_kernel_policy >= 80 && g_kernel_policy <= 86 && !causal) {
-      // diagnostics only (wrong results): unrolled v5 minus one component (fa_fwd_v5.hip)
-      static const int kAbl[7] = {12, 28, 4, 68, 132, 260, 6};  // 82 = the default (see v5)
-      e = launch_fwd_v5(a, false, 2, kAbl[g_kernel_policy - 80], st, &handled);
-    }
-    if (g_kernel_policy >= 91 && g_kernel_policy <= 96 && d == 64 && !causal) {
-      e = launch_fwd_v4_ablation(a, g_kernel_policy - 90, st);  // diagnostics only
-      handled = true;
-    }
-    if (g_kernel_policy == 0) {
-      // v5 for non-causal N % 64 == 0. Causal v5 (policies 27-31) is correct but slower
-      // than the 4-wave v4 (790 vs 811 TF/s at C3, 813 vs 836 at (1,16,16384,64)):
-      // 256-query workgroups balance the triangle worse and its diagonal tiles run serially.
-      // Non-causal default: 8 waves per workgroup with LDS-DMA K/V staging (policy 37:
-      // 993 vs 967 TF/s for the 4-wave register-staged form, profiles/r1_ab_v5_nw8.txt).
-      // Then (policy 56): the Vᵀ fragments of P2 kept in registers for P4 (+1.8 %,
-      // profiles/r1_ab_v5_vkeep.txt) and each pair's row-sum add / bf16 pack one MFMA slot
-      // after its exponentials (no trans-use s_nop; +2.2 % more, profiles/r1_ab_v5_defer.txt).
-      if (!causal) e = launch_fwd_v5(a, false, 2, 2048 + 99332, st, &handled);
-      // Causal: v4 with heavy + light query blocks paired per workgroup
-      // (profiles/r1_ab_causal_pair.txt): 4 waves (policy 50) below N = 8192 (860 vs 806
-      // TF/s unpaired at C3, 824 for 8 waves), 8 waves (policy 51) from there (934 vs 898
-      // for 4 waves at (1,16,16384,64)). The light block of each pair runs first
-      // (policies 63 / 64, profiles/r1_ab_causal_lightfirst.txt): same time (±1 %), and
-      // the heavy block finds the light block's K/V tiles still in L2, so HBM traffic at C3
-      // drops from 321 to 273 MB per launch (algorithmic 270 MB).
-      if (!handled)
-        e = launch_fwd_v4(a, causal != 0, causal && N >= 8192 ? 8 : 4, !causal, st, &handled,
-                          causal ? 2 : 0);
-    }
-    // d = 128: the pipelined frozen-reference kernel (fa_fwd_d128.hip). Default: 8 waves
-    // non-causal, 4 causal (warm-clock A/B, profiles/r1_ab_d128_warm.txt: non-causal 1085 vs
-    // 1001 TF/s at (8,16,4096,128), 1143 vs 1046 at (1,16,16384,128); causal 846 vs 819).
-    // 32 / 33 force 8 / 4 waves; 44 / 45 the same with LDS-DMA staging (neutral to -3 %).
-    if (!handled && (g_kernel_policy == 0 || (g_kernel_policy >= 32 && g_kernel_policy <= 33) ||
-                     (g_kernel_policy >= 44 && g_kernel_policy <= 45) || g_kernel_policy == 52 ||
-                     g_kernel_policy == 53 || (g_kernel_policy >= 63 && g_kernel_policy <= 65))) {
-      // 44 / 45: 8 / 4 waves with LDS-DMA staging; 52 / 53: causal heavy + light block
-      // pairs per workgroup, 4 / 8 waves
-      const int nw = (g_kernel_policy == 32 || g_kernel_policy == 44 || g_kernel_policy == 53) ? 8
-                     : (g_kernel_policy == 33 || g_kernel_policy == 45 || g_kernel_policy == 52 ||
-                        g_kernel_policy == 63) ? 4
-                     : 8;
-      // causal default: 8 waves with paired query blocks (policy 53: 944 vs 866 TF/s for
-      // unpaired 4 waves at (8,16,4096,128), 1101 vs 1020 at (1,16,16384,128))
-      e = launch_fwd_d128(a, causal != 0, nw, g_kernel_policy == 44 || g_kernel_policy == 45, st,
-                          &handled,
-                          g_kernel_policy >= 63 || (g_kernel_policy == 0 && causal) ? 2  // light first
-                          : g_kernel_policy >= 52                                    ? 1
-                                                                                     : 0);
-    }
-    // any shape the kernels above decline: the single-phase kernel, 8 waves by default
-    // (faster than 4 at d = 128: 959 vs 802 TF/s at (1,16,16384,128))
-    if (!handled)
-      e = launch_fwd_fast(a, causal != 0, g_kernel_policy == 0 ? 2 : g_kernel_policy, st, &handled);
-    if (handled) return check_hip(e, "mt_flash_attn_fwd(fast)");
+    const hipError_t e = fwd_bf16_dispatch(a, causal != 0, pol, st, &handled);
+    if (handled) return check_hip(e, "mt_flash_attn_fwd(bf16)");
   }
   return check_hip(launch_fwd_generic(a, dtype == MT_BF16, vec, causal != 0, st),
                    "mt_flash_attn_fwd");
@@ -251,19 +334,20 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
   const int es = dtype == MT_BF16 ? 2 : 4;
   const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv},
                           {q, k, v, o, dout, dq, dk, dv});
-  if (dtype == MT_BF16 && vec && g_kernel_policy != 1) {
+  const int pol = g_kernel_policy.load(std::memory_order_relaxed);
+  if (dtype == MT_BF16 && vec && pol != kPolGeneric) {
     bool handled = false;
-    // 40: software-pipelined dK/dV (A/B variant). An in-wave interleaved dQ tile was
-    // measured 1.7 % slower than the plain tile and removed (profiles/r1_ab_bwd_dq.txt).
-    // dK/dV variants: 0 32-query steps, 1 software-pipelined (policy 40), 2 64-query steps
-    // (policy 42). Default: 2 non-causal (1.912 vs 1.952 ms at C3), 0 causal (1.12 vs
-    // 1.31 ms: the masked diagonal steps spill in the 64-query form); policy 43 forces 0.
-    const int variant = g_kernel_policy == 40   ? 1
-                        : g_kernel_policy == 42 ? 2
-                        : g_kernel_policy == 62 ? 3  // 64-query steps, one wave per SIMD
-                        : g_kernel_policy == 66 ? 4  // 64-query steps, Q / dO by LDS-DMA
-                        : g_kernel_policy == 43 ? 0
-                                                : (causal ? 0 : 2);
+    // dK/dV forms: 0 32-query steps, 1 software-pipelined, 2 64-query steps, 3 64-query
+    // steps at one wave per SIMD, 4 64-query steps with LDS-DMA Q/dO. Default: 2
+    // non-causal (1.912 vs 1.952 ms at C3), 0 causal (1.12 vs 1.31 ms: the masked diagonal
+    // steps spill in the 64-query form). An in-wave interleaved dQ tile measured 1.7 %
+    // slower than the plain tile and was removed (profiles/r1_ab_bwd_dq.txt).
+    const int variant = pol == kPolBwdPipe        ? 1
+                        : pol == kPolBwdQ64        ? 2
+                        : pol == kPolBwdQ64OneWave ? 3
+                        : pol == kPolBwdQ64Dma     ? 4
+                        : pol == kPolBwdQ32        ? 0
+                                                   : (causal ? 0 : 2);
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }

@@ -1,4 +1,4 @@
-// Helpers shared by the bf16 MFMA forward kernels (fa_fwd_v2.hip, fa_fwd_v3.hip):
+// Helpers shared by the bf16 MFMA kernels (fa_fwd_v4/v5/d128.hip, fa_bwd_bf16.hip):
 // the XOR swizzles of the K / V LDS images and the wave's per-query row max.
 #pragma once
 #include "fa_common.h"

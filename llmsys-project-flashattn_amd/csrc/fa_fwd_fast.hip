@@ -85,6 +85,9 @@ __device__ __forceinline__ bf16x8 softmax_frag(const f32x16& s, int h, float c2,
 // 3 no PV MFMA, 4 no K/V staging, 5 no LDS operand reads.
 template <int D, bool CAUSAL, int NW, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_fast(AttnArgs p, int nqb) {
+#ifndef MT_DIAGNOSTICS
+  static_assert(ABL == 0, "ablation variants exist only in the MT_DIAGNOSTICS build");
+#endif
   constexpr int kThreads = 64 * NW;
   constexpr int kBQ = 32 * NW;
   constexpr int CPR = D / 8;                       // 16-B chunks per row
@@ -781,7 +784,8 @@ static hipError_t launch_fast_t(const AttnArgs& a, hipStream_t st) {
 
 // Variant map (mt_flash_set_kernel_policy): 0 = default = single-phase 4-wave kernel
 // (fastest measured: r01 A/B in profiles/), 2 = single-phase 8-wave, 3 = same as 0,
-// 4 / 5 = software-pipelined 8 / 4-wave, 6 = ping-pong 8-wave, 10..15 = ablation builds.
+// 4 / 5 = software-pipelined 8 / 4-wave, 6 = ping-pong 8-wave, 10..15 = ablation builds
+// (MT_DIAGNOSTICS only: wrong results, timing only).
 hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStream_t st,
                            bool* handled) {
   *handled = true;
@@ -802,6 +806,7 @@ hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStrea
     case 6: MT_DISPATCH(launch_pp_t)
     default: break;
   }
+#ifdef MT_DIAGNOSTICS
   if (variant >= 10 && variant <= 15 && d == 64 && !causal) {  // diagnostics
     switch (variant) {
       case 10: return launch_fast_t<64, false, 8, 0>(a, st);
@@ -812,6 +817,7 @@ hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStrea
       default: return launch_fast_t<64, false, 8, 5>(a, st);
     }
   }
+#endif
   MT_DISPATCH(launch_fast_t, 4)
 #undef MT_DISPATCH
 }

@@ -232,6 +232,9 @@ __device__ __forceinline__ void bulk4(const bf16* sk, const bf16* sv, const Ctx4
 // the XCD's L2 (heavy-first re-reads them after nqb - 1 - u other tiles have passed).
 template <bool CAUSAL, int NW, bool PK, int ABL = 0, bool DEEP = false, int PAIR = 0>
 __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_v4(AttnArgs p, int nqb) {
+#ifndef MT_DIAGNOSTICS
+  static_assert(ABL == 0, "ablation variants exist only in the MT_DIAGNOSTICS build");
+#endif
   using C = V4<NW>;
   constexpr int D = 64;
   static_assert(C::LPT == 1 || C::LPT == 2, "staging layout");
@@ -452,6 +455,7 @@ static hipError_t launch_v4_t(const AttnArgs& a, hipStream_t st) {
 
 // d = 64 only; every per-head K/V byte offset up to two tiles past N must fit the 31-bit
 // buffer offset (the bulk loop stages one tile ahead of the last one it needs).
+#ifdef MT_DIAGNOSTICS
 // Diagnostic ablations (wrong results by construction; timing only): d = 64, non-causal.
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st) {
   switch (abl) {
@@ -463,6 +467,7 @@ hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st) {
     default: return launch_v4_t<false, 4, true, 6>(a, st);
   }
 }
+#endif
 
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st) {
   if (pk) return causal ? launch_v4_t<true, 4, true, 0, true>(a, st) : launch_v4_t<false, 4, true, 0, true>(a, st);

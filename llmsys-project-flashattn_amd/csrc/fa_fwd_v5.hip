@@ -237,6 +237,10 @@ __device__ __forceinline__ float lane_pair_sum(float x) {
 // AHEAD: LDS operand reads are issued this many MFMAs ahead of their use. VAR: see sm_pair.
 template <int AHEAD, int VAR, bool CAUSAL, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
+#ifndef MT_DIAGNOSTICS
+  static_assert((VAR & (2 | 8 | 16 | 64 | 128 | 256)) == 0,
+                "wrong-result ablation variants exist only in the MT_DIAGNOSTICS build");
+#endif
   constexpr int LPT = lpt<NW>();
   constexpr int kBQ = 64 * NW;  // queries per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -599,16 +603,18 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
     kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;
   else if (var == 1028)
     kfn = fa_fwd_bf16_v5<2, 1028, false>;
-  else if (var >= 8)  // diagnostic ablations
+#ifdef MT_DIAGNOSTICS
+  else if (var >= 8 || var == 2)  // diagnostic ablations (wrong results, timing only)
     kfn = var == 12    ? fa_fwd_bf16_v5<2, 12, false>
           : var == 28  ? fa_fwd_bf16_v5<2, 28, false>
           : var == 68  ? fa_fwd_bf16_v5<2, 68, false>
           : var == 132 ? fa_fwd_bf16_v5<2, 132, false>
           : var == 260 ? fa_fwd_bf16_v5<2, 260, false>
+          : var == 2   ? fa_fwd_bf16_v5<2, 2, false>
                        : fa_fwd_bf16_v5<2, 6, false>;
+#endif
   else
     kfn = var == 4   ? fa_fwd_bf16_v5<2, 4, false>
-          : var == 2 ? fa_fwd_bf16_v5<2, 2, false>
           : ahead >= 6 ? fa_fwd_bf16_v5<6, 0, false>
           : ahead >= 4 ? fa_fwd_bf16_v5<4, 0, false>
                        : fa_fwd_bf16_v5<2, 0, false>;

@@ -33,7 +33,8 @@ _ip = ctypes.POINTER(ctypes.c_int)
 _PROTOS = {
     "mt_last_error": (ctypes.c_char_p, []),
     "mt_abi_version": (_int, []),
-    "mt_flash_set_kernel_policy": (None, [_int]),
+    "mt_flash_set_kernel_policy": (_int, [_int]),
+    "mt_flash_get_kernel_policy": (_int, []),
     "mt_flash_attn_fwd": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,
                                  _i64p, _i64p, _i64p, _i64p, _vp]),
     "mt_flash_attn_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
@@ -83,6 +84,40 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         _lib = l
     return _lib
+
+
+def use_library(path: str) -> ctypes.CDLL:
+    """Load a different build of the library (diagnostics only: scripts/ablate*.py load
+    ``_lib/diag/libminitorch_hip_diag.so``, built by ``make DIAG=1``). The package itself
+    always loads LIB_PATH."""
+    global _lib, LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("use_library() must run before the first lib() call")
+    LIB_PATH = path
+    return lib()
+
+
+def set_policy(policy: int) -> None:
+    """Select a kernel policy for A/B timing (mt_flash_set_kernel_policy; raises for an
+    id the library rejects)."""
+    check(lib().mt_flash_set_kernel_policy(int(policy)), "mt_flash_set_kernel_policy")
+
+
+class policy:
+    """``with _hip.policy(p): ...`` runs the block under kernel policy p, then restores
+    the previous one."""
+
+    def __init__(self, p: int):
+        self.p = int(p)
+
+    def __enter__(self):
+        self.prev = lib().mt_flash_get_kernel_policy()
+        set_policy(self.p)
+        return self
+
+    def __exit__(self, *exc):
+        set_policy(self.prev)
+        return False
 
 
 def register(name: str, restype, argtypes) -> None:

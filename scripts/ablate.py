@@ -3,6 +3,10 @@ import os, sys, json
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "llmsys-project-flashattn_amd"))
 import torch
 from minitorch import _hip
+# diagnostics build (make DIAG=1): the product library rejects the ablation policies
+_DIAG = os.path.join(os.path.dirname(_hip.LIB_PATH), "diag", "libminitorch_hip_diag.so")
+if os.path.exists(_DIAG):
+    _hip.use_library(_DIAG)
 pols = [int(x) for x in sys.argv[1].split(",")]
 causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
 B, H, N, d = 8, 16, 4096, 64
@@ -13,7 +17,7 @@ res = {p: [] for p in pols}
 flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
 for rnd in range(5):
     for p in pols:
-        _hip.lib().mt_flash_set_kernel_policy(p)
+        _hip.set_policy(p)
         for _ in range(3): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize(); e0.record()

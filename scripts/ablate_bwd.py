@@ -4,6 +4,10 @@ import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "llmsys-project-flashattn_amd"))
 import torch
 from minitorch import _hip
+# diagnostics build (make DIAG=1): the product library rejects the ablation policies
+_DIAG = os.path.join(os.path.dirname(_hip.LIB_PATH), "diag", "libminitorch_hip_diag.so")
+if os.path.exists(_DIAG):
+    _hip.use_library(_DIAG)
 pols = [int(x) for x in sys.argv[1].split(",")]
 causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
 B, H, N, d = 8, 16, 4096, 64
@@ -16,7 +20,7 @@ flops = 2.5 * 4.0 * B * H * N * N * d / (2 if causal else 1)
 res = {p: [] for p in pols}
 for rnd in range(5):
     for p in pols:
-        _hip.lib().mt_flash_set_kernel_policy(p)
+        _hip.set_policy(p)
         for _ in range(2):
             _hip.flash_bwd(q, k, v, o, do, m, l, causal, dq=dq, dk=dk, dv=dv, workspace=ws)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -25,7 +29,7 @@ for rnd in range(5):
             _hip.flash_bwd(q, k, v, o, do, m, l, causal, dq=dq, dk=dk, dv=dv, workspace=ws)
         e1.record(); torch.cuda.synchronize()
         res[p].append(e0.elapsed_time(e1) / 5)
-_hip.lib().mt_flash_set_kernel_policy(0)
+_hip.set_policy(0)
 for p in pols:
     t = sorted(res[p]); med = t[len(t) // 2]
     print(f"bwd policy {p:3d}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s (FA-2 convention)")

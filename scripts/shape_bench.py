@@ -13,13 +13,13 @@ o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.em
 flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
 # untimed clock ramp (~0.3 s of kernels) so the first policy is not measured on a cold GPU
 import time
-_hip.lib().mt_flash_set_kernel_policy(pols[0])
+_hip.set_policy(pols[0])
 t_ramp = time.perf_counter()
 while time.perf_counter() - t_ramp < 0.3:
     _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
     torch.cuda.synchronize()
 for p in pols:
-    _hip.lib().mt_flash_set_kernel_policy(p)
+    _hip.set_policy(p)
     for _ in range(2): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(); e0.record()
@@ -28,4 +28,4 @@ for p in pols:
     e1.record(); torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     print(f"({B},{H},{N},{d}) causal={causal} policy {p}: {ms:.3f} ms  {flops / ms / 1e9:.1f} TF/s")
-_hip.lib().mt_flash_set_kernel_policy(0)
+_hip.set_policy(0)

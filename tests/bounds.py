@@ -1,0 +1,46 @@
+"""Elementwise error bounds for the bf16 kernels against the fp32 oracle (test
+infrastructure). A bf16 MFMA kernel rounds its MFMA operands that are computed in the
+kernel (P before PV and dVᵀ, dS before dKᵀ and dQ) and its outputs to 8 significant
+bits, each a relative error of at most 2^-9; everything else accumulates in fp32. So,
+elementwise, with |·| taken before the products:
+
+    |O  - O_ref|  <= atol + r · (P |V|)                    (causal rows average few keys)
+    |dV - dV_ref| <= atol + r · (Pᵀ |dO|)
+    |dK - dK_ref| <= atol + r · (1/√d) · (|dS|ᵀ |Q|)
+    |dQ - dQ_ref| <= atol + r · (1/√d) · (|dS| |K|)
+
+where |dS| = P ∘ (|dP − δ| + Δδ) and Δδ = 2^-8 · rowsum(|dO| ∘ |O|) covers δ = rowsum(dO ∘ O)
+being formed from the bf16-rounded O. r = 2^-7 is twice the two roundings (operand +
+output) each product sees. The products are formed in fp64 from the same bf16-rounded
+inputs the kernels read.
+"""
+import numpy as np
+
+R_BF16 = 2.0 ** -7
+
+
+def head_terms(q, k, v, do, causal):
+    """fp64 P, |dS| pieces for one head (N, d)."""
+    q, k, v, do = (np.asarray(a, np.float64) for a in (q, k, v, do))
+    N, d = q.shape
+    sc = 1.0 / np.sqrt(d)
+    S = (q @ k.T) * sc
+    if causal:
+        S[np.triu_indices(N, 1)] = -np.inf
+    S -= S.max(axis=1, keepdims=True)
+    P = np.exp(S)
+    P /= P.sum(axis=1, keepdims=True)
+    O = P @ v
+    dP = do @ v.T
+    delta = (do * O).sum(axis=1, keepdims=True)
+    ddelta = 2.0 ** -8 * (np.abs(do) * np.abs(O)).sum(axis=1, keepdims=True)
+    absdS = P * (np.abs(dP - delta) + ddelta)
+    return P, absdS, sc
+
+
+def grad_bounds(q, k, v, do, causal, atol=1e-3, r=R_BF16):
+    P, absdS, sc = head_terms(q, k, v, do, causal)
+    q, k, do = (np.abs(np.asarray(a, np.float64)) for a in (q, k, do))
+    return (atol + r * sc * (absdS @ k),      # dQ
+            atol + r * sc * (absdS.T @ q),    # dK
+            atol + r * (P.T @ do))            # dV

@@ -53,3 +53,32 @@ def test_errors_are_reported_not_fatal():
                                None, None, None, None, None)
     assert rc != 0
     assert b"dtype" in lib.mt_last_error()
+
+
+def test_kernel_policy_switch_rejects_unknown_ids():
+    """Only policies that compute the default's attention are selectable: the timing-only
+    ablations (wrong results by construction) are not in the product library, and unknown
+    ids leave the policy unchanged with a status."""
+    from minitorch import _hip
+    lib = _hip.lib()
+    assert lib.mt_flash_get_kernel_policy() == 0
+    for bad in (-1, 7, 16, 80, 86, 91, 96, 97, 10, 15, 1000):
+        assert lib.mt_flash_set_kernel_policy(bad) != 0, bad
+        assert b"unknown policy" in lib.mt_last_error()
+        assert lib.mt_flash_get_kernel_policy() == 0
+    with _hip.policy(56):
+        assert lib.mt_flash_get_kernel_policy() == 56
+    assert lib.mt_flash_get_kernel_policy() == 0
+    with pytest.raises(RuntimeError):
+        _hip.set_policy(97)
+
+
+def test_product_library_has_no_ablation_kernels():
+    """The product .so carries no instantiation of the wrong-result ablation templates."""
+    from minitorch import _hip
+    import subprocess
+    if not os.path.exists(_hip.LIB_PATH):
+        pytest.skip("library not built")
+    syms = subprocess.run(["nm", "-C", "-D", "--defined-only", _hip.LIB_PATH], capture_output=True,
+                          text=True).stdout
+    assert "launch_fwd_v4_ablation" not in syms
