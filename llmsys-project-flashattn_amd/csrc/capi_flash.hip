@@ -68,9 +68,11 @@ enum : int {
   kPolV5AsmDma = 61,
   // fa_fwd_d128.hip: 32 / 33 8 / 4 waves, 44 / 45 the same with LDS-DMA staging
   kPolD128w8 = 32, kPolD128w4 = 33, kPolD128Dma8 = 44, kPolD128Dma4 = 45,
-  // fa_bwd_bf16.hip dK/dV forms: 40 software-pipelined, 42 64-query steps, 43 32-query
-  // steps, 62 64-query steps at one wave per SIMD, 66 64-query steps with LDS-DMA Q/dO
-  kPolBwdPipe = 40, kPolBwdQ64 = 42, kPolBwdQ32 = 43, kPolBwdQ64OneWave = 62,
+  // fa_bwd_bf16.hip dK/dV forms: 40 software-pipelined, 43 32-query steps, 62 64-query
+  // steps at one wave per SIMD, 66 64-query steps with LDS-DMA Q/dO (the non-causal
+  // default). (42, the register-staged 64-query form at two waves per SIMD, was removed: its
+  // spilling build computed a wrong dK whenever N / 64 was odd.)
+  kPolBwdPipe = 40, kPolBwdQ32 = 43, kPolBwdQ64OneWave = 62,
   kPolBwdQ64Dma = 66,
 };
 static const int kValidPolicies[] = {
@@ -81,7 +83,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ64, kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -343,11 +345,10 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
     // steps spill in the 64-query form). An in-wave interleaved dQ tile measured 1.7 %
     // slower than the plain tile and was removed (profiles/r1_ab_bwd_dq.txt).
     const int variant = pol == kPolBwdPipe        ? 1
-                        : pol == kPolBwdQ64        ? 2
                         : pol == kPolBwdQ64OneWave ? 3
                         : pol == kPolBwdQ64Dma     ? 4
                         : pol == kPolBwdQ32        ? 0
-                                                   : (causal ? 0 : 2);
+                                                   : (causal ? 0 : 4);
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }
@@ -363,6 +364,11 @@ struct DevBuf {
 
 static int host_fwd(float* Q, float* K, float* V, float* O, float* l, float* m, int B, int nh,
                     int N, int d, int causal, const char* name) {
+  if (check_sizes(MT_F32, B, nh, N, d) || ((!Q || !K || !V || !O || !l || !m) &&
+                                           set_error("%s: null host pointer", name))) {
+    fprintf(stderr, "%s failed: %s\n", name, g_err);
+    return 1;
+  }
   const size_t n = (size_t)B * nh * N * d, r = (size_t)B * nh * N;
   DevBuf dq, dk, dv, dof, dm, dl;
   if (check_hip(hipMalloc(&dq.p, n * 4), name) || check_hip(hipMalloc(&dk.p, n * 4), name) ||
@@ -390,6 +396,12 @@ fail:
 static int host_bwd(float* Q, float* K, float* V, float* O, float* dQ, float* dK, float* dV,
                     float* dO, float* l, float* m, int B, int nh, int N, int d, int causal,
                     const char* name) {
+  if (check_sizes(MT_F32, B, nh, N, d) ||
+      ((!Q || !K || !V || !O || !dQ || !dK || !dV || !dO || !l || !m) &&
+       set_error("%s: null host pointer", name))) {
+    fprintf(stderr, "%s failed: %s\n", name, g_err);
+    return 1;
+  }
   const size_t n = (size_t)B * nh * N * d, r = (size_t)B * nh * N;
   DevBuf bufs[11];
   float* hin[5] = {Q, K, V, O, dO};

@@ -409,6 +409,9 @@ struct HostTensor {
   int64_t shape[mt::kMaxDims], strides[mt::kMaxDims];
   ~HostTensor() { if (dev) (void)hipFree(dev); }
   int up(const float* h, const int* shp, const int* str, int dims, const char* w) {
+    if (dims < 1 || dims > mt::kMaxDims)
+      return mt::set_error("%s: tensor rank %d outside 1..%d", w, dims, mt::kMaxDims);
+    if (!shp || !str) return mt::set_error("%s: null shape/stride pointer", w);
     for (int d = 0; d < dims; ++d) { shape[d] = shp[d]; strides[d] = str[d]; }
     const size_t n = (size_t)extent(shp, str, dims) * sizeof(float);
     if (mt::check_hip(hipMalloc(&dev, n), w)) return 1;

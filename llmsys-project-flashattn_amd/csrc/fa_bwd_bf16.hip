@@ -926,7 +926,6 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
     const size_t smem = (variant == 1 ? 3 : variant >= 2 ? 4 : 2) * (size_t)kBufQ;
     auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
-               : variant == 2 ? fa_bwd_dkv_bf16_q64<CAUSAL>
                : variant == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
                : variant == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
                               : fa_bwd_dkv_bf16<CAUSAL>;

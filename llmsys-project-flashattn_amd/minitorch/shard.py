@@ -28,10 +28,43 @@ def bh_range(bh: int, world: int, rank: int) -> Tuple[int, int]:
 
 def shard(t, world: int, rank: int):
     """View of this rank's rows of a [B,H,N,d] (or [B,H,N]) tensor, flattened to
-    [rows, N(, d)]. ``t`` must be contiguous over (B, H)."""
+    [rows, N(, d)]. ``t`` must be viewable as [B*H, ...] (contiguous over (B, H) with the
+    trailing strides kept): a permuted projection view such as the MHA's [B,N,H,dh]
+    storage would otherwise be silently copied whole on every rank, so it is refused."""
     B, H = t.shape[:2]
     lo, hi = bh_range(B * H, world, rank)
-    return t.reshape((B * H,) + tuple(t.shape[2:]))[lo:hi]
+    try:
+        flat = t.view((B * H,) + tuple(t.shape[2:]))
+    except RuntimeError as e:
+        raise ValueError(
+            f"shard(): tensor of shape {tuple(t.shape)} and strides {tuple(t.stride())} is not "
+            "contiguous over (B, H); call .contiguous() once before sharding") from e
+    return flat[lo:hi]
+
+
+def _local_or_shard(t, global_ndim: int, world: int, rank: int, rows: int):
+    """``t`` as this rank's [rows, ...] block: a global tensor (``global_ndim`` dims) is
+    sharded; a rank-local one (one dim fewer, as ``sharded_flash_fwd(gather=False)``
+    returns) is taken as it is after a row-count check."""
+    if t.dim() == global_ndim:
+        return shard(t, world, rank)
+    if t.dim() == global_ndim - 1:
+        if t.shape[0] != rows:
+            raise ValueError(f"rank-local tensor has {t.shape[0]} rows, this rank owns {rows}")
+        return t
+    raise ValueError(f"expected a {global_ndim}-d global or {global_ndim - 1}-d rank-local tensor, "
+                     f"got shape {tuple(t.shape)}")
+
+
+def _world_rank(group, world: Optional[int], rank: Optional[int]) -> Tuple[int, int]:
+    import torch.distributed as dist
+    if world is not None or rank is not None:
+        if world is None or rank is None:
+            raise ValueError("give both world and rank, or neither")
+        return world, rank
+    if dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
 
 
 def _hip_fwd(q, k, v, causal):
@@ -61,38 +94,67 @@ def _gather(local, world: int, group, bh: int, rank_sizes: Sequence[int]):
 
 
 def sharded_flash_fwd(q, k, v, causal: bool = False, group=None, gather: bool = True,
-                      attn: Optional[Callable] = None):
+                      attn: Optional[Callable] = None, world: Optional[int] = None,
+                      rank: Optional[int] = None):
     """Forward over this rank's B*H shard of the global [B,H,N,d] Q/K/V.
 
     Returns ``(O, m, l)``: with ``gather`` the full [B,H,N,d] / [B,H,N] results on every
-    rank (one all-gather per output), otherwise this rank's shard [rows,N,d] / [rows,N]."""
-    import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    rank (one all-gather per output), otherwise this rank's shard [rows,N,d] / [rows,N]
+    (at world size 1, the full tensors in their global shape).
+
+    ``world``/``rank`` default to the process group's; giving them explicitly computes that
+    rank's shard without any collective (``gather=False`` only) — a single process can then
+    produce every rank's rows of a ragged split."""
+    world, rank = _world_rank(group, world, rank)
+    if gather and world > 1 and not (dist_ready() and world == _group_world(group)):
+        raise ValueError("gather=True needs an initialised process group of that world size")
     B, H, N, d = q.shape
     fn = attn or _hip_fwd
     qs, ks, vs = (shard(t, world, rank) for t in (q, k, v))
     o, m, l = fn(qs[None], ks[None], vs[None], causal)
     o, m, l = o[0], m[0], l[0]
-    if not gather or world == 1:
-        return (o.reshape(B, H, N, d), m.reshape(B, H, N), l.reshape(B, H, N)) if world == 1 else (o, m, l)
+    if world == 1:
+        return o.reshape(B, H, N, d), m.reshape(B, H, N), l.reshape(B, H, N)
+    if not gather:
+        return o, m, l
     sizes = [bh_range(B * H, world, r)[1] - bh_range(B * H, world, r)[0] for r in range(world)]
     outs = [_gather(t, world, group, B * H, sizes) for t in (o, m, l)]
     return outs[0].reshape(B, H, N, d), outs[1].reshape(B, H, N), outs[2].reshape(B, H, N)
 
 
 def sharded_flash_bwd(q, k, v, o, do, m, l, causal: bool = False, group=None, gather: bool = True,
-                      attn_bwd: Optional[Callable] = None):
-    """Backward over this rank's B*H shard; every input is the global tensor (or any tensor
-    whose shard view is this rank's rows). Returns (dQ, dK, dV), gathered if asked."""
-    import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+                      attn_bwd: Optional[Callable] = None, world: Optional[int] = None,
+                      rank: Optional[int] = None):
+    """Backward over this rank's B*H shard. q, k, v and do are the global [B,H,N,d]
+    tensors; o, m and l are either global ([B,H,N,d] / [B,H,N]) or this rank's rows
+    ([rows,N,d] / [rows,N], the ``gather=False`` forward's output), so a training step
+    that never gathers O feeds its forward straight into the backward. Returns
+    (dQ, dK, dV): gathered [B,H,N,d] with ``gather``, else this rank's [rows,N,d]
+    (at world size 1, the global shape). ``world``/``rank``: as in sharded_flash_fwd."""
+    world, rank = _world_rank(group, world, rank)
+    if gather and world > 1 and not (dist_ready() and world == _group_world(group)):
+        raise ValueError("gather=True needs an initialised process group of that world size")
     B, H, N, d = q.shape
+    lo, hi = bh_range(B * H, world, rank)
     fn = attn_bwd or _hip_bwd
-    args = [shard(t, world, rank)[None] for t in (q, k, v, o, do, m, l)]
-    grads = [g[0] for g in fn(*args, causal)]
-    if not gather or world == 1:
-        return tuple(g.reshape(B, H, N, d) for g in grads) if world == 1 else tuple(grads)
+    args = [shard(t, world, rank) for t in (q, k, v)]
+    args.append(_local_or_shard(o, 4, world, rank, hi - lo))
+    args.append(shard(do, world, rank))
+    args += [_local_or_shard(t, 3, world, rank, hi - lo) for t in (m, l)]
+    grads = [g[0] for g in fn(*(a[None] for a in args), causal)]
+    if world == 1:
+        return tuple(g.reshape(B, H, N, d) for g in grads)
+    if not gather:
+        return tuple(grads)
     sizes = [bh_range(B * H, world, r)[1] - bh_range(B * H, world, r)[0] for r in range(world)]
     return tuple(_gather(g, world, group, B * H, sizes).reshape(B, H, N, d) for g in grads)
+
+
+def dist_ready() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+def _group_world(group) -> int:
+    import torch.distributed as dist
+    return dist.get_world_size(group)

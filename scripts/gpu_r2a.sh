@@ -1,7 +1,7 @@
 # Round-2a: first GPU check of the re-entry tree: gpu tests (with the parity record),
 # smoke, a kernel-trace profile of the bench, the default bench line.
 set -o pipefail
-TAG=${1:-r2a}
+TAG=${1:-r2c}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 export MT_PARITY_OUT=gpurun_out/parity_$TAG.json

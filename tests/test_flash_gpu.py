@@ -396,7 +396,7 @@ def test_spiked_rescale(torch_dev, policy, d):
         _hip.set_policy(0)
 
 
-@pytest.mark.parametrize("policy", (0, 40, 42, 43, 62, 66))
+@pytest.mark.parametrize("policy", (0, 40, 43, 62, 66))
 @pytest.mark.parametrize("causal", [False, True])
 def test_bf16_bwd_policies_vs_oracle(torch_dev, policy, causal):
     """bf16 d=64 backward variants (0 default, 40 software-pipelined dK/dV) against the
@@ -406,7 +406,8 @@ def test_bf16_bwd_policies_vs_oracle(torch_dev, policy, causal):
     rng = np.random.default_rng(41)
     try:
         _hip.set_policy(policy)
-        for (B, H, N) in ((1, 2, 512), (1, 1, 777), (2, 1, 200)):
+        # N / 64 odd (64, 192) pins the case the removed policy 42 got wrong
+        for (B, H, N) in ((1, 2, 512), (1, 1, 777), (2, 1, 200), (1, 1, 64), (2, 3, 192)):
             q, k, v, do = (A.bf16_round(rng.standard_normal((B, H, N, 64)).astype(np.float32))
                            for _ in range(4))
             tq, tk, tv, tdo = (_dev(torch, x, torch.bfloat16) for x in (q, k, v, do))

@@ -294,3 +294,54 @@ def test_decoder_lm_training_step(mt):
         losses.append(loss.item())
     assert np.isfinite(losses).all()
     assert losses[-1] < losses[0], losses
+
+
+def _fixtures(kind):
+    import glob
+    import os
+    paths = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", f"{kind}_*.npz")))
+    assert paths
+    return [(os.path.basename(p), dict(np.load(p))) for p in paths]
+
+
+def test_attn_softmax_vs_reference_fixtures(mt, parity_record):
+    """The fused HIP softmax against the reference's own minitorch compositions
+    (tests/golden/softmax_*.npz from oracle/gen_companion_golden.py; reference
+    kernel_tests/test_softmax_fw.py:14 atol = rtol = 1e-3, test_softmax_bw.py:14
+    atol 1e-2 / rtol 1e-3): fw with the [B,1,1,to] padding mask, bw through autodiff."""
+    minitorch, B = mt
+    for name, f in _fixtures("softmax"):
+        x = minitorch.tensor_from_numpy(f["inp"], B, True)
+        mask = minitorch.tensor_from_numpy(f["mask_bt"][:, None, None, :].copy(), B)
+        y = x.attn_softmax(mask).to_numpy()
+        np.testing.assert_allclose(y, f["fw"], atol=1e-3, rtol=1e-3)
+        x2 = minitorch.tensor_from_numpy(f["inp"], B, True)
+        zero = minitorch.tensor_from_numpy(np.zeros((f["inp"].shape[0], 1, 1, f["inp"].shape[3]),
+                                                    np.float32), B)
+        x2.attn_softmax(zero).backward(minitorch.tensor_from_numpy(f["dout"], B))
+        g = x2.grad.to_numpy()
+        np.testing.assert_allclose(g, f["bw"], atol=1e-2, rtol=1e-3)
+        parity_record("test_attn_softmax_vs_reference_fixtures", name,
+                      max_abs_fw=float(np.abs(y - f["fw"]).max()),
+                      max_abs_bw=float(np.abs(g - f["bw"]).max()), bound="fw 1e-3, bw 1e-2")
+
+
+def test_layernorm_vs_reference_fixtures(mt, parity_record):
+    """The fused HIP LayerNorm against the reference's compositions (tests/golden/
+    layernorm_*.npz; reference kernel_tests/test_layernorm_fw.py:20 atol 1e-2 / rtol 1e-3,
+    test_layernorm_bw.py:20 atol 1e-3 / rtol 1e-2)."""
+    minitorch, B = mt
+    for name, f in _fixtures("layernorm"):
+        x = minitorch.tensor_from_numpy(f["x"], B, True)
+        g = minitorch.tensor_from_numpy(f["gamma"], B, True)
+        b = minitorch.tensor_from_numpy(f["beta"], B, True)
+        y = x.layernorm(g, b)
+        yn = y.to_numpy()
+        np.testing.assert_allclose(yn, f["fw"], atol=1e-2, rtol=1e-3)
+        y.backward(minitorch.tensor_from_numpy(f["dout"], B))
+        got = (g.grad.to_numpy().reshape(-1), b.grad.to_numpy().reshape(-1), x.grad.to_numpy())
+        for gv, want in zip(got, (f["dgamma"], f["dbeta"], f["dinp"])):
+            np.testing.assert_allclose(gv, want, atol=1e-3, rtol=1e-2)
+        parity_record("test_layernorm_vs_reference_fixtures", name,
+                      max_abs_fw=float(np.abs(yn - f["fw"]).max()),
+                      max_abs_dinp=float(np.abs(got[2] - f["dinp"]).max()), bound="fw 1e-2, bw 1e-3")

@@ -58,3 +58,41 @@ def test_bf16_rounding():
     assert r[0] == 1.0 and r[1] == 1.0  # tie to even
     assert np.all(np.abs(r - x) <= np.abs(x) * 2 ** -8)
     np.testing.assert_array_equal(A.bf16_from_bits(A.bf16_bits(x)), r)
+
+
+# ---- companion-kernel fixtures (oracle/gen_companion_golden.py: the reference's own
+# minitorch compositions from its kernel_tests) -------------------------------------------
+def _companion(golden_dir, kind):
+    import glob
+    paths = sorted(glob.glob(os.path.join(golden_dir, f"{kind}_*.npz")))
+    assert paths, f"no {kind} fixtures"
+    return [dict(np.load(p)) for p in paths]
+
+
+def test_softmax_fixtures_match_formula(golden_dir):
+    """The reference composition equals the kernel contract (softmax_kernel.cu: exp(x - max)
+    over (Σ + 1e-8), mask [B,to] added per row; bw y∘(dy − Σ dy∘y)) in NumPy f64."""
+    for f in _companion(golden_dir, "softmax"):
+        x = f["inp"].astype(np.float64)
+        z = x + f["mask_bt"][:, None, None, :]
+        e = np.exp(z - z.max(-1, keepdims=True))
+        np.testing.assert_allclose(f["fw"], e / (e.sum(-1, keepdims=True) + 1e-8), atol=1e-6)
+        e0 = np.exp(x - x.max(-1, keepdims=True))
+        y = e0 / e0.sum(-1, keepdims=True)
+        dy = f["dout"].astype(np.float64)
+        np.testing.assert_allclose(f["bw"], y * (dy - (dy * y).sum(-1, keepdims=True)), atol=1e-6)
+
+
+def test_layernorm_fixtures_match_formula(golden_dir):
+    for f in _companion(golden_dir, "layernorm"):
+        x = f["x"].astype(np.float64)
+        mu, var = x.mean(-1, keepdims=True), x.var(-1, keepdims=True)
+        xh = (x - mu) / np.sqrt(var + 1e-8)
+        np.testing.assert_allclose(f["fw"], f["gamma"] * xh + f["beta"], atol=1e-5)
+        np.testing.assert_allclose(f["var"], var[:, 0], atol=1e-6)
+        dy = f["dout"].astype(np.float64)
+        dyg = dy * f["gamma"]
+        dx = (dyg - dyg.mean(-1, keepdims=True) - xh * (dyg * xh).mean(-1, keepdims=True)) / np.sqrt(var)
+        np.testing.assert_allclose(f["dinp"], dx, atol=1e-4)
+        np.testing.assert_allclose(f["dgamma"], (dy * xh).sum(0), atol=1e-4)
+        np.testing.assert_allclose(f["dbeta"], dy.sum(0), atol=1e-4)

@@ -26,6 +26,38 @@ def test_bh_range_partition():
     assert s.shape == (3, 4, 5) and s.data_ptr() == t.reshape(6, 4, 5)[3].data_ptr()
 
 
+def test_shard_refuses_permuted_view():
+    t = torch.zeros(2, 5, 3, 4).permute(0, 2, 1, 3)  # [B,H,N,d] view of [B,N,H,d] storage
+    with pytest.raises(ValueError, match="not contiguous over"):
+        shard(t, 2, 0)
+
+
+def test_explicit_rank_ragged_no_collective():
+    """One process computes every rank's rows of a ragged 3-way split (B*H = 4) with
+    explicit world/rank, feeds each rank-local forward into the backward, and the pieces
+    concatenate to the unsharded oracle result."""
+    from minitorch.shard import sharded_flash_bwd, sharded_flash_fwd
+    g = torch.Generator().manual_seed(3)
+    shape = (2, 2, 40, 8)
+    q, k, v, do = (torch.randn(shape, generator=g) for _ in range(4))
+    flat = lambda t: t.reshape(-1, *t.shape[2:])
+    ro, rm, rl = _oracle_fwd(flat(q), flat(k), flat(v), True)
+    rg = _oracle_bwd(flat(q), flat(k), flat(v), ro, flat(do), rm, rl, True)
+    outs, grads = [], []
+    for r in range(3):
+        o, m, l = sharded_flash_fwd(q, k, v, True, gather=False, attn=_oracle_fwd, world=3, rank=r)
+        outs.append(o)
+        grads.append(sharded_flash_bwd(q, k, v, o, do, m, l, True, gather=False,
+                                       attn_bwd=_oracle_bwd, world=3, rank=r))
+    assert [o.shape[0] for o in outs] == [2, 1, 1]
+    np.testing.assert_allclose(torch.cat(outs).numpy(), ro.numpy(), atol=1e-6)
+    for i in range(3):
+        np.testing.assert_allclose(torch.cat([gr[i] for gr in grads]).numpy(), rg[i].numpy(), atol=1e-5)
+    with pytest.raises(ValueError, match="rows"):
+        sharded_flash_bwd(q, k, v, outs[0], do, m, l, True, gather=False, attn_bwd=_oracle_bwd,
+                          world=3, rank=2)
+
+
 def _oracle_fwd(q, k, v, causal):
     from oracle import attention as A
     o, m, l = A.attention_fwd(q.numpy(), k.numpy(), v.numpy(), causal)
@@ -64,6 +96,11 @@ def _worker(rank, world, port, shape, causal, errq):
         os_, _, _ = sharded_flash_fwd(q, k, v, causal, gather=False, attn=_oracle_fwd)
         lo, hi = bh_range(shape[0] * shape[1], world, rank)
         np.testing.assert_allclose(os_.numpy(), ro[lo:hi].numpy(), atol=1e-6)
+        # the no-gather training path: rank-local O/m/l straight into the backward
+        os_, ms_, ls_ = sharded_flash_fwd(q, k, v, causal, gather=False, attn=_oracle_fwd)
+        lg = sharded_flash_bwd(q, k, v, os_, do, ms_, ls_, causal, gather=False, attn_bwd=_oracle_bwd)
+        for got, want in zip(lg, ref):
+            np.testing.assert_allclose(got.numpy(), want[lo:hi].numpy(), atol=1e-5)
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # surfaced to the parent
