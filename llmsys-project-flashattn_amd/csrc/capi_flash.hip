@@ -66,6 +66,8 @@ enum : int {
   kPolV5Stagger = 47, kPolV5ScalarStagger = 48, kPolV5StaggerPrio = 49, kPolV5VKeep = 54,
   kPolV5VKeepPrio = 55, kPolV5Defer = 56, kPolV5Defer3 = 57, kPolV5Defer4 = 58,
   kPolV5AsmDma = 61,
+  // v5 causal: paired query blocks, pipelined per-wave diagonal, 8 / 4 waves
+  kPolV5Causal8 = 67, kPolV5Causal4 = 68,
   // fa_fwd_d128.hip: 32 / 33 8 / 4 waves, 44 / 45 the same with LDS-DMA staging
   kPolD128w8 = 32, kPolD128w4 = 33, kPolD128Dma8 = 44, kPolD128Dma4 = 45,
   // fa_bwd_bf16.hip dK/dV forms: 40 software-pipelined, 43 32-query steps, 62 64-query
@@ -83,7 +85,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -180,6 +182,11 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
                         st, handled);
       break;
     case kPolV5NoUnroll: e = launch_fwd_v5(a, causal, 2, 0, st, handled); break;
+    case kPolV5Causal8: case kPolV5Causal4:
+      if (causal)
+        e = launch_fwd_v5(a, true, 2, pol == kPolV5Causal8 ? v5::kDefault : v5::kDefault & ~v5::kW8,
+                          st, handled);
+      break;
     default: break;
   }
   if (!causal && !*handled) {  // non-causal-only v5 forms
@@ -225,6 +232,13 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
 #endif
     if (var >= 0) e = launch_fwd_v5(a, false, ahead, var, st, handled);
   }
+  if (!*handled && pol == kPolDefault && causal && a.d == 64 &&
+      (int64_t)((a.N + 511) / 512 + 1) / 2 * a.B * a.H >= 256)
+    // causal d = 64 with at least one 8-wave workgroup per CU: v5 with paired light / heavy
+    // query blocks and each wave's masked diagonal tile inside its pipelined loop (982 vs
+    // 819 TF/s for v4 at C3 causal, 1072 vs 916 at (1,16,16384,64); with fewer workgroups
+    // than CUs v4's 256-query blocks fill the chip better: profiles/r2_ab_causal_v5.txt).
+    e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
   if (!*handled && pol == kPolDefault && a.d == 64)
     // causal, ragged N or short N: v4. Causal pairs a heavy and a light query block per
     // workgroup, light block first (860 vs 806 TF/s unpaired at C3; 4 waves below

@@ -1,6 +1,8 @@
 // FlashAttention forward, bf16 MFMA kernel v5 (d = 64, N % 64 == 0): two 32-query blocks
-// per wave, skewed by half a tile. Causal: the pipelined loop covers the key tiles below
-// the workgroup's first query; the four diagonal tiles run a serial masked path.
+// per wave, skewed by half a tile. Causal: a workgroup takes a light and a heavy query block
+// of one head in turn; each wave runs the pipelined loop over the key tiles up to its own
+// diagonal tile (the peeled last tile, masked), then keeps staging and joining barriers for
+// the waves whose diagonal lies further on.
 //
 // v4 gives each wave one 32-query block and relies on the second wave of its SIMD to
 // overlap one wave's softmax with the other's MFMAs. v5 gives each wave two blocks, A and
@@ -261,12 +263,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   const int nblk = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
   const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  const int bh = logical / nqb;
-  const int qb = CAUSAL ? nqb - 1 - logical % nqb : logical % nqb;  // causal: heaviest first
+  // Non-causal: one query block per workgroup. Causal: a pair of query blocks of one head,
+  // the light block u first, then the heavy block nqb-1-u (every workgroup walks about
+  // nqb + 1 blocks' worth of key tiles; the heavy block finds the light block's tiles still
+  // in the XCD's L2).
+  const int nunit = CAUSAL ? (nqb + 1) / 2 : nqb;
+  const int bh = logical / nunit, unit = logical % nunit;
   const int b = bh / p.H, hh = bh % p.H;
-  const int q0 = qb * kBQ;
-  const int qw = q0 + wave * 64;              // first query of this wave (block A; B = +32)
-  const int qA = qw + c32;                    // this lane's query in block A; B = qA + 32
 
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
   const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
@@ -277,16 +280,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   const __amdgpu_buffer_rsrc_t rv =
       __builtin_amdgcn_make_buffer_rsrc((void*)Vg, (short)0, ((N - 1) * svn + D) * 2, 0x00020000);
 
-  bf16x8 qfA[4], qfB[4];
-  {
-    const bf16* ra = Qg + (int64_t)min(qA, N - 1) * p.sq[2];
-    const bf16* rb = Qg + (int64_t)min(qA + 32, N - 1) * p.sq[2];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      qfA[ks] = *(const bf16x8*)(ra + ks * 16 + 8 * hf);
-      qfB[ks] = *(const bf16x8*)(rb + ks * 16 + 8 * hf);
-    }
-  }
   Ctx5<LPT> c;
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) c.koff[ks] = k_swz<D>(c32, 2 * ks + hf);
@@ -312,20 +305,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
     }
   }
   const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
-  // Tiles: non-causal, all N / 64 and every one mask-free. Causal: the keys below the
-  // workgroup's last query; the first q0 / 64 tiles are mask-free for all its queries, the
-  // last four hold the diagonal (serial path, masked per block, skipped where fully masked).
-  const int ntiles = CAUSAL ? min(N, q0 + kBQ) / kBK : N / kBK;
-  const int nbulk = CAUSAL ? q0 / kBK : ntiles;
   const float c2 = p.scale_log2;
-
-  f32x16 OA[2], OB[2];
-  bf16x8 vk[8];  // Vᵀ fragments kept from P2 to P4 (VAR bit 32768)
-  constexpr int kKeep = (VAR & 32768) ? 1 : 0;
-  float mA = -INFINITY, mB = -INFINITY;
-  float pA = 0.f, pB = 0.f;  // this lane's share of each block's row sum
-#pragma unroll
-  for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
 
   auto dma_k = [&](bf16* slot, int step) __attribute__((always_inline)) {
 #pragma unroll
@@ -342,25 +322,69 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   if (NW == 8 && (VAR & 4096) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
     __builtin_amdgcn_s_setprio(1);
 
-  // ---- pass 0: the pipelined loop with the frozen first-tile reference over the tiles
-  //      [0, nbulk), mask-free for every query of the workgroup ---------------------------
-  if (!CAUSAL || nbulk >= 2) {  // non-causal: the launcher guarantees N >= 128
-    uint4 rK[LPT], rV[LPT];
-    if (VAR & 1024) {
-      dma_k(sK, 0);
-      dma_v(sV, 0);
-      dma_k(sK + TILE, ktile_b);
-      if (VAR & 524288) __builtin_amdgcn_s_waitcnt(0x0F70);  // asm DMA: hipcc does not wait
-    } else {
-      load5(rK, rk, c.kgo, 0);
-      load5(rV, rv, c.vgo, 0);
-      store5(sK, rK, c.kso);
-      store5(sV, rV, c.vso);
-      load5(rK, rk, c.kgo, ktile_b);
-      store5(sK + TILE, rK, c.kso);
-    }
-    __syncthreads();
+  // One query block [q0, q0 + kBQ) of head bh.
+  auto run_block = [&](const int q0) __attribute__((always_inline)) {
+  const int qw = q0 + wave * 64;              // first query of this wave (block A; B = +32)
+  const int qA = qw + c32;                    // this lane's query in block A; B = qA + 32
 
+  bf16x8 qfA[4], qfB[4];
+  {
+    const bf16* ra = Qg + (int64_t)min(qA, N - 1) * p.sq[2];
+    const bf16* rb = Qg + (int64_t)min(qA + 32, N - 1) * p.sq[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qfA[ks] = *(const bf16x8*)(ra + ks * 16 + 8 * hf);
+      qfB[ks] = *(const bf16x8*)(rb + ks * 16 + 8 * hf);
+    }
+  }
+  // Tiles the workgroup stages: non-causal all N / 64; causal the keys below its last query.
+  // Tiles this wave computes: non-causal all; causal [0, tD] with tD = qw / 64 its diagonal
+  // tile (the last, masked; none when the wave's queries are past N). A causal wave that
+  // is done keeps staging its share of the later tiles and joins every barrier (the tail
+  // loop), so all waves of the workgroup take the same barriers.
+  const int ntiles = CAUSAL ? min(N, q0 + kBQ) / kBK : N / kBK;
+  const int tD = qw / kBK;
+  const int nbulk = CAUSAL ? (qw < N ? tD + 1 : 0) : ntiles;
+
+  f32x16 OA[2], OB[2];
+  bf16x8 vk[8];  // Vᵀ fragments kept from P2 to P4 (VAR bit 32768)
+  constexpr int kKeep = (VAR & 32768) ? 1 : 0;
+  float mA = -INFINITY, mB = -INFINITY;
+  float pA = 0.f, pB = 0.f;  // this lane's share of each block's row sum
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
+
+  // causal diagonal tile of a wave (keys qw .. qw + 63): key row r of a 32-key block is
+  // masked for this lane's query when it lies above it (row > c32 within the same block)
+  auto mask_tri = [&](f32x16& s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (acc_row(r, hf) > c32) s[r] = -INFINITY;
+  };
+  auto mask_all = [&](f32x16& s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = -INFINITY;
+  };
+
+  // ---- pass 0: the pipelined loop with the frozen first-tile reference over the tiles
+  //      [0, nbulk); causal: its last tile is the wave's masked diagonal -------------------
+  uint4 rK[LPT], rV[LPT];
+  if (VAR & 1024) {
+    dma_k(sK, 0);
+    dma_v(sV, 0);
+    dma_k(sK + TILE, ktile_b);
+    if (VAR & 524288) __builtin_amdgcn_s_waitcnt(0x0F70);  // asm DMA: hipcc does not wait
+  } else {
+    load5(rK, rk, c.kgo, 0);
+    load5(rV, rv, c.vgo, 0);
+    store5(sK, rK, c.kso);
+    store5(sV, rV, c.vso);
+    load5(rK, rk, c.kgo, ktile_b);
+    store5(sK + TILE, rK, c.kso);
+  }
+  __syncthreads();
+
+  if (nbulk >= 1) {  // non-causal: the launcher guarantees N >= 128
     // reference maxima from tile 0; S_B(0) kept for the pipeline, P_B(0) keys 0-31 computed
     f32x16 SA[2], SB[2];
     {
@@ -371,6 +395,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       bf16x8 dpf[2];
       phase_qk<false, AHEAD, VAR>(sK, ko, qfA, SA, SA[0], c2, 0.f, dummy, dpf);
       phase_qk<false, AHEAD, VAR>(sK, ko, qfB, SB, SB[0], c2, 0.f, dummy, dpf);
+    }
+    if (CAUSAL && tD == 0) {  // tile 0 is this wave's diagonal: reference over visible keys
+      mask_tri(SA[0]);
+      mask_all(SA[1]);
+      mask_tri(SB[1]);
     }
     mA = row_max32(SA[0], SA[1]);
     mB = row_max32(SB[0], SB[1]);
@@ -448,7 +477,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       for (int ks = 0; ks < 4; ++ks) koA[ks] = c.koff[ks] + (t & 3) * TILE;
       vo[0] = c.voff[0] + (t & (kVS - 1)) * TILE;
       vo[1] = c.voff[1] + (t & (kVS - 1)) * TILE;
+      if (CAUSAL) mask_tri(SB[1]);  // S_B(tD), keys 32-63: the diagonal of block B
       phase_qk<true, AHEAD, VAR>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);
+      if (CAUSAL) {  // S_A(tD): keys 0-31 the diagonal of block A, keys 32-63 above it
+        mask_tri(SA[0]);
+        mask_all(SA[1]);
+      }
       phase_pv<true, AHEAD, VAR, kKeep>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0, vk);
 #pragma unroll
       for (int i = 0; i < 8; ++i) sm_pair<VAR>(SA[1], i, c2, nmcA, accA, pA1);
@@ -459,10 +493,25 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
     pA = accA[0] + accA[1];
     pB = accB[0] + accB[1];
   }
+  if (CAUSAL) {
+    // tail: this wave's share of the staging of the tiles the other waves still need
+    for (int t = nbulk > 0 ? nbulk - 1 : 0; t + 1 < ntiles; ++t) {
+      if (VAR & 1024) {
+        dma_k(sK + ((t + 2) & 3) * TILE, (t + 2) * ktile_b);
+        dma_v(sV + ((t + 1) & (kVS - 1)) * TILE, (t + 1) * vtile_b);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+      } else {
+        load5(rK, rk, c.kgo, (t + 2) * ktile_b);
+        load5(rV, rv, c.vgo, (t + 1) * vtile_b);
+        store5(sK + ((t + 2) & 3) * TILE, rK, c.kso);
+        store5(sV + ((t + 1) & 1) * TILE, rV, c.vso);
+      }
+      __syncthreads();
+    }
+  }
 
-  // ---- serial path: tiles [t0, ntiles) with the per-tile deferred-max bookkeeping ------
-  // (causal diagonal tiles after the bulk; the whole range if the bulk was too short or a
-  // lane's row-sum share left 2^64, in which case the workgroup starts over)
+  // ---- serial path: every tile again with the per-tile deferred-max bookkeeping, when a
+  // lane's row-sum share left 2^64 (the workgroup starts over) ----------------------------
   auto serial = [&](int t0) {
     int ko[4], vo[2];
 #pragma unroll
@@ -470,12 +519,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
     vo[0] = c.voff[0];
     vo[1] = c.voff[1];
     for (int t = t0; t < ntiles; ++t) {
-      uint4 rK[LPT], rV[LPT];
-      load5(rK, rk, c.kgo, t * ktile_b);
-      load5(rV, rv, c.vgo, t * vtile_b);
+      uint4 rK2[LPT], rV2[LPT];
+      load5(rK2, rk, c.kgo, t * ktile_b);
+      load5(rV2, rv, c.vgo, t * vtile_b);
       __syncthreads();
-      store5(sK, rK, c.kso);
-      store5(sV, rV, c.vso);
+      store5(sK, rK2, c.kso);
+      store5(sV, rV2, c.vso);
       __syncthreads();
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk) {
@@ -517,15 +566,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       }
     }
   };
-  const int tdone = (!CAUSAL || nbulk >= 2) ? nbulk : 0;
   if (__syncthreads_or(!(pA <= kLimit) || !(pB <= kLimit))) {
     mA = mB = -INFINITY;
     pA = pB = 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
     serial(0);
-  } else if (CAUSAL && tdone < ntiles) {
-    serial(tdone);
   }
   const float lA = lane_pair_sum(pA), lB = lane_pair_sum(pB);
 
@@ -566,6 +612,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       }
     }
   }
+  };  // run_block
+
+  if (CAUSAL) {
+    const int heavy = nqb - 1 - unit;
+    run_block(unit * kBQ);
+    if (heavy != unit) {
+      __syncthreads();  // every wave is done with the light block's LDS tiles
+      run_block(heavy * kBQ);
+    }
+  } else {
+    run_block(unit * kBQ);
+  }
 }
 
 // d = 64, N a multiple of 64 (no ragged tile) and at least two tiles, and all per-head K/V
@@ -583,7 +641,11 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
   void (*kfn)(AttnArgs, int);
   const int nw = (var & 2048) ? 8 : 4;  // VAR bit 2048 (launcher only): 8 waves per workgroup
   var &= ~2048;
-  if (nw == 8 && ahead == 3)  // LDS operand reads 3 / 4 MFMAs ahead (policies 57 / 58)
+  if (causal)  // paired query blocks, pipelined diagonal (8 or 4 waves), or the 4-wave forms
+    kfn = var == 99332 ? (nw == 8 ? fa_fwd_bf16_v5<2, 99332, true, 8> : fa_fwd_bf16_v5<2, 99332, true, 4>)
+          : var == 4   ? fa_fwd_bf16_v5<2, 4, true>
+                       : fa_fwd_bf16_v5<2, 0, true>;
+  else if (nw == 8 && ahead == 3)  // LDS operand reads 3 / 4 MFMAs ahead (policies 57 / 58)
     kfn = fa_fwd_bf16_v5<3, 99332, false, 8>;
   else if (nw == 8 && ahead == 4)
     kfn = fa_fwd_bf16_v5<4, 99332, false, 8>;
@@ -599,8 +661,6 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
           : var == 99332 ? fa_fwd_bf16_v5<2, 99332, false, 8>
           : var == 623620 ? fa_fwd_bf16_v5<2, 623620, false, 8>
                         : fa_fwd_bf16_v5<2, 4, false, 8>;
-  else if (causal)
-    kfn = var == 4 ? fa_fwd_bf16_v5<2, 4, true> : fa_fwd_bf16_v5<2, 0, true>;
   else if (var == 1028)
     kfn = fa_fwd_bf16_v5<2, 1028, false>;
 #ifdef MT_DIAGNOSTICS
@@ -622,7 +682,8 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
   if (e != hipSuccess) return e;
   const int kBQ = 64 * nw;
   const int nqb = (a.N + kBQ - 1) / kBQ;
-  const int64_t nblk = (int64_t)nqb * a.B * a.H;
+  // causal: one workgroup per (light, heavy) pair of query blocks
+  const int64_t nblk = (int64_t)(causal ? (nqb + 1) / 2 : nqb) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(64 * nw), smem, st, a, nqb);
   return hipGetLastError();

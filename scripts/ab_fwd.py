@@ -1,0 +1,33 @@
+"""Interleaved in-process A/B timing of forward-kernel policies (diagnostics, GPU box).
+usage: python scripts/ab_fwd.py POL[,POL...] [causal] [B,H,N,d] [rounds]"""
+import os, sys, time
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "llmsys-project-flashattn_amd"))
+import torch
+from minitorch import _hip
+pols = [int(x) for x in sys.argv[1].split(",")]
+causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
+B, H, N, d = (int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "8,16,4096,64").split(","))
+rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 7
+g = torch.Generator(device="cuda").manual_seed(0)
+q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
+o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
+flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
+t0 = time.time()
+while time.time() - t0 < 0.5:  # clock ramp
+    _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l); torch.cuda.synchronize()
+res = {p: [] for p in pols}
+reps = max(3, int(2e12 / flops))
+for rnd in range(rounds):
+    for p in pols:
+        _hip.set_policy(p)
+        for _ in range(2): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(); e0.record()
+        for _ in range(reps): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
+        e1.record(); torch.cuda.synchronize()
+        res[p].append(e0.elapsed_time(e1) / reps)
+_hip.set_policy(0)
+print(f"shape {(B, H, N, d)} causal={causal} reps={reps} rounds={rounds}")
+for p in pols:
+    t = sorted(res[p]); med = t[len(t) // 2]
+    print(f"policy {p:3d}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s", flush=True)

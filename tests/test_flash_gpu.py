@@ -268,6 +268,49 @@ def test_long_causal_paired_default(torch_dev, d):
     _subset_check_fwd(torch, q, k, v, o, True, [(0, 0), (0, 2)], 1e-3, 2.0 ** -7)
 
 
+@pytest.mark.parametrize("policy", [0, 67, 68])
+def test_v5_causal_pairs_vs_oracle(torch_dev, policy, parity_record):
+    """The v5 causal form (paired light/heavy query blocks per workgroup, each wave's
+    pipelined loop ending on its own masked diagonal tile, finished waves staging for the
+    rest): every head, every row against the C oracle at the elementwise causal bound.
+    Shapes: one tile past the minimum (N = 128, 192), a single query block, an odd number
+    of query blocks (the middle block runs alone), partial last blocks with waves past N,
+    and a long head."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(67)
+    worst = 0.0
+    try:
+        _hip.set_policy(policy)
+        for (B, H, N) in ((1, 2, 128), (2, 1, 192), (1, 2, 512), (1, 3, 1216), (1, 1, 1600),
+                          (2, 2, 2560), (1, 1, 8192)):
+            q, k, v = (A.bf16_round(rng.standard_normal((B, H, N, 64)).astype(np.float32))
+                       for _ in range(3))
+            o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), True)
+            torch.cuda.synchronize()
+            o_ref, m_ref, l_ref = cref.attn_fwd(q.reshape(B * H, N, 64), k.reshape(B * H, N, 64),
+                                                v.reshape(B * H, N, 64), True)
+            o_ref = o_ref.reshape(B, H, N, 64)
+            bound = 1e-3 + 2.0 ** -7 * _pv_abs(q, k, v)
+            err = np.abs(_np(o) - o_ref)
+            assert np.all(err <= bound), f"{(B, H, N)}: max err/bound {float((err / bound).max()):.3f}"
+            _check_ml(_np(m), _np(l), m_ref.reshape(B, H, N), l_ref.reshape(B, H, N), exact=False)
+            worst = max(worst, float(err.max()))
+    finally:
+        _hip.set_policy(0)
+    parity_record("test_v5_causal_pairs_vs_oracle", f"policy {policy}", max_abs=worst,
+                  bound="1e-3 + 2^-7 * (P|V|) elementwise")
+
+
+def _pv_abs(q, k, v):
+    """(P |V|) per element for causal heads (the O term of tests/bounds.py), from the C
+    oracle run on |V|."""
+    B, H, N, d = q.shape
+    pabs, _, _ = cref.attn_fwd(q.reshape(B * H, N, d), k.reshape(B * H, N, d),
+                               np.abs(v).reshape(B * H, N, d), True)
+    return pabs.reshape(B, H, N, d)
+
+
 def test_deterministic(torch_dev):
     """No atomics: two runs are bitwise identical."""
     from minitorch import _hip
@@ -313,7 +356,8 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # 21-26 v4, 27-31 / 35-39 / 46-49 / 54-58 / 61 v5, 32 / 33 / 44 / 45 d = 128, 50-53 / 63-65
 # causal heavy + light query-block pairs. Every one computes the same attention.
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
-                 44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65)
+                 44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
+                 67, 68)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
