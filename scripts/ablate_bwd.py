@@ -6,7 +6,8 @@ import torch
 from minitorch import _hip
 # diagnostics build (make DIAG=1): the product library rejects the ablation policies
 _DIAG = os.path.join(os.path.dirname(_hip.LIB_PATH), "diag", "libminitorch_hip_diag.so")
-if os.path.exists(_DIAG):
+if os.environ.get("MT_DIAG") == "1":  # only when asked: the diag build can be stale
+    assert os.path.exists(_DIAG), "make -C llmsys-project-flashattn_amd DIAG=1"
     _hip.use_library(_DIAG)
 pols = [int(x) for x in sys.argv[1].split(",")]
 causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
