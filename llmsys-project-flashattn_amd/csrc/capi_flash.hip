@@ -75,7 +75,7 @@ enum : int {
   // default). (42, the register-staged 64-query form at two waves per SIMD, was removed: its
   // spilling build computed a wrong dK whenever N / 64 was odd.)
   kPolBwdPipe = 40, kPolBwdQ32 = 43, kPolBwdQ64OneWave = 62,
-  kPolBwdQ64Dma = 66,
+  kPolBwdQ64Dma = 66, kPolBwdQ64Dma8 = 69,  // 69: 66 with 8 waves (256 keys) per workgroup
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -85,15 +85,15 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
   for (int v : kValidPolicies)
     if (v == p) return true;
 #ifdef MT_DIAGNOSTICS
-  // wrong-result ablations (timing only): v5 80-86 / 97, v4 91-96, fast 10-15
-  if ((p >= 80 && p <= 86) || p == 97 || (p >= 91 && p <= 96) || (p >= 10 && p <= 15)) return true;
+  // wrong-result ablations (timing only): v5 80-86 / 97, v4 91-96, fast 10-15, bwd 87-90
+  if ((p >= 80 && p <= 97) || (p >= 10 && p <= 15)) return true;
 #endif
   return false;
 }
@@ -215,7 +215,10 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       case kPolDefault:
         // d = 64, N % 64 == 0: v5 with 8 waves, LDS-DMA K/V staging, Vᵀ reuse and the
         // exp-to-use distance (policy 56; A/B history in DESIGN.md §3, profiles/r1_ab_v5_*).
-        var = v5::kDefault;
+        // With fewer 8-wave workgroups than CUs (the 8-GPU strong split of C3 leaves 16
+        // heads per GPU: 128 workgroups), the 4-wave form's 256-query blocks fill the chip:
+        // 864 vs 699 TF/s at (1,16,4096,64) (profiles/r2_ab_small_grids.txt).
+        var = (int64_t)((N + 511) / 512) * a.B * a.H < 256 ? (v5::kDma | v5::kUnroll) : v5::kDefault;
         break;
       default: break;
     }
@@ -353,16 +356,21 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
   const int pol = g_kernel_policy.load(std::memory_order_relaxed);
   if (dtype == MT_BF16 && vec && pol != kPolGeneric) {
     bool handled = false;
-    // dK/dV forms: 0 32-query steps, 1 software-pipelined, 2 64-query steps, 3 64-query
-    // steps at one wave per SIMD, 4 64-query steps with LDS-DMA Q/dO. Default: 2
-    // non-causal (1.912 vs 1.952 ms at C3), 0 causal (1.12 vs 1.31 ms: the masked diagonal
-    // steps spill in the 64-query form). An in-wave interleaved dQ tile measured 1.7 %
-    // slower than the plain tile and was removed (profiles/r1_ab_bwd_dq.txt).
+    // dK/dV forms: 0 32-query steps, 1 software-pipelined, 3 64-query steps at one wave
+    // per SIMD, 4 64-query steps with LDS-DMA Q/dO, 5 the same with 8 waves (256 keys per
+    // dK/dV workgroup, 256 queries per dQ workgroup). Default: 5 non-causal (1.868 vs
+    // 1.937 ms for 4 at C3, profiles/r2_ab_bwd.txt), 0 causal (1.12 vs 1.31 ms: the masked
+    // diagonal steps spill in the 64-query form). An in-wave interleaved dQ tile measured
+    // 1.7 % slower than the plain tile and was removed (profiles/r1_ab_bwd_dq.txt).
     const int variant = pol == kPolBwdPipe        ? 1
                         : pol == kPolBwdQ64OneWave ? 3
                         : pol == kPolBwdQ64Dma     ? 4
+                        : pol == kPolBwdQ64Dma8    ? 5
+#ifdef MT_DIAGNOSTICS
+                        : (pol >= 87 && pol <= 90)  ? pol - 81  // dK/dV ablations (wrong results)
+#endif
                         : pol == kPolBwdQ32        ? 0
-                                                   : (causal ? 0 : 4);
+                                                   : (causal ? 0 : 5);
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }

@@ -68,13 +68,14 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
 }
 
 // LDS-DMA: one wave instruction moves 64 x 16 B from per-lane buffer offsets (go) to 1 KiB
-// of LDS at dst in lane order (8 rows of a [rows][64] bf16 image); the image swizzle is
-// applied on the per-lane source. Issued from inline asm so hipcc's waitcnt pass does not
-// put a vmcnt(0) in front of the next LDS read (fa_fwd_v5.hip dma5, VAR bit 524288); the
-// caller waits vmcnt(0) before the barrier that publishes the slot. M0 is saved/restored.
-__device__ __forceinline__ void dma_rows(void* dst, __amdgpu_buffer_rsrc_t rs, int go) {
-  const unsigned lds = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)dst);
+// of LDS at byte address lds (wave-uniform, an SGPR) in lane order (8 rows of a [rows][64]
+// bf16 image); the image swizzle is applied on the per-lane source. Issued from inline asm
+// so hipcc's waitcnt pass does not put a vmcnt(0) in front of the next LDS read (fa_fwd_v5.hip
+// dma5, VAR bit 524288); the caller waits vmcnt(0) before the barrier that publishes the
+// slot. M0 is saved/restored. The LDS address is a 32-bit scalar (the workgroup's LDS base
+// read once, plus constants): a generic pointer here costs a 64-bit VGPR pair per
+// destination, a readfirstlane pair and a null check per instruction, and spills.
+__device__ __forceinline__ void dma_rows(uint32_t lds, __amdgpu_buffer_rsrc_t rs, int go) {
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
@@ -82,6 +83,12 @@ __device__ __forceinline__ void dma_rows(void* dst, __amdgpu_buffer_rsrc_t rs, i
       : "=&s"(keep)
       : "v"(go), "s"(lds), "s"(rs)
       : "memory");
+}
+
+// The workgroup's dynamic-LDS base as a wave-uniform 32-bit byte address.
+__device__ __forceinline__ uint32_t lds_base(const void* smem) {
+  return __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
 }
 
 }  // namespace
@@ -125,7 +132,9 @@ struct DkvCtx {
   int toff[2];          // transpose-image offsets per d block
 };
 
-template <bool CAUSAL, bool MASK>
+// ABL (diagnostic timing builds only, wrong results): bit 1 skips the softmax VALU (P = S,
+// dS = dP' go straight to bf16).
+template <bool CAUSAL, bool MASK, int ABL = 0>
 __device__ __forceinline__ void dkv_tile(const char* slot, const DkvCtx& c, f32x16 (&dK)[2],
                                          f32x16 (&dV)[2], float c2, int qt, int N, int my_k, int hf) {
   const bf16* Qr = (const bf16*)slot;
@@ -154,11 +163,13 @@ __device__ __forceinline__ void dkv_tile(const char* slot, const DkvCtx& c, f32x
       if (q >= N || (CAUSAL && my_k > q)) S[r] = -INFINITY;
     }
   }
+  if (!(ABL & 1)) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float pv = __builtin_amdgcn_exp2f(S[r] * c2);
-    S[r] = pv;
-    dP[r] = pv * dP[r];
+    for (int r = 0; r < 16; ++r) {
+      const float pv = __builtin_amdgcn_exp2f(S[r] * c2);
+      S[r] = pv;
+      dP[r] = pv * dP[r];
+    }
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -574,8 +585,17 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16(AttnArgs p, int nkb) {
 // 512 VGPR+AGPR, no spills, no second wave to overlap with).
 // DMA: the Q / dO images arrive by LDS-DMA (dma_rows) instead of buffer loads into VGPRs
 // plus ds_writes: no staging registers live across the step (policy 66, A/B variant).
-template <bool CAUSAL, int MINB = 2, bool DMA = false>
-__global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int nkb) {
+// NW = waves per workgroup (32 keys each): 4, or 8 with DMA (256 keys per workgroup: every
+// staged Q / dO step feeds twice the keys, halving the L2 -> LDS traffic per MFMA; each
+// wave then stages one of the two 32-query sub-tiles).
+// ABL (diagnostic timing builds only, wrong results): bit 1 no softmax VALU, bit 2 no
+// staging after the first step, bit 4 no barrier per step.
+template <bool CAUSAL, int MINB = 2, bool DMA = false, int NW = 4, int ABL = 0>
+__global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int nkb) {
+  static_assert(NW == 4 || (NW == 8 && DMA), "8-wave form: LDS-DMA staging only");
+#ifndef MT_DIAGNOSTICS
+  static_assert(ABL == 0, "wrong-result ablations exist only in the MT_DIAGNOSTICS build");
+#endif
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
@@ -583,7 +603,8 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int bh = logical / nkb, kb = logical % nkb;
   const int b = bh / p.H, hh = bh % p.H;
-  const int k0 = kb * 128;
+  constexpr int kKB = 32 * NW;  // keys per workgroup
+  const int k0 = kb * kKB;
   const int my_k = k0 + wave * 32 + c32;
   const int wk_lo = k0 + wave * 32;
 
@@ -616,8 +637,13 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
   // DMA: wave w fills rows 8w..8w+7 of each image; lane l -> row 8w + l/8, LDS chunk l%8,
   // which holds source chunk (l%8) ^ swz(row) (the swizzles are XOR, self-inverse)
   int gdq[2] = {0, 0}, gdo[2] = {0, 0};
+  // this wave's rows 8w..8w+7 of every image (8 waves: rows 8(w%4).. of sub-tile w/4's
+  // images), as a scalar LDS byte address
+  const int wq = NW == 8 ? (wave & 3) : wave, wu = NW == 8 ? (wave >> 2) : 0;
+  const uint32_t lds0 = lds_base(smem) + __builtin_amdgcn_readfirstlane(wq) * 8 * D * 2 +
+                        __builtin_amdgcn_readfirstlane(wu) * kBufQ;
   if (DMA) {
-    const int r = 8 * wave + (lane >> 3), pc = lane & 7;
+    const int r = 8 * wq + (lane >> 3), pc = lane & 7;
     const int ck = pc ^ ((r >> 1) & 7), cv = pc ^ (((r >> 1) & 1) << 2);
     gdq[0] = (r * sqn + ck * 8) * 2;
     gdq[1] = (r * sqn + cv * 8) * 2;
@@ -634,9 +660,16 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
 #define DKV2_LOAD(T_, SLOT_)                                                             \
   {                                                                                      \
     const int qs_ = qt0 + (T_) * kStep;                                                  \
-    _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
+    if (NW == 8) {                                                                       \
+      const uint32_t img_ = lds0 + 2 * (SLOT_) * kBufQ;                                  \
+      const int oq_ = (qs_ + wu * kQT) * sqn * 2, oo_ = (qs_ + wu * kQT) * son * 2;      \
+      dma_rows(img_, rq, gdq[0] + oq_);                                                  \
+      dma_rows(img_ + kImgQ * 2, rq, gdq[1] + oq_);                                      \
+      dma_rows(img_ + 2 * kImgQ * 2, ro, gdo[0] + oo_);                                  \
+      dma_rows(img_ + 3 * kImgQ * 2, ro, gdo[1] + oo_);                                  \
+    } else _Pragma("unroll") for (int u = 0; u < 2; ++u) {                               \
       if (DMA) {                                                                         \
-        char* img_ = smem + (2 * (SLOT_) + u) * kBufQ + wave * 8 * D * 2;                \
+        const uint32_t img_ = lds0 + (2 * (SLOT_) + u) * kBufQ;                          \
         const int oq_ = (qs_ + u * kQT) * sqn * 2, oo_ = (qs_ + u * kQT) * son * 2;      \
         dma_rows(img_, rq, gdq[0] + oq_);                                                \
         dma_rows(img_ + kImgQ * 2, rq, gdq[1] + oq_);                                    \
@@ -680,21 +713,21 @@ __global__ __launch_bounds__(256, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int
   __syncthreads();
   // steps: [0, nhead) causal diagonal (masked), [nhead, nfull) mask-free, [nfull, nstep)
   // ragged tail (masked)
-  const int nhead = CAUSAL ? min(nstep, 128 / kStep) : 0;
+  const int nhead = CAUSAL ? min(nstep, kKB / kStep) : 0;
   const int nfull = max(nhead, (N - qt0) / kStep);
 #define DKV2_STEP(MASK_, SLOT_, T_)                                                      \
   {                                                                                      \
     const int t_ = (T_);                                                                 \
-    const bool more_ = t_ + 1 < nstep;                                                   \
+    const bool more_ = t_ + 1 < nstep && !(ABL & 2);                                     \
     if (more_) DKV2_LOAD(t_ + 1, (SLOT_) ^ 1)                                            \
     _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
       const int qt_ = qt0 + t_ * kStep + u * kQT;                                        \
       if (!(MASK_) || (qt_ < N && (!CAUSAL || qt_ + kQT - 1 >= wk_lo)))                 \
-        dkv_tile<CAUSAL, MASK_>(smem + (2 * (SLOT_) + u) * kBufQ, c, dK, dV, c2, qt_, N, \
-                                my_k, hf);                                               \
+        dkv_tile<CAUSAL, MASK_, ABL>(smem + (2 * (SLOT_) + u) * kBufQ, c, dK, dV, c2, qt_, \
+                                     N, my_k, hf);                                       \
     }                                                                                    \
     if (more_) DKV2_STORE((SLOT_) ^ 1)                                                   \
-    __syncthreads();                                                                     \
+    if (!(ABL & 4)) __syncthreads();                                                     \
   }
   int t = 0;
   for (; t < nhead; ++t) {
@@ -795,8 +828,10 @@ __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16
 
 }  // namespace
 
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
+// NW = waves per workgroup (32 queries each): 4 or 8 (256 queries: every staged K / V tile
+// feeds twice the queries).
+template <bool CAUSAL, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
@@ -806,7 +841,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
   int qb = logical % nqb;
   if (CAUSAL) qb = nqb - 1 - qb;  // heaviest first
   const int b = bh / p.H, hh = bh % p.H;
-  const int q0 = qb * 128;
+  constexpr int kQB = 32 * NW;  // queries per workgroup
+  constexpr int kRows = 8 / NW;  // 16-B staging chunks per thread per image (64 rows x 8)
+  const int q0 = qb * kQB;
   const int my_q = q0 + wave * 32 + c32;
   const int wq_hi = q0 + wave * 32 + 31;
 
@@ -833,25 +870,25 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
   const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
   const int skn = (int)p.sk[2], svn = (int)p.sv[2];
   const __amdgpu_buffer_rsrc_t rk = head_rsrc(Kg, N, skn), rv = head_rsrc(Vg, N, svn);
-  int gk[2], gv[2], srow[2], stri[2];
+  int gk[kRows], gv[kRows], srow[kRows], stri[kRows];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = (tid >> 3) + 32 * i, cc = tid & 7;
+  for (int i = 0; i < kRows; ++i) {
+    const int r = (tid >> 3) + 8 * NW * i, cc = tid & 7;
     gk[i] = (r * skn + cc * 8) * 2;
     gv[i] = (r * svn + cc * 8) * 2;
     srow[i] = k_swz<D>(r, cc);
     stri[i] = v_swz<D>(r, cc);
   }
 
-  const int kend = CAUSAL ? min(N, q0 + 128) : N;
+  const int kend = CAUSAL ? min(N, q0 + kQB) : N;
   const int ntile = (kend + kKT - 1) / kKT;
   const int nfull = CAUSAL ? min(N / kKT, q0 / kKT) : N / kKT;
 
-  uint4 sk[2], svv[2];
+  uint4 sk[kRows], svv[kRows];
 #define DQ_LOAD(T_)                                                                      \
   {                                                                                      \
     const int k0_ = (T_) * kKT;                                                          \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                      \
+    _Pragma("unroll") for (int i = 0; i < kRows; ++i) {                                  \
       sk[i] = bload(rk, gk[i] + k0_ * skn * 2);                                          \
       svv[i] = bload(rv, gv[i] + k0_ * svn * 2);                                         \
     }                                                                                    \
@@ -859,7 +896,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
 #define DQ_STORE(SLOT_)                                                                  \
   {                                                                                      \
     bf16* img = (bf16*)(smem + (SLOT_) * kBufK);                                         \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                      \
+    _Pragma("unroll") for (int i = 0; i < kRows; ++i) {                                  \
       *(uint4*)(img + srow[i]) = sk[i];                                                  \
       *(uint4*)(img + kImgK + stri[i]) = sk[i];                                          \
       *(uint4*)(img + 2 * kImgK + srow[i]) = svv[i];                                     \
@@ -921,28 +958,37 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   {
-    const int nkb = (a.N + 127) / 128;
+    const int kkb = variant >= 5 ? 256 : 128;  // keys per workgroup
+    const int nkb = (a.N + kkb - 1) / kkb;
     const int64_t nblk = (int64_t)nkb * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
     const size_t smem = (variant == 1 ? 3 : variant >= 2 ? 4 : 2) * (size_t)kBufQ;
     auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
                : variant == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
                : variant == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
+               : variant == 5 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
+#ifdef MT_DIAGNOSTICS
+               : variant == 6 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 1>
+               : variant == 7 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 2>
+               : variant == 8 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 6>
+               : variant == 9 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 7>
+#endif
                               : fa_bwd_dkv_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(256), smem, st, a, nkb);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(kkb * 2), smem, st, a, nkb);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   {
-    const int nqb = (a.N + 127) / 128;
+    const int kqb = variant >= 5 ? 256 : 128;  // queries per workgroup
+    const int nqb = (a.N + kqb - 1) / kqb;
     const int64_t nblk = (int64_t)nqb * a.B * a.H;
     const size_t smem = 2 * (size_t)kBufK;
-    auto kfn = fa_bwd_dq_bf16<CAUSAL>;
+    auto kfn = variant >= 5 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(256), smem, st, a, nqb);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(kqb * 2), smem, st, a, nqb);
     return hipGetLastError();
   }
 }
