@@ -374,14 +374,25 @@ def extra_legs(torch, _hip, time_fn):
     extra["bwd_causal_ms"] = round(bwdc_ms, 4)
     extra["bwd_causal_tflops"] = round(2.5 * fwd_flops(B, H, N, d, True) / (bwdc_ms * 1e-3) / 1e12, 2)
     del q, k, v, do, o, m, l, dq, dk, dv, ws
-    # config 2: (8,16,1024,64) fp32 forward
+    # config 2: (8,16,1024,64) fp32 forward, and the fp32 backward minitorch's MHA runs
+    # (the reference's own precision)
     c2 = (8, 16, 1024, 64)
-    q2, k2, v2 = (make_shard(torch, c2, 0, torch.float32, s, "cuda") for s in (5, 6, 7))
-    c2_ms = time_fn(lambda: _hip.flash_fwd(q2, k2, v2, False), 20, 3)
+    q2, k2, v2, do2 = (make_shard(torch, c2, 0, torch.float32, s, "cuda") for s in (5, 6, 7, 11))
+    o2 = torch.empty_like(q2)
+    m2 = torch.empty(c2[:3], dtype=torch.float32, device="cuda")
+    l2 = torch.empty_like(m2)
+    c2_ms = time_fn(lambda: _hip.flash_fwd(q2, k2, v2, False, out=o2, m=m2, l=l2), 20, 3)
     extra["c2_fp32_fwd_ms"] = round(c2_ms, 4)
     extra["c2_fp32_fwd_tflops"] = round(fwd_flops(*c2) / (c2_ms * 1e-3) / 1e12, 2)
     extra["c2_fp32_frac_of_f32_peak"] = round(extra["c2_fp32_fwd_tflops"] / PEAK_F32_TFLOPS, 4)
-    del q2, k2, v2
+    ws2 = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(*c2) // 4, dtype=torch.float32,
+                      device="cuda")
+    g2 = [torch.empty_like(q2) for _ in range(3)]
+    c2b_ms = time_fn(lambda: _hip.flash_bwd(q2, k2, v2, o2, do2, m2, l2, False, dq=g2[0], dk=g2[1],
+                                            dv=g2[2], workspace=ws2), 10, 2)
+    extra["c2_fp32_bwd_ms"] = round(c2b_ms, 4)
+    extra["c2_fp32_bwd_tflops"] = round(2.5 * fwd_flops(*c2) / (c2b_ms * 1e-3) / 1e12, 2)
+    del q2, k2, v2, do2, o2, m2, l2, ws2, g2
     # config 4's per-GPU shard at 8 GPUs: (8,16,16384,128) bf16 forward (1/8 of B = 64)
     c4 = (8, 16, 16384, 128)
     q4, k4, v4 = (make_shard(torch, c4, 0, torch.bfloat16, s, "cuda") for s in (8, 9, 10))
@@ -397,8 +408,9 @@ def extra_legs(torch, _hip, time_fn):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # default: ~1 s of timed device work at C3 (0.5 ms per step)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
     ap.add_argument("--split", choices=("strong", "weak"), default="strong")
     ap.add_argument("--causal", action="store_true")
@@ -445,10 +457,17 @@ def main():
         clock = Clock(torch, "cuda")
 
         def time_fn(fn, steps, warmup):
+            # warm-up, then a ~0.15 s clock ramp, then at least `steps` calls and ~0.2 s of them
             for _ in range(warmup):
                 fn()
             clock.sync()
-            return clock.span(fn, steps)
+            t0 = time.perf_counter()
+            fn()
+            clock.sync()
+            one = max(time.perf_counter() - t0, 1e-5)
+            for _ in range(int(0.15 / one)):
+                fn()
+            return clock.span(fn, max(steps, int(0.2 / one)))
 
         result["extra"] = extra_legs(torch, _hip, time_fn)
 

@@ -768,6 +768,128 @@ __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p,
   }
 }
 
+// dK/dV, 8 waves, with the two waves of each SIMD half a step apart (MI355X_MICROARCH.md,
+// "Two waves per SIMD", item 9: partners running the same program with one barrier per
+// block reach their MFMA bursts, their softmax VALU and their LDS reads together).
+// Step t = 64 queries (sub-tiles u0, u1), staged by LDS-DMA two steps ahead into a 4-step
+// ring (130 KiB, one workgroup per CU). Waves 0-3 (SIMD partners of waves 4-7) compute
+// (t, u0) then (t, u1); waves 4-7 compute (t - 1, u1) then (t, u0), and (last, u1) after
+// the loop, so the partner of a wave in its first sub-tile is in its second. Non-causal,
+// N % 64 == 0 (every step mask-free); the launcher sends other shapes to the 64-query
+// kernel.
+__global__ __launch_bounds__(512, 2) void fa_bwd_dkv_bf16_st(AttnArgs p, int nkb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int kStepB = 2 * kBufQ;  // bytes per ring step (2 sub-tiles)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = logical / nkb, kb = logical % nkb;
+  const int b = bh / p.H, hh = bh % p.H;
+  const int k0 = kb * 256;
+  const int my_k = k0 + wave * 32 + c32;
+  const bool late = __builtin_amdgcn_readfirstlane(wave) >= 4;
+
+  DkvCtx c;
+  {
+    const int kr = min(my_k, N - 1);
+    const bf16* krow = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1] + (int64_t)kr * p.sk[2];
+    const bf16* vrow = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1] + (int64_t)kr * p.sv[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      c.kf[ks] = *(const bf16x8*)(krow + 16 * ks + 8 * hf);
+      c.vf[ks] = *(const bf16x8*)(vrow + 16 * ks + 8 * hf);
+      c.roff[ks] = k_swz<D>(c32, 2 * ks + hf);
+    }
+    c.toff[0] = tr_off(lane, 0);
+    c.toff[1] = tr_off(lane, 1);
+  }
+  const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* Og = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int sqn = (int)p.sq[2], son = (int)p.sdo[2];
+  const __amdgpu_buffer_rsrc_t rq = head_rsrc(Qg, N, sqn), ro = head_rsrc(Og, N, son);
+  const float* nlse = p.lse2 + (int64_t)bh * N;
+  const float* ndel = p.delta + (int64_t)bh * N;
+  // DMA: wave w stages rows 8(w%4) .. +7 of the four images of sub-tile w/4
+  const int wq = wave & 3, wu = wave >> 2;
+  const uint32_t lds0 = lds_base(smem) + __builtin_amdgcn_readfirstlane(wq) * 8 * D * 2 +
+                        __builtin_amdgcn_readfirstlane(wu) * kBufQ;
+  int gq0, gq1, go0, go1;
+  {
+    const int r = 8 * wq + (lane >> 3), pc = lane & 7;
+    const int ck = pc ^ ((r >> 1) & 7), cv = pc ^ (((r >> 1) & 1) << 2);
+    gq0 = (r * sqn + ck * 8) * 2 + wu * kQT * sqn * 2;
+    gq1 = (r * sqn + cv * 8) * 2 + wu * kQT * sqn * 2;
+    go0 = (r * son + ck * 8) * 2 + wu * kQT * son * 2;
+    go1 = (r * son + cv * 8) * 2 + wu * kQT * son * 2;
+  }
+  const int nstep = N / 64;
+  float sv = 0.f;
+  auto stage = [&](int t, int slot) __attribute__((always_inline)) {
+    const uint32_t img = lds0 + slot * kStepB;
+    const int oq = t * 64 * sqn * 2, oo = t * 64 * son * 2;
+    dma_rows(img, rq, gq0 + oq);
+    dma_rows(img + kImgQ * 2, rq, gq1 + oq);
+    dma_rows(img + 2 * kImgQ * 2, ro, go0 + oo);
+    dma_rows(img + 3 * kImgQ * 2, ro, go1 + oo);
+    if (tid < 4 * kQT) {
+      const int q = t * 64 + (tid >> 6) * kQT + (tid & (kQT - 1));
+      sv = (tid & kQT) == 0 ? nlse[q] : ndel[q];
+    }
+  };
+  auto publish = [&](int slot) __attribute__((always_inline)) {
+    if (tid < 4 * kQT)
+      ((float*)((bf16*)(smem + slot * kStepB + (tid >> 6) * kBufQ) + 4 * kImgQ))[tid & 63] = sv;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x16 dK[2], dV[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
+  const float c2 = p.scale_log2;
+
+  // prologue: steps 0 and 1 staged
+  stage(0, 0);
+  publish(0);
+  if (nstep > 1) {
+    stage(1, 1);
+    publish(1);
+  }
+  __syncthreads();
+  for (int t = 0; t < nstep; ++t) {
+    // 4-step ring: step t + 2 goes into the slot of step t - 2, which every wave finished
+    // before the last barrier (waves 4-7 read step t - 2's sub-tile u1 during step t - 1)
+    const bool more = t + 2 < nstep;
+    if (more) stage(t + 2, (t + 2) & 3);
+    const char* cur = smem + (t & 3) * kStepB;
+    if (!late) {
+      dkv_tile<false, false>(cur, c, dK, dV, c2, 0, N, my_k, hf);
+      dkv_tile<false, false>(cur + kBufQ, c, dK, dV, c2, 0, N, my_k, hf);
+    } else {
+      if (t > 0) dkv_tile<false, false>(smem + ((t - 1) & 3) * kStepB + kBufQ, c, dK, dV, c2, 0, N, my_k, hf);
+      dkv_tile<false, false>(cur, c, dK, dV, c2, 0, N, my_k, hf);
+    }
+    if (more) publish((t + 2) & 3);
+    __syncthreads();
+  }
+  if (late) dkv_tile<false, false>(smem + ((nstep - 1) & 3) * kStepB + kBufQ, c, dK, dV, c2, 0, N, my_k, hf);
+
+  if (my_k < N) {
+    bf16* dKg = (bf16*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
+    bf16* dVg = (bf16*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
+    const float sc = p.scale;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = db * 32 + 8 * g + 4 * hf;
+        store4(dKg + col, dK[db][4 * g] * sc, dK[db][4 * g + 1] * sc, dK[db][4 * g + 2] * sc,
+               dK[db][4 * g + 3] * sc, true);
+        store4(dVg + col, dV[db][4 * g], dV[db][4 * g + 1], dV[db][4 * g + 2], dV[db][4 * g + 3], true);
+      }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // dQ. Workgroup = 4 waves = 128 queries; 64-key tiles.
 namespace {
@@ -830,6 +952,7 @@ __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16
 
 // NW = waves per workgroup (32 queries each): 4 or 8 (256 queries: every staged K / V tile
 // feeds twice the queries).
+// (Capping it at 3 waves per SIMD, 168 VGPRs, spills 42-70 values: not kept.)
 template <bool CAUSAL, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -953,20 +1076,23 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb
 // ---------------------------------------------------------------------------------------
 template <bool CAUSAL>
 static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t st) {
+  // (variant is adjusted below for shapes a form does not take)
   const int64_t rows = (int64_t)a.B * a.H * a.N;
   hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   {
+    if (variant == 11 && (CAUSAL || a.N % 64 != 0)) variant = 5;  // staggered form: mask-free shapes
     const int kkb = variant >= 5 ? 256 : 128;  // keys per workgroup
     const int nkb = (a.N + kkb - 1) / kkb;
     const int64_t nblk = (int64_t)nkb * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-    const size_t smem = (variant == 1 ? 3 : variant >= 2 ? 4 : 2) * (size_t)kBufQ;
+    const size_t smem = (variant == 11 ? 8 : variant == 1 ? 3 : variant >= 2 ? 4 : 2) * (size_t)kBufQ;
     auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
                : variant == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
                : variant == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
                : variant == 5 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
+               : variant == 11 ? fa_bwd_dkv_bf16_st
 #ifdef MT_DIAGNOSTICS
                : variant == 6 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 1>
                : variant == 7 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 2>
