@@ -856,19 +856,20 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkv_bf16_st(AttnArgs p, int nkb
     publish(1);
   }
   __syncthreads();
+  // The same instruction stream for both halves, only the two sub-tile addresses differ
+  // (a branch around the tiles would make the compiler copy the accumulators between
+  // the two paths): early (t, u0), (t, u1); late (t - 1, u1), (t, u0). Step 0 is peeled
+  // for the late half, which has no step -1.
+  const uint32_t lateb = late ? 1u : 0u;
   for (int t = 0; t < nstep; ++t) {
     // 4-step ring: step t + 2 goes into the slot of step t - 2, which every wave finished
     // before the last barrier (waves 4-7 read step t - 2's sub-tile u1 during step t - 1)
     const bool more = t + 2 < nstep;
     if (more) stage(t + 2, (t + 2) & 3);
-    const char* cur = smem + (t & 3) * kStepB;
-    if (!late) {
-      dkv_tile<false, false>(cur, c, dK, dV, c2, 0, N, my_k, hf);
-      dkv_tile<false, false>(cur + kBufQ, c, dK, dV, c2, 0, N, my_k, hf);
-    } else {
-      if (t > 0) dkv_tile<false, false>(smem + ((t - 1) & 3) * kStepB + kBufQ, c, dK, dV, c2, 0, N, my_k, hf);
-      dkv_tile<false, false>(cur, c, dK, dV, c2, 0, N, my_k, hf);
-    }
+    const int cur = (t & 3) * kStepB, prv = ((t - 1) & 3) * kStepB;
+    const int offA = lateb ? prv + kBufQ : cur, offB = lateb ? cur : cur + kBufQ;
+    if (t > 0 || !late) dkv_tile<false, false>(smem + offA, c, dK, dV, c2, 0, N, my_k, hf);
+    dkv_tile<false, false>(smem + offB, c, dK, dV, c2, 0, N, my_k, hf);
     if (more) publish((t + 2) & 3);
     __syncthreads();
   }
@@ -904,8 +905,12 @@ struct DqCtx {
 };
 
 template <bool CAUSAL, bool MASK>
+// PF: the eight Kᵀ transpose fragments of the dQ products are read right after the S / dP
+// products are issued (pinned there by a scheduling barrier), so they land during the
+// softmax instead of in front of each dQ MFMA.
 __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16 (&dQ)[2], float c2,
-                                        float nlq, const f32x16& dinit, int k0, int N, int my_q, int hf) {
+                                        float nlq, const f32x16& dinit, int k0, int N, int my_q, int hf,
+                                        bool PF = false) {
   const bf16* Kr = (const bf16*)slot;
   const bf16* Kt = Kr + kImgK;
   const bf16* Vr = Kr + 2 * kImgK;
@@ -920,6 +925,12 @@ __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16
       dP[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Vr + kb * 32 * D + c.roff[ks]),
                                                        c.of[ks], ks ? dP[kb] : dinit, 0, 0, 0);
     }
+  bf16x8 kt[8];
+  if (PF) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kt[i] = tr_frag(Kt, (i >> 2) * 32 + 16 * ((i >> 1) & 1), c.toff[i & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   if (MASK) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -943,8 +954,8 @@ __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16
       const bf16x8 sf = to_bf16x8(dP[kb], s);
 #pragma unroll
       for (int db = 0; db < 2; ++db)
-        dQ[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Kt, kb * 32 + 16 * s, c.toff[db]), sf,
-                                                         dQ[db], 0, 0, 0);
+        dQ[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            PF ? kt[kb * 4 + s * 2 + db] : tr_frag(Kt, kb * 32 + 16 * s, c.toff[db]), sf, dQ[db], 0, 0, 0);
     }
 }
 
@@ -953,7 +964,7 @@ __device__ __forceinline__ void dq_tile(const char* slot, const DqCtx& c, f32x16
 // NW = waves per workgroup (32 queries each): 4 or 8 (256 queries: every staged K / V tile
 // feeds twice the queries).
 // (Capping it at 3 waves per SIMD, 168 VGPRs, spills 42-70 values: not kept.)
-template <bool CAUSAL, int NW = 4>
+template <bool CAUSAL, int NW = 4, bool PF = false>
 __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1041,7 +1052,7 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb
     if (more_) DQ_LOAD(t_ + 1)                                                           \
     if (!(MASK_) || !CAUSAL || t_ * kKT <= wq_hi)                                        \
       dq_tile<CAUSAL, MASK_>(smem + (SLOT_) * kBufK, c, dQ, c2, nlq, dinit, t_ * kKT, N, \
-                             my_q, hf);                                                  \
+                             my_q, hf, PF);                                              \
     if (more_) DQ_STORE((SLOT_) ^ 1)                                                     \
     __syncthreads();                                                                     \
   }
@@ -1091,7 +1102,7 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
                : variant == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
                : variant == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
-               : variant == 5 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
+               : (variant == 5 || variant == 12) ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
                : variant == 11 ? fa_bwd_dkv_bf16_st
 #ifdef MT_DIAGNOSTICS
                : variant == 6 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 1>
@@ -1111,7 +1122,8 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     const int nqb = (a.N + kqb - 1) / kqb;
     const int64_t nblk = (int64_t)nqb * a.B * a.H;
     const size_t smem = 2 * (size_t)kBufK;
-    auto kfn = variant >= 5 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
+    auto kfn = variant == 12 ? fa_bwd_dq_bf16<CAUSAL, 8, true>
+               : variant >= 5 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(kqb * 2), smem, st, a, nqb);

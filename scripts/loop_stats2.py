@@ -8,7 +8,7 @@ import sys
 path, kname = sys.argv[1], sys.argv[2]
 L = open(path).read().split("\n")
 a = next(i for i, l in enumerate(L) if l.startswith(kname + ":"))
-b = next(i for i in range(a, len(L)) if "s_endpgm" in L[i])
+b = next(i for i in range(a, len(L)) if L[i].startswith(".Lfunc_end"))
 L = L[a:b + 1]
 blocks, cur = [], None  # (label line, header of the loop it belongs to)
 for i, l in enumerate(L):
