@@ -1019,6 +1019,7 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb
 
 // ---------------------------------------------------------------------------------------
 hipError_t launch_dkv_w64(const AttnArgs& a, int nkb, unsigned nblk, size_t smem, hipStream_t st);
+hipError_t launch_dq_pipe(const AttnArgs& a, int nqb, unsigned nblk, hipStream_t st);
 
 template <bool CAUSAL>
 static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t st) {
@@ -1030,6 +1031,7 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   {
     if (variant == 11 && (CAUSAL || a.N % 64 != 0)) variant = 5;  // staggered form: mask-free shapes
     if (variant == 13 && (CAUSAL || a.N % 32 != 0)) variant = 5;  // one-wave-per-SIMD form: the same
+    if (variant == 14 && (CAUSAL || a.N % 64 != 0)) variant = 5;  // pipelined dQ: the same
     const int kkb = variant >= 5 ? 256 : 128;  // keys per workgroup
     const int nthr = variant == 13 ? 256 : kkb * 2;
     const int nkb = (a.N + kkb - 1) / kkb;
@@ -1039,7 +1041,7 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
                : variant == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
                : variant == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
-               : (variant == 5 || variant == 12) ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
+               : (variant == 5 || variant == 12 || variant == 14) ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
                : variant == 11 ? fa_bwd_dkv_bf16_st
 #ifdef MT_DIAGNOSTICS
                : variant == 6 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 1>
@@ -1063,6 +1065,7 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     const int nqb = (a.N + kqb - 1) / kqb;
     const int64_t nblk = (int64_t)nqb * a.B * a.H;
     const size_t smem = 2 * (size_t)kBufK;
+    if (variant == 14) return launch_dq_pipe(a, nqb, (unsigned)nblk, st);
     auto kfn = variant == 12 ? fa_bwd_dq_bf16<CAUSAL, 8, true>
                : variant >= 5 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
