@@ -80,6 +80,8 @@ enum : int {
   kPolBwdDqPf = 71,     // 69 with the dQ kernel's Kᵀ fragments read ahead of the softmax
   kPolBwdW64 = 72,      // dK/dV at one wave per SIMD, 64 keys per wave (non-causal, N % 32 == 0)
   kPolBwdDqPipe = 73,   // 69 with the in-wave pipelined dQ kernel (non-causal, N % 64 == 0)
+  kPolBwdMix0 = 74,     // 43's 32-query dK/dV (128 keys) with the 8-wave dQ
+  kPolBwdMix4 = 75,     // 66's 4-wave LDS-DMA dK/dV with the 8-wave dQ
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -89,7 +91,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -374,6 +376,8 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
                         : pol == kPolBwdDqPf       ? 12
                         : pol == kPolBwdW64        ? 13
                         : pol == kPolBwdDqPipe     ? 14
+                        : pol == kPolBwdMix0       ? 15
+                        : pol == kPolBwdMix4       ? 16
 #ifdef MT_DIAGNOSTICS
                         : (pol >= 87 && pol <= 90)  ? pol - 81  // dK/dV ablations (wrong results)
 #endif

@@ -1028,29 +1028,39 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  // variant -> (dK/dV form, dQ form). dK/dV: 0 32-query steps (128 keys), 1 software-
+  // pipelined, 3 / 4 64-query steps (one wave per SIMD / LDS-DMA), 5 the 8-wave LDS-DMA form
+  // (256 keys), 11 staggered SIMD partners, 13 one wave per SIMD with 64 keys per wave.
+  // dQ: 4 (128 queries) or 8 waves (256), 8 with the Kᵀ reads ahead (12), in-wave pipelined (14).
+  int dkv = variant, dq = variant >= 5 ? 8 : 4;
+  if (variant == 12) dkv = 5;
+  if (variant == 14) dkv = 5;
+  if (variant == 15) { dkv = 0; dq = 8; }   // causal A/B: 128-key dK/dV, 8-wave dQ
+  if (variant == 16) { dkv = 4; dq = 8; }   // causal A/B: 4-wave LDS-DMA dK/dV, 8-wave dQ
+  if (variant == 12) dq = 12;
+  if (variant == 14) dq = (CAUSAL || a.N % 64 != 0) ? 8 : 14;  // pipelined dQ: mask-free shapes
+  if (dkv == 11 && (CAUSAL || a.N % 64 != 0)) dkv = 5;  // staggered form: mask-free shapes
+  if (dkv == 13 && (CAUSAL || a.N % 32 != 0)) dkv = 5;  // one-wave-per-SIMD form: the same
   {
-    if (variant == 11 && (CAUSAL || a.N % 64 != 0)) variant = 5;  // staggered form: mask-free shapes
-    if (variant == 13 && (CAUSAL || a.N % 32 != 0)) variant = 5;  // one-wave-per-SIMD form: the same
-    if (variant == 14 && (CAUSAL || a.N % 64 != 0)) variant = 5;  // pipelined dQ: the same
-    const int kkb = variant >= 5 ? 256 : 128;  // keys per workgroup
-    const int nthr = variant == 13 ? 256 : kkb * 2;
+    const int kkb = dkv >= 5 ? 256 : 128;  // keys per workgroup
+    const int nthr = dkv == 13 ? 256 : kkb * 2;
     const int nkb = (a.N + kkb - 1) / kkb;
     const int64_t nblk = (int64_t)nkb * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-    const size_t smem = (variant == 11 ? 8 : variant == 1 ? 3 : variant == 13 ? 3 : variant >= 2 ? 4 : 2) * (size_t)kBufQ;
-    auto kfn = variant == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
-               : variant == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
-               : variant == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
-               : (variant == 5 || variant == 12 || variant == 14) ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
-               : variant == 11 ? fa_bwd_dkv_bf16_st
+    const size_t smem = (dkv == 11 ? 8 : (dkv == 1 || dkv == 13) ? 3 : dkv >= 2 ? 4 : 2) * (size_t)kBufQ;
+    auto kfn = dkv == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
+               : dkv == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
+               : dkv == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
+               : dkv == 5 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
+               : dkv == 11 ? fa_bwd_dkv_bf16_st
 #ifdef MT_DIAGNOSTICS
-               : variant == 6 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 1>
-               : variant == 7 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 2>
-               : variant == 8 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 6>
-               : variant == 9 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 7>
+               : dkv == 6 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 1>
+               : dkv == 7 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 2>
+               : dkv == 8 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 6>
+               : dkv == 9 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 7>
 #endif
-                              : fa_bwd_dkv_bf16<CAUSAL>;
-    if (variant == 13) {
+                          : fa_bwd_dkv_bf16<CAUSAL>;
+    if (dkv == 13) {
       e = launch_dkv_w64(a, nkb, (unsigned)nblk, smem, st);
     } else {
       e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -1061,13 +1071,13 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     if (e != hipSuccess) return e;
   }
   {
-    const int kqb = variant >= 5 ? 256 : 128;  // queries per workgroup
+    const int kqb = dq == 4 ? 128 : 256;  // queries per workgroup
     const int nqb = (a.N + kqb - 1) / kqb;
     const int64_t nblk = (int64_t)nqb * a.B * a.H;
     const size_t smem = 2 * (size_t)kBufK;
-    if (variant == 14) return launch_dq_pipe(a, nqb, (unsigned)nblk, st);
-    auto kfn = variant == 12 ? fa_bwd_dq_bf16<CAUSAL, 8, true>
-               : variant >= 5 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
+    if (dq == 14) return launch_dq_pipe(a, nqb, (unsigned)nblk, st);
+    auto kfn = dq == 12 ? fa_bwd_dq_bf16<CAUSAL, 8, true>
+               : dq == 8 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(kqb * 2), smem, st, a, nqb);
