@@ -82,6 +82,9 @@ enum : int {
   kPolBwdDqPipe = 73,   // 69 with the in-wave pipelined dQ kernel (non-causal, N % 64 == 0)
   kPolBwdMix0 = 74,     // 43's 32-query dK/dV (128 keys) with the 8-wave dQ
   kPolBwdMix4 = 75,     // 66's 4-wave LDS-DMA dK/dV with the 8-wave dQ
+  // v5 with the keys split between the two halves of an 8-wave workgroup (256 queries per
+  // workgroup, non-causal, N % 128 == 0, N >= 256)
+  kPolV5Split = 76,
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -91,7 +94,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -109,7 +112,7 @@ static bool policy_valid(int p) {
 // staggered waves, Vᵀ fragment reuse, exp-to-use distance, DMA from inline asm.
 namespace v5 {
 constexpr int kUnroll = 4, kDma = 1024, kW8 = 2048, kPrio = 4096, kScalar = 8192,
-              kStagger = 16384, kVKeep = 32768, kDefer = 65536, kAsmDma = 524288;
+              kStagger = 16384, kVKeep = 32768, kDefer = 65536, kSplit = 131072, kAsmDma = 524288;
 constexpr int kDefault = kW8 | kDefer | kVKeep | kDma | kUnroll;
 }  // namespace v5
 
@@ -218,13 +221,20 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
         ahead = pol - kPolV5Defer + 2;
         break;
       case kPolV5AsmDma: var = v5::kDefault | v5::kAsmDma; break;
+      case kPolV5Split: var = v5::kDefault | v5::kSplit; break;
       case kPolDefault:
         // d = 64, N % 64 == 0: v5 with 8 waves, LDS-DMA K/V staging, Vᵀ reuse and the
         // exp-to-use distance (policy 56; A/B history in DESIGN.md §3, profiles/r1_ab_v5_*).
         // With fewer 8-wave workgroups than CUs (the 8-GPU strong split of C3 leaves 16
-        // heads per GPU: 128 workgroups), the 4-wave form's 256-query blocks fill the chip:
-        // 864 vs 699 TF/s at (1,16,4096,64) (profiles/r2_ab_small_grids.txt).
-        var = (int64_t)((N + 511) / 512) * a.B * a.H < 256 ? (v5::kDma | v5::kUnroll) : v5::kDefault;
+        // heads per GPU: 128 workgroups), the keys are split between the two halves of each
+        // 8-wave workgroup (256 queries per workgroup, twice the workgroups, two waves per
+        // SIMD): 975 vs 911 TF/s for the 4-wave form at (1,16,4096,64), 602 vs 503 at
+        // (1,8,4096,64) (profiles/r2_ab_split.txt); shapes the split does not take
+        // (N % 128 != 0 or N < 256) keep the 4-wave form (profiles/r2_ab_small_grids.txt).
+        if ((int64_t)((N + 511) / 512) * a.B * a.H < 256)
+          var = (N % 128 == 0 && N >= 256) ? (v5::kDefault | v5::kSplit) : (v5::kDma | v5::kUnroll);
+        else
+          var = v5::kDefault;
         break;
       default: break;
     }

@@ -243,11 +243,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   static_assert((VAR & (2 | 8 | 16 | 64 | 128 | 256)) == 0,
                 "wrong-result ablation variants exist only in the MT_DIAGNOSTICS build");
 #endif
-  constexpr int LPT = lpt<NW>();
-  constexpr int kBQ = 64 * NW;  // queries per workgroup
+  // VAR bit 131072 (8 waves, non-causal, LDS-DMA): split keys inside the workgroup. Waves
+  // 0-3 and 4-7 take the same 256 queries (wave w and w + 4 the same 64) over the first and
+  // the second half of the keys, each half with its own K/V rings and its own share of the
+  // staging, both under the same barriers; at the end the second half hands (m, l, O) to the
+  // first through LDS, which merges the two and stores. A grid of B·H·N / 256 workgroups
+  // then runs two waves per SIMD where the unsplit 8-wave form has fewer workgroups than CUs.
+  constexpr bool SPLIT = (VAR & 131072) != 0;
+  static_assert(!SPLIT || (NW == 8 && !CAUSAL && (VAR & 1024)), "split keys: 8 waves, non-causal, LDS-DMA");
+  constexpr int NWQ = SPLIT ? 4 : NW;  // waves sharing one query block and its key tiles
+  constexpr int LPT = lpt<NWQ>();
+  constexpr int kBQ = 64 * NWQ;  // queries per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  bf16* const sK = (bf16*)smem_raw;          // [kKSlots][TILE]
-  bf16* const sV = sK + kKSlots * TILE;      // [kVS][TILE]
   // VAR bit 16384 (8 waves): waves 4-7 (the second wave of each SIMD) take the tile barrier
   // after P2 instead of after P4, so they run half a tile behind waves 0-3 and the two
   // waves of a SIMD stop reaching their MFMA / VALU bursts in lockstep
@@ -258,6 +265,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N;
+  const int half = SPLIT ? (__builtin_amdgcn_readfirstlane(wave) >> 2) : 0;
+  const int wq = SPLIT ? (wave & 3) : wave;  // this wave's 64 queries within the block
+  const int Nk = SPLIT ? N / 2 : N;          // keys this wave's half walks
+  bf16* const sK = (bf16*)smem_raw + half * (kKSlots + kVS) * TILE;  // [kKSlots][TILE]
+  bf16* const sV = sK + kKSlots * TILE;                              // [kVS][TILE]
   const bool late = (VAR & 16384) && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= 4;
 
   const int nblk = gridDim.x, hw = blockIdx.x;
@@ -272,13 +284,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   const int b = bh / p.H, hh = bh % p.H;
 
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
-  const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
-  const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1] + (int64_t)half * Nk * p.sk[2];
+  const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1] + (int64_t)half * Nk * p.sv[2];
   const int skn = (int)p.sk[2], svn = (int)p.sv[2];
   const __amdgpu_buffer_rsrc_t rk =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Kg, (short)0, ((N - 1) * skn + D) * 2, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)Kg, (short)0, ((Nk - 1) * skn + D) * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rv =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Vg, (short)0, ((N - 1) * svn + D) * 2, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)Vg, (short)0, ((Nk - 1) * svn + D) * 2, 0x00020000);
 
   Ctx5<LPT> c;
 #pragma unroll
@@ -290,16 +302,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       const int col = db * 32 + 16 * g + 4 * (i16 & 3);
       c.voff[db] = v_swz<D>(4 * hf + (i16 >> 2), col >> 3) + (col & 7);
     }
-    const int st_r = tid / (D / 8), st_c = tid % (D / 8);
+    const int tq = SPLIT ? (tid & 255) : tid;  // thread index within the half
+    const int st_r = tq / (D / 8), st_c = tq % (D / 8);
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int r = st_r + i * (64 * NW / (D / 8));
+      const int r = st_r + i * (64 * NWQ / (D / 8));
       c.kgo[i] = (r * skn + st_c * 8) * 2;
       c.vgo[i] = (r * svn + st_c * 8) * 2;
       c.kso[i] = k_swz<D>(r, st_c);
       c.vso[i] = v_swz<D>(r, st_c);
       // DMA: wave w's instruction i fills rows 8 * (LPT * w + i) .. + 7
-      const int dr = 8 * (LPT * wave + i) + (lane >> 3), dc = lane & 7;
+      const int dr = 8 * (LPT * wq + i) + (lane >> 3), dc = lane & 7;
       c.kdo[i] = (dr * skn + (dc ^ ((dr >> 1) & 7)) * 8) * 2;
       c.vdo[i] = (dr * svn + (dc ^ (((dr >> 1) & 1) << 2)) * 8) * 2;
     }
@@ -309,11 +322,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
 
   auto dma_k = [&](bf16* slot, int step) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma5<VAR>(slot + 8 * (LPT * wave + i) * D, rk, c.kdo[i], step);
+    for (int i = 0; i < LPT; ++i) dma5<VAR>(slot + 8 * (LPT * wq + i) * D, rk, c.kdo[i], step);
   };
   auto dma_v = [&](bf16* slot, int step) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma5<VAR>(slot + 8 * (LPT * wave + i) * D, rv, c.vdo[i], step);
+    for (int i = 0; i < LPT; ++i) dma5<VAR>(slot + 8 * (LPT * wq + i) * D, rv, c.vdo[i], step);
   };
 
   // VAR bit 4096 (8 waves): the younger half of the workgroup (waves 4-7) runs at issue
@@ -324,7 +337,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
 
   // One query block [q0, q0 + kBQ) of head bh.
   auto run_block = [&](const int q0) __attribute__((always_inline)) {
-  const int qw = q0 + wave * 64;              // first query of this wave (block A; B = +32)
+  const int qw = q0 + wq * 64;                // first query of this wave (block A; B = +32)
   const int qA = qw + c32;                    // this lane's query in block A; B = qA + 32
 
   bf16x8 qfA[4], qfB[4];
@@ -342,7 +355,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   // tile (the last, masked; none when the wave's queries are past N). A causal wave that
   // is done keeps staging its share of the later tiles and joins every barrier (the tail
   // loop), so all waves of the workgroup take the same barriers.
-  const int ntiles = CAUSAL ? min(N, q0 + kBQ) / kBK : N / kBK;
+  const int ntiles = CAUSAL ? min(N, q0 + kBQ) / kBK : Nk / kBK;
   const int tD = qw / kBK;
   const int nbulk = CAUSAL ? (qw < N ? tD + 1 : 0) : ntiles;
 
@@ -573,6 +586,44 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
     for (int i = 0; i < 2; ++i) { OA[i] = f32x16{}; OB[i] = f32x16{}; }
     serial(0);
   }
+  if (SPLIT) {  // merge the second half's (m, row-sum share, O) into the first half's
+    __syncthreads();  // every wave is done with its half's LDS tiles
+    float4* xch = (float4*)smem_raw + wq * 17 * 64 + lane;
+    if (half) {
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          xch[(4 * db + g) * 64] = make_float4(OA[db][4 * g], OA[db][4 * g + 1], OA[db][4 * g + 2], OA[db][4 * g + 3]);
+          xch[(8 + 4 * db + g) * 64] = make_float4(OB[db][4 * g], OB[db][4 * g + 1], OB[db][4 * g + 2], OB[db][4 * g + 3]);
+        }
+      xch[16 * 64] = make_float4(mA, mB, pA, pB);
+    }
+    __syncthreads();
+    if (half) return;
+    const float4 t = xch[16 * 64];
+    const float nA = fmaxf(mA, t.x), nB = fmaxf(mB, t.y);
+    const float a0 = __builtin_amdgcn_exp2f((mA - nA) * c2), a1 = __builtin_amdgcn_exp2f((t.x - nA) * c2);
+    const float b0 = __builtin_amdgcn_exp2f((mB - nB) * c2), b1 = __builtin_amdgcn_exp2f((t.y - nB) * c2);
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 u = xch[(4 * db + g) * 64], w = xch[(8 + 4 * db + g) * 64];
+        OA[db][4 * g] = OA[db][4 * g] * a0 + u.x * a1;
+        OA[db][4 * g + 1] = OA[db][4 * g + 1] * a0 + u.y * a1;
+        OA[db][4 * g + 2] = OA[db][4 * g + 2] * a0 + u.z * a1;
+        OA[db][4 * g + 3] = OA[db][4 * g + 3] * a0 + u.w * a1;
+        OB[db][4 * g] = OB[db][4 * g] * b0 + w.x * b1;
+        OB[db][4 * g + 1] = OB[db][4 * g + 1] * b0 + w.y * b1;
+        OB[db][4 * g + 2] = OB[db][4 * g + 2] * b0 + w.z * b1;
+        OB[db][4 * g + 3] = OB[db][4 * g + 3] * b0 + w.w * b1;
+      }
+    pA = pA * a0 + t.z * a1;
+    pB = pB * b0 + t.w * b1;
+    mA = nA;
+    mB = nB;
+  }
   const float lA = lane_pair_sum(pA), lB = lane_pair_sum(pB);
 
 #pragma unroll
@@ -633,11 +684,13 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
                          bool* handled) {
   *handled = false;
   if (a.d != 64 || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
+  const bool split = (var & 131072) != 0;  // split keys: each half needs two whole tiles
+  if (split && (causal || a.N % (2 * kBK) != 0 || a.N < 4 * kBK)) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
-  const size_t smem = (size_t)(kKSlots + ((var & 16384) ? 4 : kVSlots)) * TILE * sizeof(bf16);
+  const size_t smem = (size_t)(split ? 2 : 1) * (kKSlots + ((var & 16384) ? 4 : kVSlots)) * TILE * sizeof(bf16);
   void (*kfn)(AttnArgs, int);
   const int nw = (var & 2048) ? 8 : 4;  // VAR bit 2048 (launcher only): 8 waves per workgroup
   var &= ~2048;
@@ -659,6 +712,7 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
           : var == 33796 ? fa_fwd_bf16_v5<2, 33796, false, 8>
           : var == 37892 ? fa_fwd_bf16_v5<2, 37892, false, 8>
           : var == 99332 ? fa_fwd_bf16_v5<2, 99332, false, 8>
+          : var == 230404 ? fa_fwd_bf16_v5<2, 230404, false, 8>
           : var == 623620 ? fa_fwd_bf16_v5<2, 623620, false, 8>
                         : fa_fwd_bf16_v5<2, 4, false, 8>;
   else if (var == 1028)
@@ -680,7 +734,7 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
                        : fa_fwd_bf16_v5<2, 0, false>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
-  const int kBQ = 64 * nw;
+  const int kBQ = split ? 256 : 64 * nw;
   const int nqb = (a.N + kBQ - 1) / kBQ;
   // causal: one workgroup per (light, heavy) pair of query blocks
   const int64_t nblk = (int64_t)(causal ? (nqb + 1) / 2 : nqb) * a.B * a.H;

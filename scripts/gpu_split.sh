@@ -1,0 +1,15 @@
+# v5 split keys (policy 76): parity tests, then interleaved A/B at the strong-split shapes.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-split}
+timeout -k 10 600 python -u -m pytest tests/test_flash_gpu.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+   -k "split_keys or fast_policies or huge_spike or spiked_rescale or variants_agree" > gpurun_out/tests_$TAG.log 2>&1
+rc=$?
+tail -3 gpurun_out/tests_$TAG.log
+[ $rc -eq 0 ] || exit $rc
+: > gpurun_out/ab_$TAG.txt
+for shp in 1,16,4096,64 2,16,4096,64 1,8,4096,64 1,16,8192,64 8,16,4096,64; do
+  timeout -k 10 200 python scripts/ab_fwd.py ${POLS:-0,35,22,76,56} nc $shp 5 >> gpurun_out/ab_$TAG.txt 2>&1 || exit 1
+done
+cat gpurun_out/ab_$TAG.txt

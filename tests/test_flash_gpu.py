@@ -302,12 +302,45 @@ def test_v5_causal_pairs_vs_oracle(torch_dev, policy, parity_record):
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
-def _pv_abs(q, k, v):
-    """(P |V|) per element for causal heads (the O term of tests/bounds.py), from the C
-    oracle run on |V|."""
+@pytest.mark.parametrize("policy", [0, 76])
+def test_v5_split_keys_vs_oracle(torch_dev, policy, parity_record):
+    """v5 with the keys split between the two halves of an 8-wave workgroup (policy 76; the
+    default for grids of fewer 8-wave workgroups than CUs): every head, every row against
+    the C oracle at the non-causal bound 1e-3, including the merge of two halves whose
+    first-tile references differ (one key row aligned with a query row in the second half
+    only) and the smallest split shape (N = 256: two tiles per half)."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(76)
+    worst = 0.0
+    try:
+        _hip.set_policy(policy)
+        for (B, H, N) in ((1, 2, 256), (1, 3, 1024), (1, 16, 2048), (2, 1, 4096)):
+            q, k, v = (A.bf16_round(rng.standard_normal((B, H, N, 64)).astype(np.float32))
+                       for _ in range(3))
+            k[0, 0, N - 5] = A.bf16_round(q[0, 0, 7] * 3.0)  # a large score in the second half
+            o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), False)
+            torch.cuda.synchronize()
+            o_ref, m_ref, l_ref = cref.attn_fwd(q.reshape(B * H, N, 64), k.reshape(B * H, N, 64),
+                                                v.reshape(B * H, N, 64), False)
+            err = np.abs(_np(o) - o_ref.reshape(B, H, N, 64))
+            # short heads of N(0,1) scores average few keys, so |O| reaches ~1-2 and the bf16
+            # rounding of O alone passes 1e-3: the elementwise bound of tests/bounds.py
+            bound = 1e-3 + 2.0 ** -7 * _pv_abs(q, k, v, causal=False)
+            assert np.all(err <= bound), f"{(B, H, N)}: max err/bound {float((err / bound).max()):.3f}"
+            _check_ml(_np(m), _np(l), m_ref.reshape(B, H, N), l_ref.reshape(B, H, N), exact=False)
+            worst = max(worst, float((err / bound).max()))
+    finally:
+        _hip.set_policy(0)
+    parity_record("test_v5_split_keys_vs_oracle", f"policy {policy}", max_err_over_bound=worst,
+                  bound="1e-3 + 2^-7 * (P|V|) elementwise")
+
+
+def _pv_abs(q, k, v, causal=True):
+    """(P |V|) per element (the O term of tests/bounds.py), from the C oracle run on |V|."""
     B, H, N, d = q.shape
     pabs, _, _ = cref.attn_fwd(q.reshape(B * H, N, d), k.reshape(B * H, N, d),
-                               np.abs(v).reshape(B * H, N, d), True)
+                               np.abs(v).reshape(B * H, N, d), causal)
     return pabs.reshape(B, H, N, d)
 
 
@@ -357,7 +390,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # causal heavy + light query-block pairs. Every one computes the same attention.
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
                  44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
-                 67, 68)
+                 67, 68, 76)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
@@ -370,7 +403,7 @@ def test_fast_policies_vs_oracle(torch_dev, policy):
     try:
         _hip.set_policy(policy)
         for (B, H, N, d) in ((1, 3, 1000, 64), (2, 1, 517, 128), (1, 2, 64, 64), (1, 2, 1216, 64),
-                             (1, 1, 1536, 128)):
+                             (1, 1, 1536, 128), (1, 2, 768, 64)):
             q, k, v = (A.bf16_round(rng.standard_normal((B, H, N, d)).astype(np.float32))
                        for _ in range(3))
             for causal in (False, True):
