@@ -85,6 +85,7 @@ enum : int {
   // v5 with the keys split between the two halves of an 8-wave workgroup (256 queries per
   // workgroup, non-causal, N % 128 == 0, N >= 256)
   kPolV5Split = 76,
+  kPolBwdQ128 = 77,  // 69 with 128-query dK/dV steps (4 sub-tiles per barrier)
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -94,7 +95,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -388,6 +389,7 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
                         : pol == kPolBwdDqPipe     ? 14
                         : pol == kPolBwdMix0       ? 15
                         : pol == kPolBwdMix4       ? 16
+                        : pol == kPolBwdQ128       ? 17
 #ifdef MT_DIAGNOSTICS
                         : (pol >= 87 && pol <= 90)  ? pol - 81  // dK/dV ablations (wrong results)
 #endif

@@ -522,9 +522,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_bf16(AttnArgs p, int nkb) {
 // wave then stages one of the two 32-query sub-tiles).
 // ABL (diagnostic timing builds only, wrong results): bit 1 no softmax VALU, bit 2 no
 // staging after the first step, bit 4 no barrier per step.
-template <bool CAUSAL, int MINB = 2, bool DMA = false, int NW = 4, int ABL = 0>
+// SUB = 32-query sub-tiles per barrier-to-barrier step: 2, or 4 in the 8-wave form (half the
+// barriers and DMA waits per MFMA; 2 x 4 sub-slots of LDS, 133 KiB).
+template <bool CAUSAL, int MINB = 2, bool DMA = false, int NW = 4, int ABL = 0, int SUB = 2>
 __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p, int nkb) {
   static_assert(NW == 4 || (NW == 8 && DMA), "8-wave form: LDS-DMA staging only");
+  static_assert(SUB == 2 || (SUB == 4 && NW == 8), "4 sub-tiles per step: 8-wave form only");
 #ifndef MT_DIAGNOSTICS
   static_assert(ABL == 0, "wrong-result ablations exist only in the MT_DIAGNOSTICS build");
 #endif
@@ -568,10 +571,12 @@ __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p,
   const float* ndel = p.delta + (int64_t)bh * N;
   // DMA: wave w fills rows 8w..8w+7 of each image; lane l -> row 8w + l/8, LDS chunk l%8,
   // which holds source chunk (l%8) ^ swz(row) (the swizzles are XOR, self-inverse)
+  // this wave's rows 8w..8w+7 of every image (8 waves: rows 8(w%4).. of sub-tiles
+  // G(w/4) .. G(w/4) + G - 1, G = SUB / 2), as a scalar LDS byte address; one set of per-lane
+  // source offsets serves all G sub-tiles (the same rows, a wave-uniform query offset)
+  constexpr int G = NW == 8 ? SUB / 2 : 1;
   int gdq[2] = {0, 0}, gdo[2] = {0, 0};
-  // this wave's rows 8w..8w+7 of every image (8 waves: rows 8(w%4).. of sub-tile w/4's
-  // images), as a scalar LDS byte address
-  const int wq = NW == 8 ? (wave & 3) : wave, wu = NW == 8 ? (wave >> 2) : 0;
+  const int wq = NW == 8 ? (wave & 3) : wave, wu = NW == 8 ? G * (wave >> 2) : 0;
   const uint32_t lds0 = lds_base(smem) + __builtin_amdgcn_readfirstlane(wq) * 8 * D * 2 +
                         __builtin_amdgcn_readfirstlane(wu) * kBufQ;
   if (DMA) {
@@ -583,7 +588,7 @@ __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p,
     gdo[1] = (r * son + cv * 8) * 2;
   }
 
-  constexpr int kStep = 2 * kQT;
+  constexpr int kStep = SUB * kQT;
   const int qt0 = CAUSAL ? k0 : 0;
   const int nstep = N > qt0 ? (N - qt0 + kStep - 1) / kStep : 0;
 
@@ -593,12 +598,14 @@ __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p,
   {                                                                                      \
     const int qs_ = qt0 + (T_) * kStep;                                                  \
     if (NW == 8) {                                                                       \
-      const uint32_t img_ = lds0 + 2 * (SLOT_) * kBufQ;                                  \
-      const int oq_ = (qs_ + wu * kQT) * sqn * 2, oo_ = (qs_ + wu * kQT) * son * 2;      \
-      dma_rows(img_, rq, gdq[0] + oq_);                                                  \
-      dma_rows(img_ + kImgQ * 2, rq, gdq[1] + oq_);                                      \
-      dma_rows(img_ + 2 * kImgQ * 2, ro, gdo[0] + oo_);                                  \
-      dma_rows(img_ + 3 * kImgQ * 2, ro, gdo[1] + oo_);                                  \
+      _Pragma("unroll") for (int g = 0; g < G; ++g) {                                    \
+        const uint32_t img_ = lds0 + (SUB * (SLOT_) + g) * kBufQ;                        \
+        const int oq_ = (qs_ + (wu + g) * kQT) * sqn * 2, oo_ = (qs_ + (wu + g) * kQT) * son * 2; \
+        dma_rows(img_, rq, gdq[0] + oq_);                                                \
+        dma_rows(img_ + kImgQ * 2, rq, gdq[1] + oq_);                                    \
+        dma_rows(img_ + 2 * kImgQ * 2, ro, gdo[0] + oo_);                                \
+        dma_rows(img_ + 3 * kImgQ * 2, ro, gdo[1] + oo_);                                \
+      }                                                                                  \
     } else _Pragma("unroll") for (int u = 0; u < 2; ++u) {                               \
       if (DMA) {                                                                         \
         const uint32_t img_ = lds0 + (2 * (SLOT_) + u) * kBufQ;                          \
@@ -612,7 +619,7 @@ __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p,
         so[u] = bload(ro, goo + (qs_ + u * kQT) * son * 2);                              \
       }                                                                                  \
     }                                                                                    \
-    if (tid < 4 * kQT) {                                                                 \
+    if (tid < SUB * 2 * kQT) {                                                           \
       const int q_ = qs_ + (tid >> 6) * kQT + (tid & (kQT - 1));                         \
       sv = q_ < N ? ((tid & kQT) == 0 ? nlse[q_] : ndel[q_]) : 0.f;                      \
     }                                                                                    \
@@ -628,8 +635,8 @@ __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p,
         *(uint4*)(img + 3 * kImgQ + stri) = so[u];                                       \
       }                                                                                  \
     }                                                                                    \
-    if (tid < 4 * kQT)                                                                   \
-      ((float*)((bf16*)(smem + (2 * (SLOT_) + (tid >> 6)) * kBufQ) + 4 * kImgQ))[tid & 63] = sv; \
+    if (tid < SUB * 2 * kQT)                                                             \
+      ((float*)((bf16*)(smem + (SUB * (SLOT_) + (tid >> 6)) * kBufQ) + 4 * kImgQ))[tid & 63] = sv; \
     if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                            \
   }
 
@@ -652,11 +659,12 @@ __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p,
     const int t_ = (T_);                                                                 \
     const bool more_ = t_ + 1 < nstep && !(ABL & 2);                                     \
     if (more_) DKV2_LOAD(t_ + 1, (SLOT_) ^ 1)                                            \
-    _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                      \
+    _Pragma("unroll") for (int u = 0; u < SUB; ++u) {                                    \
       const int qt_ = qt0 + t_ * kStep + u * kQT;                                        \
       if (!(MASK_) || (qt_ < N && (!CAUSAL || qt_ + kQT - 1 >= wk_lo)))                 \
-        dkv_tile<CAUSAL, MASK_, ABL>(smem + (2 * (SLOT_) + u) * kBufQ, c, dK, dV, c2, qt_, \
+        dkv_tile<CAUSAL, MASK_, ABL>(smem + (SUB * (SLOT_) + u) * kBufQ, c, dK, dV, c2, qt_, \
                                      N, my_k, hf);                                       \
+      if (SUB > 2) __builtin_amdgcn_sched_barrier(0);                                    \
     }                                                                                    \
     if (more_) DKV2_STORE((SLOT_) ^ 1)                                                   \
     if (!(ABL & 4)) __syncthreads();                                                     \
@@ -1037,6 +1045,7 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   if (variant == 14) dkv = 5;
   if (variant == 15) { dkv = 0; dq = 8; }   // causal A/B: 128-key dK/dV, 8-wave dQ
   if (variant == 16) { dkv = 4; dq = 8; }   // causal A/B: 4-wave LDS-DMA dK/dV, 8-wave dQ
+  if (variant == 17) { dkv = 17; dq = 8; }  // 8-wave dK/dV with 128-query steps
   if (variant == 12) dq = 12;
   if (variant == 14) dq = (CAUSAL || a.N % 64 != 0) ? 8 : 14;  // pipelined dQ: mask-free shapes
   if (dkv == 11 && (CAUSAL || a.N % 64 != 0)) dkv = 5;  // staggered form: mask-free shapes
@@ -1047,12 +1056,13 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     const int nkb = (a.N + kkb - 1) / kkb;
     const int64_t nblk = (int64_t)nkb * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-    const size_t smem = (dkv == 11 ? 8 : (dkv == 1 || dkv == 13) ? 3 : dkv >= 2 ? 4 : 2) * (size_t)kBufQ;
+    const size_t smem = (dkv == 11 || dkv == 17 ? 8 : (dkv == 1 || dkv == 13) ? 3 : dkv >= 2 ? 4 : 2) * (size_t)kBufQ;
     auto kfn = dkv == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
                : dkv == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
                : dkv == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
                : dkv == 5 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
                : dkv == 11 ? fa_bwd_dkv_bf16_st
+               : dkv == 17 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 0, 4>
 #ifdef MT_DIAGNOSTICS
                : dkv == 6 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 1>
                : dkv == 7 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 2>
