@@ -22,7 +22,7 @@
 namespace mt {
 
 template <typename T, int DT, int KB, bool VEC, bool CAUSAL>
-__global__ __launch_bounds__(256) void fa_fwd_generic(AttnArgs p) {
+__global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
   constexpr int BQ = 128, BK = 32 * KB;
   constexpr int PAD = 16 / sizeof(T);
   constexpr int LD = DT + PAD;
@@ -34,8 +34,15 @@ __global__ __launch_bounds__(256) void fa_fwd_generic(AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
-  const int q0 = blockIdx.x * BQ;
-  const int bh = blockIdx.y, b = bh / p.H, hh = bh % p.H;
+  // XCD-aware block order: the grid is flattened and dealt out so that all query blocks of
+  // one (b,h) run on one XCD and find its K/V in that XCD's L2 (the hardware hands
+  // consecutive workgroups to the 8 XCDs in turn)
+  const int nqb = gridDim.x, nbh = gridDim.y;
+  const int hw = blockIdx.y * nqb + blockIdx.x, nblk = nqb * nbh;
+  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
+  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
+  const int q0 = (logical % nqb) * BQ;
+  const int bh = logical / nqb, b = bh / p.H, hh = bh % p.H;
   const int oc = blockIdx.z * DT;  // first output column of this slice
   const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
   const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
@@ -53,7 +60,31 @@ __global__ __launch_bounds__(256) void fa_fwd_generic(AttnArgs p) {
   const int kend = CAUSAL ? min(N, q0 + BQ) : N;
   const int ntiles = (kend + BK - 1) / BK;
 
+  // One d-chunk with 16-B rows: the K / V tile t + 1 is loaded into registers while tile t
+  // computes and written to LDS after the next barrier, so no global-load latency is exposed
+  // after the first tile. Otherwise: K (per d-chunk), then V, staged in place.
+  const bool pref = VEC && nch == 1;
+  constexpr int EPC = 16 / sizeof(T), CPR = DT / EPC, NCK = BK * CPR / 256;
+  uint4 pk[NCK], pv[NCK];
+  auto pre_load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCK; ++i) {
+      const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC, gr = k0 + r;
+      pk[i] = pv[i] = make_uint4(0, 0, 0, 0);
+      if (gr < N && cc < d) pk[i] = *(const uint4*)(Kg + (int64_t)gr * p.sk[2] + cc);
+      if (gr < N && oc + cc < d) pv[i] = *(const uint4*)(Vg + (int64_t)gr * p.sv[2] + oc + cc);
+    }
+  };
+  auto pre_store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCK; ++i) {
+      const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC;
+      *(uint4*)(sK + r * LD + cc) = pk[i];
+      *(uint4*)(sV + r * LD + cc) = pv[i];
+    }
+  };
   if (nch == 1) stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, 0, d);
+  if (pref) pre_load(0);
 
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * BK;
@@ -63,8 +94,13 @@ __global__ __launch_bounds__(256) void fa_fwd_generic(AttnArgs p) {
     for (int i = 0; i < KB; ++i) S[i] = f32x16{};
     for (int c = 0; c < nch; ++c) {
       __syncthreads();
-      if (nch > 1) stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, c * DT, d);
-      stage_tile<T, BK, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
+      if (pref) {
+        pre_store();
+        if (t + 1 < ntiles) pre_load(k0 + BK);
+      } else {
+        if (nch > 1) stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, c * DT, d);
+        stage_tile<T, BK, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
+      }
       __syncthreads();
       const int ksteps = min(DT, dpad - c * DT) / 16;
       if (active) {
@@ -79,7 +115,7 @@ __global__ __launch_bounds__(256) void fa_fwd_generic(AttnArgs p) {
       }
     }
     // V rows k0.., output columns oc..oc+DT (sV is not read by the QKᵀ phase).
-    stage_tile<T, BK, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, oc, d);
+    if (!pref) stage_tile<T, BK, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, oc, d);
 
     if (active) {
       // Online softmax in the log2 domain; lane (c32, hf) holds 16*KB keys of query my_q.
@@ -112,7 +148,7 @@ __global__ __launch_bounds__(256) void fa_fwd_generic(AttnArgs p) {
 #pragma unroll
       for (int i = 0; i < DT / 32; ++i) O[i] *= alpha;
     }
-    __syncthreads();
+    if (!pref) __syncthreads();  // the V tile staged above
     if (active) {
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
