@@ -22,6 +22,17 @@
 
 namespace mt {
 
+// XCD-aware block order for the (blocks per head, B·H) grids below: the grid's (x, y) is
+// flattened and dealt out so that the blocks of one (b,h) run on one XCD and share its L2.
+__device__ __forceinline__ void xcd_order(int& blk, int& bh) {
+  const int nx = gridDim.x, nblk = gridDim.x * gridDim.y;
+  const int hw = blockIdx.y * nx + blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
+  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
+  blk = logical % nx;
+  bh = logical / nx;
+}
+
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void fa_bwd_prep(AttnArgs p) {
@@ -62,8 +73,10 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
-  const int k0 = blockIdx.x * BKV;
-  const int bh = blockIdx.y, b = bh / p.H, hh = bh % p.H;
+  int kblk, bh;
+  xcd_order(kblk, bh);
+  const int k0 = kblk * BKV;
+  const int b = bh / p.H, hh = bh % p.H;
   const int oc = blockIdx.z * DT;
   const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
   const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
@@ -85,6 +98,43 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
     stage_tile<T, BKV, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, 0, d);
   }
   const int qstart = CAUSAL ? (k0 / BQ) * BQ : 0;
+  // one d-chunk with 16-B rows: the Q / dO tile (and its row constants) of step qt + BQ is
+  // loaded into registers while step qt computes (fa_fwd.hip, same scheme)
+  const bool pref = VEC && nch == 1;
+  constexpr int EPC = 16 / sizeof(T), CPR = DT / EPC, NCK = (BQ * CPR + 255) / 256;
+  uint4 pq[NCK], po[NCK];
+  float pl = 0.f, pd = 0.f;
+  auto pre_load = [&](int qt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCK; ++i) {
+      const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC, gr = qt + r;
+      pq[i] = po[i] = make_uint4(0, 0, 0, 0);
+      if (ch < BQ * CPR && gr < N && cc < d) {
+        pq[i] = *(const uint4*)(Qg + (int64_t)gr * p.sq[2] + cc);
+        po[i] = *(const uint4*)(dOg + (int64_t)gr * p.sdo[2] + cc);
+      }
+    }
+    if (tid < BQ) {
+      const int q = qt + tid;
+      pl = q < N ? lse2[q] : 0.f;
+      pd = q < N ? delta[q] : 0.f;
+    }
+  };
+  auto pre_store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCK; ++i) {
+      const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC;
+      if (ch < BQ * CPR) {
+        *(uint4*)(sQ + r * LD + cc) = pq[i];
+        *(uint4*)(sO + r * LD + cc) = po[i];
+      }
+    }
+    if (tid < BQ) {
+      sLse[tid] = pl;
+      sDel[tid] = pd;
+    }
+  };
+  if (pref && qstart < N) pre_load(qstart);
   for (int qt = qstart; qt < N; qt += BQ) {
     const bool active = !(CAUSAL && qt + BQ - 1 < wave_kmin);
     f32x16 S[QB], dP[QB];
@@ -92,16 +142,21 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
     for (int i = 0; i < QB; ++i) { S[i] = f32x16{}; dP[i] = f32x16{}; }
     for (int c = 0; c < nch; ++c) {
       __syncthreads();
-      if (nch > 1) {
-        stage_tile<T, BKV, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
-        stage_tile<T, BKV, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, c * DT, d);
-      }
-      stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], qt, N, c * DT, d);
-      stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], qt, N, c * DT, d);
-      if (c == 0 && tid < BQ) {
-        const int q = qt + tid;
-        sLse[tid] = q < N ? lse2[q] : 0.f;
-        sDel[tid] = q < N ? delta[q] : 0.f;
+      if (pref) {
+        pre_store();
+        if (qt + BQ < N) pre_load(qt + BQ);
+      } else {
+        if (nch > 1) {
+          stage_tile<T, BKV, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
+          stage_tile<T, BKV, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, c * DT, d);
+        }
+        stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], qt, N, c * DT, d);
+        stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], qt, N, c * DT, d);
+        if (c == 0 && tid < BQ) {
+          const int q = qt + tid;
+          sLse[tid] = q < N ? lse2[q] : 0.f;
+          sDel[tid] = q < N ? delta[q] : 0.f;
+        }
       }
       __syncthreads();
       const int ksteps = min(DT, dpad - c * DT) / 16;
@@ -201,8 +256,10 @@ __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
-  const int q0 = blockIdx.x * BQ;
-  const int bh = blockIdx.y, b = bh / p.H, hh = bh % p.H;
+  int qblk, bh;
+  xcd_order(qblk, bh);
+  const int q0 = qblk * BQ;
+  const int b = bh / p.H, hh = bh % p.H;
   const int oc = blockIdx.z * DT;
   const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
   const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
@@ -224,6 +281,33 @@ __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
     stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], q0, N, 0, d);
   }
   const int kend = CAUSAL ? min(N, q0 + BQ) : N;
+  // one d-chunk with 16-B rows: the K / V tile of step k0 + BK is loaded into registers
+  // while step k0 computes (fa_fwd.hip, same scheme)
+  const bool pref = VEC && nch == 1;
+  constexpr int EPC = 16 / sizeof(T), CPR = DT / EPC, NCK = (BK * CPR + 255) / 256;
+  uint4 pk[NCK], pv[NCK];
+  auto pre_load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCK; ++i) {
+      const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC, gr = k0 + r;
+      pk[i] = pv[i] = make_uint4(0, 0, 0, 0);
+      if (ch < BK * CPR && gr < N && cc < d) {
+        pk[i] = *(const uint4*)(Kg + (int64_t)gr * p.sk[2] + cc);
+        pv[i] = *(const uint4*)(Vg + (int64_t)gr * p.sv[2] + cc);
+      }
+    }
+  };
+  auto pre_store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCK; ++i) {
+      const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC;
+      if (ch < BK * CPR) {
+        *(uint4*)(sK + r * LD + cc) = pk[i];
+        *(uint4*)(sV + r * LD + cc) = pv[i];
+      }
+    }
+  };
+  if (pref && kend > 0) pre_load(0);
   for (int k0 = 0; k0 < kend; k0 += BK) {
     const bool active = !(CAUSAL && k0 > wave_qmax);
     f32x16 S[KB], dP[KB];
@@ -231,12 +315,17 @@ __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
     for (int i = 0; i < KB; ++i) { S[i] = f32x16{}; dP[i] = f32x16{}; }
     for (int c = 0; c < nch; ++c) {
       __syncthreads();
-      if (nch > 1) {
-        stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, c * DT, d);
-        stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], q0, N, c * DT, d);
+      if (pref) {
+        pre_store();
+        if (k0 + BK < kend) pre_load(k0 + BK);
+      } else {
+        if (nch > 1) {
+          stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, c * DT, d);
+          stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], q0, N, c * DT, d);
+        }
+        stage_tile<T, BK, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
+        stage_tile<T, BK, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, c * DT, d);
       }
-      stage_tile<T, BK, DT, 256, VEC>(sK, LD, Kg, p.sk[2], k0, N, c * DT, d);
-      stage_tile<T, BK, DT, 256, VEC>(sV, LD, Vg, p.sv[2], k0, N, c * DT, d);
       __syncthreads();
       const int ksteps = min(DT, dpad - c * DT) / 16;
       if (active) {
