@@ -86,6 +86,9 @@ enum : int {
   // workgroup, non-causal, N % 128 == 0, N >= 256)
   kPolV5Split = 76,
   kPolBwdQ128 = 77,  // 69 with 128-query dK/dV steps (4 sub-tiles per barrier)
+  // v5 with the row sums on the MFMA pipe (ones x Pᵀ) instead of VALU adds: 78 with, 79
+  // without the Vᵀ reuse (which the extra accumulators leave no registers for)
+  kPolV5RowSum = 78, kPolV5RowSumNoKeep = 79,
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -95,7 +98,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -113,7 +116,8 @@ static bool policy_valid(int p) {
 // staggered waves, Vᵀ fragment reuse, exp-to-use distance, DMA from inline asm.
 namespace v5 {
 constexpr int kUnroll = 4, kDma = 1024, kW8 = 2048, kPrio = 4096, kScalar = 8192,
-              kStagger = 16384, kVKeep = 32768, kDefer = 65536, kSplit = 131072, kAsmDma = 524288;
+              kStagger = 16384, kVKeep = 32768, kDefer = 65536, kSplit = 131072, kRowSumMfma = 262144,
+              kAsmDma = 524288;
 constexpr int kDefault = kW8 | kDefer | kVKeep | kDma | kUnroll;
 }  // namespace v5
 
@@ -223,6 +227,8 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
         break;
       case kPolV5AsmDma: var = v5::kDefault | v5::kAsmDma; break;
       case kPolV5Split: var = v5::kDefault | v5::kSplit; break;
+      case kPolV5RowSum: var = v5::kDefault | v5::kRowSumMfma; break;
+      case kPolV5RowSumNoKeep: var = (v5::kDefault | v5::kRowSumMfma) & ~v5::kVKeep; break;
       case kPolDefault:
         // d = 64, N % 64 == 0: v5 with 8 waves, LDS-DMA K/V staging, Vᵀ reuse and the
         // exp-to-use distance (policy 56; A/B history in DESIGN.md §3, profiles/r1_ab_v5_*).

@@ -73,9 +73,11 @@ __device__ __forceinline__ float add1(float a, float b) {
   return r;
 }
 
+// VAR bit 262144 (RS): the row sums come from the MFMA pipe (phase_pv), not from VALU adds.
 template <int VAR>
 __device__ __forceinline__ void sm_pair(const f32x16& s, int i, float c2, float nmc, f32x2& acc,
                                         bf16x8 (&pf)[2]) {
+  constexpr bool RS = (VAR & 262144) != 0;
   const int j = 2 * i;
   if (VAR & 8192) {
     const float e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j], c2, nmc));
@@ -93,7 +95,7 @@ __device__ __forceinline__ void sm_pair(const f32x16& s, int i, float c2, float 
     x = f32x2{s[j], s[j + 1]} * f32x2{c2, c2} + f32x2{nmc, nmc};
   const float e0 = (VAR & 128) ? x[0] : __builtin_amdgcn_exp2f(x[0]);
   const float e1 = (VAR & 128) ? x[1] : __builtin_amdgcn_exp2f(x[1]);
-  if (!(VAR & 256)) acc += f32x2{e0, e1};
+  if (!(VAR & 256) && !RS) acc += f32x2{e0, e1};
   pf[j >> 3][j & 7] = (bf16)e0;
   pf[j >> 3][(j & 7) + 1] = (bf16)e1;
 }
@@ -106,9 +108,10 @@ __device__ __forceinline__ f32x2 sm_exp(const f32x16& s, int i, float c2, float 
   const f32x2 x = f32x2{s[2 * i], s[2 * i + 1]} * f32x2{c2, c2} + f32x2{nmc, nmc};
   return f32x2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
 }
+template <bool RS = false>
 __device__ __forceinline__ void sm_fin(const f32x2& e, int i, f32x2& acc, bf16x8 (&pf)[2]) {
   const int j = 2 * i;
-  acc += e;
+  if (!RS) acc += e;
   pf[j >> 3][j & 7] = (bf16)e[0];
   pf[j >> 3][(j & 7) + 1] = (bf16)e[1];
 }
@@ -144,25 +147,31 @@ __device__ __forceinline__ void phase_qk(const bf16* sk, const int (&ko)[4], con
                                                        0, 0, 0);
     if (SOFT && (VAR & 65536)) {
       const f32x2 e = sm_exp(s_in, i, c2, nmc);
-      if (i) sm_fin(ep, i - 1, acc, pf);
+      if (i) sm_fin<(VAR & 262144) != 0>(ep, i - 1, acc, pf);
       ep = e;
     } else if (SOFT) {
       sm_pair<VAR>(s_in, i, c2, nmc, acc, pf);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (SOFT && (VAR & 65536)) sm_fin(ep, 7, acc, pf);
+  if (SOFT && (VAR & 65536)) sm_fin<(VAR & 262144) != 0>(ep, 7, acc, pf);
 }
 
 // PV phase (8 MFMAs into O with P fragments p_lo (keys 0-31) and p_hi (keys 32-63))
 // interleaved with the softmax of s_in (8 pairs) -> pf.
 // KEEP (VAR bit 32768): 1 = read the Vᵀ fragments and leave them in vk, 2 = take them from
 // vk (P2 and P4 of an iteration multiply the same V(t): the second phase reads no LDS).
+// RS (VAR bit 262144): R += ones·Pᵀ after each P fragment's second PV MFMA (every row of
+// the 32 x 32 R tile is the running row sum of the block's queries, lane = query), so the
+// softmax issues no row-sum adds; R must be given (R_ON) wherever P fragments are consumed.
 template <bool SOFT, int kAhead, int VAR, int KEEP = 0>
 __device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32x16 (&O)[2],
                                          const bf16x8 (&p_lo)[2], const bf16x8 (&p_hi)[2],
                                          const f32x16& s_in, float c2, float nmc, f32x2& acc,
-                                         bf16x8 (&pf)[2], bf16x8 (&vk)[8]) {
+                                         bf16x8 (&pf)[2], bf16x8 (&vk)[8], f32x16* R = nullptr) {
+  constexpr bool RS = (VAR & 262144) != 0;
+  typedef __attribute__((ext_vector_type(8))) short s16x8o;
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, s16x8o{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
   bf16x8 vf_own[8];
   f32x2 ep;
   bf16x8 (&vf)[8] = KEEP ? vk : vf_own;
@@ -175,16 +184,17 @@ __device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32
     if (KEEP != 2 && n + kAhead < 8) vf[n + kAhead] = (VAR & 64) ? p_hi[n & 1] : vread(sv, vo, n + kAhead);
     const bf16x8& p = (n >> 2) ? p_hi[(n >> 1) & 1] : p_lo[(n >> 1) & 1];
     O[n & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[n], p, O[n & 1], 0, 0, 0);
+    if (RS && (n & 1)) *R = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p, *R, 0, 0, 0);
     if (SOFT && (VAR & 65536)) {
       const f32x2 e = sm_exp(s_in, n, c2, nmc);
-      if (n) sm_fin(ep, n - 1, acc, pf);
+      if (n) sm_fin<RS>(ep, n - 1, acc, pf);
       ep = e;
     } else if (SOFT) {
       sm_pair<VAR>(s_in, n, c2, nmc, acc, pf);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (SOFT && (VAR & 65536)) sm_fin(ep, 7, acc, pf);
+  if (SOFT && (VAR & 65536)) sm_fin<RS>(ep, 7, acc, pf);
 }
 
 template <int LPT>
@@ -360,6 +370,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
   const int nbulk = CAUSAL ? (qw < N ? tD + 1 : 0) : ntiles;
 
   f32x16 OA[2], OB[2];
+  f32x16 RA = f32x16{}, RB = f32x16{};  // MFMA row sums (VAR bit 262144)
   bf16x8 vk[8];  // Vᵀ fragments kept from P2 to P4 (VAR bit 32768)
   constexpr int kKeep = (VAR & 32768) ? 1 : 0;
   float mA = -INFINITY, mB = -INFINITY;
@@ -450,13 +461,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
       vo[0] = c.voff[0] + vsl;
       vo[1] = c.voff[1] + vsl;
       phase_qk<true, AHEAD, VAR>(sK, koA, qfA, SA, SB[1], c2, nmcB, accB, pB1);             // P1
-      phase_pv<true, AHEAD, VAR, kKeep>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0, vk);  // P2
+      phase_pv<true, AHEAD, VAR, kKeep>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0, vk, &RB);  // P2
       if (kLate) {
         __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
       }
       phase_qk<true, AHEAD, VAR>(sK, koB, qfB, SB, SA[1], c2, nmcA, accA, pA1);             // P3
-      phase_pv<true, AHEAD, VAR, 2 * kKeep>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0, vk);  // P4
+      phase_pv<true, AHEAD, VAR, 2 * kKeep>(sV, vo, OA, pA0, pA1, SB[0], c2, nmcB, accB, pB0, vk, &RA);  // P4
       if (!(VAR & 8) && !(VAR & 1024)) {
         store5(sK + ((s0 + 2) & 3) * TILE, rK, c.kso);
         store5(sV + ((s0 + 1) & 1) * TILE, rV, c.vso);
@@ -496,15 +507,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
         mask_tri(SA[0]);
         mask_all(SA[1]);
       }
-      phase_pv<true, AHEAD, VAR, kKeep>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0, vk);
+      phase_pv<true, AHEAD, VAR, kKeep>(sV, vo, OB, pB0, pB1, SA[0], c2, nmcA, accA, pA0, vk, &RB);
 #pragma unroll
       for (int i = 0; i < 8; ++i) sm_pair<VAR>(SA[1], i, c2, nmcA, accA, pA1);
       f32x2 d2 = {0.f, 0.f};
       bf16x8 dpf[2];
-      phase_pv<false, AHEAD, VAR, 2 * kKeep>(sV, vo, OA, pA0, pA1, SA[0], c2, 0.f, d2, dpf, vk);
+      phase_pv<false, AHEAD, VAR, 2 * kKeep>(sV, vo, OA, pA0, pA1, SA[0], c2, 0.f, d2, dpf, vk, &RA);
     }
-    pA = accA[0] + accA[1];
-    pB = accB[0] + accB[1];
+    if (VAR & 262144) {  // every lane holds its query's whole sum; lane_pair_sum adds two
+      pA = 0.5f * RA[0];
+      pB = 0.5f * RB[0];
+    } else {
+      pA = accA[0] + accA[1];
+      pB = accB[0] + accB[1];
+    }
   }
   if (CAUSAL) {
     // tail: this wave's share of the staging of the tiles the other waves still need
@@ -571,11 +587,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
         }
         const float nmc = -(m * c2);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm_pair<VAR>(S[0], i, c2, nmc, acc, plo);
+        for (int i = 0; i < 8; ++i) sm_pair<(VAR & ~262144)>(S[0], i, c2, nmc, acc, plo);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm_pair<VAR>(S[1], i, c2, nmc, acc, phi);
+        for (int i = 0; i < 8; ++i) sm_pair<(VAR & ~262144)>(S[1], i, c2, nmc, acc, phi);
         l += acc[0] + acc[1];
-        phase_pv<false, AHEAD, VAR>(sV, vo, O, plo, phi, S[0], c2, 0.f, acc, dpf, vk);
+        phase_pv<false, AHEAD, (VAR & ~262144)>(sV, vo, O, plo, phi, S[0], c2, 0.f, acc, dpf, vk);
       }
     }
   };
@@ -713,6 +729,8 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
           : var == 37892 ? fa_fwd_bf16_v5<2, 37892, false, 8>
           : var == 99332 ? fa_fwd_bf16_v5<2, 99332, false, 8>
           : var == 230404 ? fa_fwd_bf16_v5<2, 230404, false, 8>
+          : var == 361476 ? fa_fwd_bf16_v5<2, 361476, false, 8>
+          : var == 328708 ? fa_fwd_bf16_v5<2, 328708, false, 8>
           : var == 623620 ? fa_fwd_bf16_v5<2, 623620, false, 8>
                         : fa_fwd_bf16_v5<2, 4, false, 8>;
   else if (var == 1028)

@@ -390,7 +390,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # causal heavy + light query-block pairs. Every one computes the same attention.
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
                  44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
-                 67, 68, 76)
+                 67, 68, 76, 78, 79)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
