@@ -106,7 +106,7 @@ static bool policy_valid(int p) {
     if (v == p) return true;
 #ifdef MT_DIAGNOSTICS
   // wrong-result ablations (timing only): v5 80-86 / 97, v4 91-96, fast 10-15, bwd 87-90
-  if ((p >= 80 && p <= 97) || (p >= 10 && p <= 15)) return true;
+  if ((p >= 80 && p <= 98) || (p >= 10 && p <= 15)) return true;
 #endif
   return false;
 }
@@ -251,6 +251,7 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       var = kAbl[pol - 80];
     }
     if (pol == 97) var = 2;  // wrong results: no scale-and-shift
+    if (pol == 98) var = v5::kDefault | 1048576;  // wrong results: 16x16x32 MFMA shape (timing)
     if (pol >= 91 && pol <= 96 && a.d == 64) {
       *handled = true;
       return launch_fwd_v4_ablation(a, pol - 90, st);

@@ -116,6 +116,27 @@ __device__ __forceinline__ void sm_fin(const f32x2& e, int i, f32x2& acc, bf16x8
   pf[j >> 3][(j & 7) + 1] = (bf16)e[1];
 }
 
+// VAR bit 1048576 (diagnostic timing builds only, wrong results): every 32x32x16 MFMA of the
+// two phases replaced by two 16x16x32 MFMAs of the same MACs on half of the accumulator, to
+// price the MFMA shape (MI355X_MICROARCH.md 'DVFS give-back' item 7) under this kernel's
+// VALU and LDS load; the softmax then reads stale registers.
+template <int VAR>
+__device__ __forceinline__ f32x16 mfma_sh(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+#ifdef MT_DIAGNOSTICS
+  if (VAR & 1048576) {
+    typedef __attribute__((ext_vector_type(4))) float f32x4;
+    f32x4 lo = {c[0], c[1], c[2], c[3]}, hi = {c[4], c[5], c[6], c[7]};
+    lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, lo, 0, 0, 0);
+    hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, hi, 0, 0, 0);
+    f32x16 r = c;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+#endif
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ bf16x8 kread(const bf16* sk, const int (&ko)[4], int i) {
   // MFMA i of a QKᵀ phase: key block i/4, k-step i%4 (block 0's chain completes first)
   return *(const bf16x8*)(sk + (i >> 2) * 32 * D + ko[i & 3]);
@@ -143,8 +164,7 @@ __device__ __forceinline__ void phase_qk(const bf16* sk, const int (&ko)[4], con
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     if (i + kAhead < 8) kf[i + kAhead] = kread(sk, ko, i + kAhead);
-    S[i >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i & 3], (i & 3) ? S[i >> 2] : f32x16{},
-                                                       0, 0, 0);
+    S[i >> 2] = mfma_sh<VAR>(kf[i], qf[i & 3], (i & 3) ? S[i >> 2] : f32x16{});
     if (SOFT && (VAR & 65536)) {
       const f32x2 e = sm_exp(s_in, i, c2, nmc);
       if (i) sm_fin<(VAR & 262144) != 0>(ep, i - 1, acc, pf);
@@ -183,7 +203,7 @@ __device__ __forceinline__ void phase_pv(const bf16* sv, const int (&vo)[2], f32
   for (int n = 0; n < 8; ++n) {
     if (KEEP != 2 && n + kAhead < 8) vf[n + kAhead] = (VAR & 64) ? p_hi[n & 1] : vread(sv, vo, n + kAhead);
     const bf16x8& p = (n >> 2) ? p_hi[(n >> 1) & 1] : p_lo[(n >> 1) & 1];
-    O[n & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[n], p, O[n & 1], 0, 0, 0);
+    O[n & 1] = mfma_sh<VAR>(vf[n], p, O[n & 1]);
     if (RS && (n & 1)) *R = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p, *R, 0, 0, 0);
     if (SOFT && (VAR & 65536)) {
       const f32x2 e = sm_exp(s_in, n, c2, nmc);
@@ -250,7 +270,7 @@ __device__ __forceinline__ float lane_pair_sum(float x) {
 template <int AHEAD, int VAR, bool CAUSAL, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, int nqb) {
 #ifndef MT_DIAGNOSTICS
-  static_assert((VAR & (2 | 8 | 16 | 64 | 128 | 256)) == 0,
+  static_assert((VAR & (2 | 8 | 16 | 64 | 128 | 256 | 1048576)) == 0,
                 "wrong-result ablation variants exist only in the MT_DIAGNOSTICS build");
 #endif
   // VAR bit 131072 (8 waves, non-causal, LDS-DMA): split keys inside the workgroup. Waves
@@ -729,6 +749,9 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
           : var == 37892 ? fa_fwd_bf16_v5<2, 37892, false, 8>
           : var == 99332 ? fa_fwd_bf16_v5<2, 99332, false, 8>
           : var == 230404 ? fa_fwd_bf16_v5<2, 230404, false, 8>
+#ifdef MT_DIAGNOSTICS
+          : var == 1147908 ? fa_fwd_bf16_v5<2, 1147908, false, 8>  // MFMA-shape ablation
+#endif
           : var == 361476 ? fa_fwd_bf16_v5<2, 361476, false, 8>
           : var == 328708 ? fa_fwd_bf16_v5<2, 328708, false, 8>
           : var == 623620 ? fa_fwd_bf16_v5<2, 623620, false, 8>
