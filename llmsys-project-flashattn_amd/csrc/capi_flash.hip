@@ -23,6 +23,7 @@ hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStr
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
                          bool* handled);
+hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled);
 hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
                            bool* handled, int pair = 0);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
@@ -89,6 +90,10 @@ enum : int {
   // v5 with the row sums on the MFMA pipe (ones x Pᵀ) instead of VALU adds: 78 with, 79
   // without the Vᵀ reuse (which the extra accumulators leave no registers for)
   kPolV5RowSum = 78, kPolV5RowSumNoKeep = 79,
+  // fa_fwd_v6.hip: v5's non-causal d = 64 schedule on the 16x16x32 MFMA; 102 with the row sums
+  // on the MFMA pipe, 103 = 102 without the Vᵀ reuse
+  kPolV6 = 100, kPolV6RowSum = 102, kPolV6RowSumNoKeep = 103,
+  kPolV6RowSumEven = 104,  // 102 with one exponential per MFMA slot
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -98,15 +103,16 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
   for (int v : kValidPolicies)
     if (v == p) return true;
 #ifdef MT_DIAGNOSTICS
-  // wrong-result ablations (timing only): v5 80-86 / 97, v4 91-96, fast 10-15, bwd 87-90
-  if ((p >= 80 && p <= 98) || (p >= 10 && p <= 15)) return true;
+  // wrong-result ablations (timing only): v5 80-86 / 97 / 98, v4 91-96, fast 10-15, bwd 87-90;
+  // 101 v6 with Q pre-scaled (reduced precision)
+  if ((p >= 80 && p <= 98) || p == 101 || (p >= 10 && p <= 15)) return true;
 #endif
   return false;
 }
@@ -196,6 +202,13 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
                         st, handled);
       break;
     case kPolV5NoUnroll: e = launch_fwd_v5(a, causal, 2, 0, st, handled); break;
+    case kPolV6: e = launch_fwd_v6(a, causal, 0, st, handled); break;
+    case kPolV6RowSum: e = launch_fwd_v6(a, causal, 2, st, handled); break;
+    case kPolV6RowSumNoKeep: e = launch_fwd_v6(a, causal, 6, st, handled); break;
+    case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
+#ifdef MT_DIAGNOSTICS
+    case 101: e = launch_fwd_v6(a, causal, 1, st, handled); break;  // reduced precision (timing)
+#endif
     case kPolV5Causal8: case kPolV5Causal4:
       if (causal)
         e = launch_fwd_v5(a, true, 2, pol == kPolV5Causal8 ? v5::kDefault : v5::kDefault & ~v5::kW8,
@@ -203,6 +216,13 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       break;
     default: break;
   }
+  if (!causal && !*handled && pol == kPolDefault && a.d == 64 &&
+      (int64_t)((N + 511) / 512) * a.B * a.H >= 256)
+    // d = 64 with at least one 8-wave workgroup per CU: v6 (v5's schedule on the 16x16x32
+    // MFMA, which the chip clocks higher) with the row sums on the MFMA pipe (policy 102:
+    // 1129 vs 1089 TF/s for v5 at C3, 1169 vs 1111 at (1,16,8192,64), profiles/r2_ab_v6.txt).
+    // Shapes it does not take (N % 64 != 0, N < 128) fall through to v5 / v4.
+    e = launch_fwd_v6(a, false, 2, st, handled);
   if (!causal && !*handled) {  // non-causal-only v5 forms
     int var = -1, ahead = 2;
     switch (pol) {

@@ -1,0 +1,490 @@
+// FlashAttention forward, bf16 MFMA kernel v6 (d = 64, non-causal, N % 64 == 0): v5's
+// schedule (fa_fwd_v5.hip) on the 16x16x32 MFMA instead of the 32x32x16 one.
+//
+// The two shapes take the same cycles per FLOP, but the chip holds a higher clock on the
+// 16x16x32 loop (MI355X_MICROARCH.md, 'DVFS give-back' item 7); priced under v5's own VALU and
+// LDS load by the diagnostic ablation 98 (profiles/r2_ab_v5_mfma_shape.txt). Everything else
+// is v5's: 8 waves, two 32-query blocks A and B per wave skewed by half a tile, the softmax of
+// one block's 32-key half beside each 16-MFMA phase of the other block, K by LDS-DMA two tiles
+// ahead into a 4-slot ring and V one tile ahead into a 2-slot ring, one barrier per tile, the
+// Vᵀ fragments of P2 kept for P4, exponentials one MFMA slot ahead of their use, the frozen
+// first-tile softmax reference with the serial deferred-max recompute when a lane's row-sum
+// share leaves 2^64, and the XCD-aware block order.
+//
+// Layouts (cdna_hip_programming.md §3, 16x16x32 bf16): lane l, g = l >> 4, i = l & 15.
+//  * Sᵀ(16 keys x 16 queries) = K·Qᵀ: A = K rows (key 16kb + i, d 32ks + 8g ..), B = Q
+//    fragment of query 16qh + i (register resident), C: keys 16kb + 4g + r, query 16qh + i.
+//    A block's 64 x 32 scores are s[kb = 0..3][qh = 0..1] (f32x4): a lane holds 16 keys of
+//    two queries; the four lanes i, i+16, i+32, i+48 share a query.
+//  * Oᵀ(16 d x 16 queries) += Vᵀ·Pᵀ over 32-key halves kk: the B operand of half kk takes
+//    the lane's own eight keys of it in k-slot order (keys 32kk + 4g + 0..3, then
+//    32kk + 16 + 4g + 0..3), and the A operand (two ds_read_b64_tr_b16 of four keys each)
+//    reads Vᵀ in the same key order. C: d 16db + 4g + r, query 16qh + i.
+//  * K image: chunk c of row r at c ^ ((r >> 1) & 7) (conflict-free for the 16-row A reads);
+//    V image: chunk c of row r at c ^ (((r >> 1) & 3) << 1) (conflict-free for the
+//    transposed reads of rows 4g .. 4g + 3 by the 32 lanes of a half-wave).
+#include "fa_fwd_bf16.h"
+
+namespace mt {
+
+namespace {
+
+using namespace fwdbf16;
+constexpr int D = 64;
+constexpr int kBK = 64;
+constexpr int TILE = kBK * D;
+constexpr int kKSlots = 4, kVSlots = 2;
+constexpr int kNW = 8;                    // waves per workgroup
+constexpr int kBQ = 64 * kNW;             // queries per workgroup
+constexpr float kLimit = 1.8446744e19f;   // 2^64
+constexpr float kThr = 8.0f;
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+struct Blk6 {
+  f32x4 s[4][2];  // scores of one 32-query block and 64-key tile: [16-key block kb][query half qh]
+};
+struct Pf6 {
+  bf16x8 p[2];  // Pᵀ B operands of one 32-key half: [query half qh]
+};
+
+__device__ __forceinline__ f32x4 mma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// K fragment f of a tile: 16-key block f >> 1, k-step f & 1 (d 32ks + 8g ..)
+__device__ __forceinline__ bf16x8 kread6(const bf16* sk, const int (&ko)[2], int f) {
+  return *(const bf16x8*)(sk + (f >> 1) * 16 * D + ko[f & 1]);
+}
+
+// Vᵀ fragment f of a tile: key half f >> 2, d block f & 3; keys 4g..4g+3 and 16+4g..16+4g+3
+// of the half (rows), d 16db + i (the lane's A row)
+__device__ __forceinline__ bf16x8 vread6(const bf16* sv, const int (&vo)[4], int f) {
+  const bf16* a1 = sv + (f >> 2) * 32 * D + vo[f & 3];
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1 + 16 * D));
+  const s16x8 av = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, av);
+}
+
+// Softmax pair i (0..7) of half kk of a block: 16-key block 2kk + (i >> 2), query half
+// (i >> 1) & 1, rows 2(i & 1), 2(i & 1) + 1. Exponentials in one MFMA slot, the row-sum add
+// and bf16 pack in the next (no transcendental-to-use stall). PS: the scores already are
+// c2 s - reference (Q pre-scaled, the shift in the MFMA's C operand): no scale-and-shift.
+template <bool PS>
+__device__ __forceinline__ f32x2 sm6_exp(const Blk6& s, int kk, int i, float c2, const float (&nmc)[2]) {
+  const int kbl = i >> 2, qh = (i >> 1) & 1, r0 = 2 * (i & 1);
+  const f32x4& v = s.s[2 * kk + kbl][qh];
+  if (PS) return f32x2{__builtin_amdgcn_exp2f(v[r0]), __builtin_amdgcn_exp2f(v[r0 + 1])};
+  // scalar f32 arithmetic: packed v_pk_fma_f32 / v_pk_add_f32 beside the MFMAs cost issue
+  // cycles the scalar forms do not (MI355X_MICROARCH.md, 'price of one filler')
+  const float x0 = __builtin_fmaf(v[r0], c2, nmc[qh]), x1 = __builtin_fmaf(v[r0 + 1], c2, nmc[qh]);
+  return f32x2{__builtin_amdgcn_exp2f(x0), __builtin_amdgcn_exp2f(x1)};
+}
+// RS: no row-sum adds (the PV phase sums the packed P on the MFMA pipe)
+template <bool RS = false>
+__device__ __forceinline__ void sm6_fin(const f32x2& e, int i, f32x2 (&acc)[2], Pf6& pf) {
+  const int kbl = i >> 2, qh = (i >> 1) & 1, r0 = 2 * (i & 1);
+  if (!RS) {
+    acc[qh][0] += e[0];
+    acc[qh][1] += e[1];
+  }
+  pf.p[qh][4 * kbl + r0] = (bf16)e[0];
+  pf.p[qh][4 * kbl + r0 + 1] = (bf16)e[1];
+}
+
+// The softmax work of MFMA slot m (0..15) of a phase. Default: the two exponentials of pair
+// m / 2 in the even slot, its row-sum adds and bf16 pack in the odd one. EV (with RS only):
+// one exponential per slot, and in odd slots the pack of the previous pair (the last pair is
+// packed after the phase's last MFMA): 12 / 16 cycles of issue per slot instead of 24 / 4.
+template <bool PS, bool RS, bool EV>
+__device__ __forceinline__ void sm6_slot(int m, const Blk6& s_in, int kk, float c2, const float (&nmc)[2],
+                                         f32x2 (&acc)[2], Pf6& pf, f32x2& ep, f32x2& ec) {
+  if (!EV) {
+    if (m & 1) sm6_fin<RS>(ep, m >> 1, acc, pf);
+    else ep = sm6_exp<PS>(s_in, kk, m >> 1, c2, nmc);
+    return;
+  }
+  const int i = m >> 1, j = m & 1, kbl = i >> 2, qh = (i >> 1) & 1, r = 2 * (i & 1) + j;
+  const float v = s_in.s[2 * kk + kbl][qh][r];
+  ec[j] = __builtin_amdgcn_exp2f(PS ? v : __builtin_fmaf(v, c2, nmc[qh]));
+  if (j) {
+    if (i) sm6_fin<true>(ep, i - 1, acc, pf);
+    ep = ec;
+  }
+}
+
+// QKᵀ phase: 16 MFMAs into S (16-key blocks in order, so keys 0-31 finish first), beside the
+// softmax of half kk of s_in. MFMA m: fragment f = m >> 1 (block f >> 1, k-step f & 1),
+// query half m & 1. The chains start from ci[qh] (zero, or the PS shift).
+template <bool SOFT, bool PS, bool RS = false, bool EV = false>
+__device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf16x8 (&qf)[2][2], Blk6& S,
+                                    const f32x4 (&ci)[2], const Blk6& s_in, int kk, float c2,
+                                    const float (&nmc)[2], f32x2 (&acc)[2], Pf6& pf) {
+  bf16x8 kf[8];
+  kf[0] = kread6(sk, ko, 0);
+  kf[1] = kread6(sk, ko, 1);
+  f32x2 ep, ec;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int f = m >> 1, kb = f >> 1, ks = f & 1, qh = m & 1;
+    if (!(m & 1) && f + 2 < 8) kf[f + 2] = kread6(sk, ko, f + 2);
+    S.s[kb][qh] = mma16(kf[f], qf[qh][ks], ks ? S.s[kb][qh] : ci[qh]);
+    if (SOFT) sm6_slot<PS, RS, EV>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (SOFT && EV) sm6_fin<true>(ep, 7, acc, pf);
+}
+
+// PV phase: 16 MFMAs into O with the P operands of halves 0 (plo) and 1 (phi), beside the
+// softmax of half kk of s_in. MFMA m: Vᵀ fragment f = m >> 1 (half f >> 2, d block f & 3),
+// query half m & 1. KEEP: 1 = read the Vᵀ fragments and leave them in vk, 2 = take them
+// from vk (P2 and P4 multiply the same V(t)). RS: R[qh] += ones·Pᵀ right after each P
+// operand's first MFMA (every element of R[qh] is then the running row sum of its query).
+template <bool SOFT, int KEEP, bool PS, bool RS = false, bool EV = false>
+__device__ __forceinline__ void pv6(const bf16* sv, const int (&vo)[4], f32x4 (&O)[4][2], const Pf6& plo,
+                                    const Pf6& phi, const Blk6& s_in, int kk, float c2,
+                                    const float (&nmc)[2], f32x2 (&acc)[2], Pf6& pf, bf16x8 (&vk)[8],
+                                    f32x4 (&R)[2]) {
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, s16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
+  bf16x8 vf_own[8];
+  bf16x8(&vf)[8] = KEEP ? vk : vf_own;
+  if (KEEP != 2) {
+    vf[0] = vread6(sv, vo, 0);
+    vf[1] = vread6(sv, vo, 1);
+  }
+  f32x2 ep, ec;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int f = m >> 1, hv = f >> 2, db = f & 3, qh = m & 1;
+    if (KEEP != 2 && !(m & 1) && f + 2 < 8) vf[f + 2] = vread6(sv, vo, f + 2);
+    O[db][qh] = mma16(vf[f], (hv ? phi : plo).p[qh], O[db][qh]);
+    if (RS && db == 0) R[qh] = mma16(ones, (hv ? phi : plo).p[qh], R[qh]);
+    if (SOFT) sm6_slot<PS, RS, EV>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (SOFT && EV) sm6_fin<true>(ep, 7, acc, pf);
+}
+
+// max over the four lanes that share a query (i, i + 16, i + 32, i + 48)
+__device__ __forceinline__ float quad_max(float x) {
+  x = fmaxf(x, __shfl_xor(x, 16));
+  return fmaxf(x, __shfl_xor(x, 32));
+}
+__device__ __forceinline__ float quad_sum(float x) {
+  x += __shfl_xor(x, 16);
+  return x + __shfl_xor(x, 32);
+}
+// a lane's max over its 16 keys of query half qh
+__device__ __forceinline__ float lane_max6(const Blk6& s, int qh) {
+  float m = fmaxf(fmaxf(s.s[0][qh][0], s.s[0][qh][1]), s.s[0][qh][2]);
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = (kb ? 0 : 3); r < 4; ++r) m = fmaxf(m, s.s[kb][qh][r]);
+  return m;
+}
+
+__device__ __forceinline__ void dma6(bf16* dst_rows, __amdgpu_buffer_rsrc_t rs, int go, int step) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst_rows, 16,
+                                           go + step, 0, 0, 0);
+}
+
+}  // namespace
+
+// PS (policy 101): Q pre-scaled by c2 = log2(e) / sqrt(d) (rounded to bf16 once, in
+// registers) and the frozen reference subtracted through the QKᵀ chains' C operand, so the
+// exponent needs no scale-and-shift (one v_fma_f32 per score fewer). The returned m is the
+// reference / log2(e); the bf16 rounding of c2 Q adds a relative score error of 2^-9, past
+// the (m, l) tolerance of the parity tests, so it exists only in the diagnostics build.
+// RS (VAR 2): row sums on the MFMA pipe (pv6). NK (VAR 4): no Vᵀ reuse (P4 re-reads V).
+// EV (VAR 8, with RS): one exponential per MFMA slot (sm6_slot).
+template <int VAR>
+__global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nqb) {
+  constexpr bool PS = VAR & 1, RS = VAR & 2, EV = RS && (VAR & 8);
+  constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* const sK = (bf16*)smem_raw;      // [kKSlots][TILE]
+  bf16* const sV = sK + kKSlots * TILE;  // [kVSlots][TILE]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int N = p.N;
+
+  const int nblk = gridDim.x, hw = blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
+  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
+  const int bh = logical / nqb, qb = logical % nqb;
+  const int b = bh / p.H, hh = bh % p.H;
+
+  const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const int skn = (int)p.sk[2], svn = (int)p.sv[2];
+  const __amdgpu_buffer_rsrc_t rk =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Kg, (short)0, ((N - 1) * skn + D) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Vg, (short)0, ((N - 1) * svn + D) * 2, 0x00020000);
+
+  int ko[2], vo[4];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) ko[ks] = k_swz<D>(i16, 4 * ks + g);
+  {
+    const int q = i16 >> 2, pp = i16 & 3, row = 4 * g + q;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+      vo[db] = row * D + (((2 * db + (pp >> 1)) ^ (((row >> 1) & 3) << 1)) * 8) + 4 * (pp & 1);
+  }
+  // LDS-DMA: wave w's instruction fills rows 8w .. 8w + 7 of a tile in lane order, so lane
+  // l fetches the source chunk the swizzle puts at chunk l % 8 of row 8w + l / 8
+  int kdo, vdo;
+  {
+    const int dr = 8 * wave + (lane >> 3), dc = lane & 7;
+    kdo = (dr * skn + (dc ^ ((dr >> 1) & 7)) * 8) * 2;
+    vdo = (dr * svn + (dc ^ (((dr >> 1) & 3) << 1)) * 8) * 2;
+  }
+  const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
+  auto dma_k = [&](bf16* sl, int step) __attribute__((always_inline)) { dma6(sl + 8 * wave * D, rk, kdo, step); };
+  auto dma_v = [&](bf16* sl, int step) __attribute__((always_inline)) { dma6(sl + 8 * wave * D, rv, vdo, step); };
+  const float c2 = p.scale_log2;
+
+  const int q0 = qb * kBQ;
+  const int qw = q0 + wave * 64;  // first query of this wave (block A; block B = +32)
+  bf16x8 qfA[2][2], qfB[2][2];    // [qh][ks]
+#pragma unroll
+  for (int qh = 0; qh < 2; ++qh) {
+    const bf16* ra = Qg + (int64_t)min(qw + 16 * qh + i16, N - 1) * p.sq[2];
+    const bf16* rb = Qg + (int64_t)min(qw + 32 + 16 * qh + i16, N - 1) * p.sq[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qfA[qh][ks] = *(const bf16x8*)(ra + 32 * ks + 8 * g);
+      qfB[qh][ks] = *(const bf16x8*)(rb + 32 * ks + 8 * g);
+      if (PS) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          qfA[qh][ks][j] = (bf16)((float)qfA[qh][ks][j] * c2);
+          qfB[qh][ks][j] = (bf16)((float)qfB[qh][ks][j] * c2);
+        }
+      }
+    }
+  }
+  const float c2e = PS ? 1.f : c2;  // the factor from an MFMA score to log2 units
+  const f32x4 ci0[2] = {f32x4{}, f32x4{}};
+  const int ntiles = N / kBK;
+
+  f32x4 OA[4][2], OB[4][2];
+  auto zero_o = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) { OA[db][qh] = f32x4{}; OB[db][qh] = f32x4{}; }
+  };
+  zero_o();
+  float mA[2], mB[2], pA[2], pB[2];  // per query half: reference max, row-sum share
+  bf16x8 vk[8];
+
+  // ---- pass 0: the pipelined loop with the frozen first-tile reference ---------------------
+  dma_k(sK, 0);
+  dma_v(sV, 0);
+  dma_k(sK + TILE, ktile_b);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  {
+    Blk6 SA, SB;
+    {
+      f32x2 dacc[2];
+      Pf6 dpf;
+      const float z[2] = {0.f, 0.f};
+      qk6<false, false>(sK, ko, qfA, SA, ci0, SA, 0, c2, z, dacc, dpf);
+      qk6<false, false>(sK, ko, qfB, SB, ci0, SB, 0, c2, z, dacc, dpf);
+    }
+    float nmcA[2], nmcB[2];
+    f32x4 ciA[2], ciB[2];
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      mA[qh] = quad_max(lane_max6(SA, qh));
+      mB[qh] = quad_max(lane_max6(SB, qh));
+      nmcA[qh] = -(mA[qh] * c2);
+      nmcB[qh] = -(mB[qh] * c2);
+      ciA[qh] = f32x4{-mA[qh], -mA[qh], -mA[qh], -mA[qh]};
+      ciB[qh] = f32x4{-mB[qh], -mB[qh], -mB[qh], -mB[qh]};
+      if (PS) {  // tile 0's scores were computed from zero
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          SA.s[kb][qh] += ciA[qh];
+          SB.s[kb][qh] += ciB[qh];
+        }
+      }
+    }
+    f32x2 accA[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, accB[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+    Pf6 pB0, pB1, pA0, pA1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm6_fin<RS>(sm6_exp<PS>(SB, 0, i, c2, nmcB), i, accB, pB0);
+    f32x4 RA[2] = {f32x4{}, f32x4{}}, RB[2] = {f32x4{}, f32x4{}};
+
+    // iteration t: K(t) in slot t % 4, K(t + 1) in slot (t + 1) % 4, V(t) in slot t % 2;
+    // stages K(t + 2) and V(t + 1). Unrolled by the K ring size (slot offsets immediate).
+    auto iter = [&](int t, int s0) __attribute__((always_inline)) {
+      __builtin_amdgcn_sched_barrier(0);
+      dma_k(sK + ((s0 + 2) & 3) * TILE, (t + 2) * ktile_b);
+      dma_v(sV + ((s0 + 1) & 1) * TILE, (t + 1) * vtile_b);
+      int koA[2], koB[2], vv[4];
+      const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & 1) * TILE;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        koA[ks] = ko[ks] + kslA;
+        koB[ks] = ko[ks] + kslB;
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db) vv[db] = vo[db] + vsl;
+      qk6<true, PS, RS, EV>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
+      pv6<true, K1, PS, RS, EV>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
+      qk6<true, PS, RS, EV>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
+      pv6<true, K2, PS, RS, EV>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    int t = 0;
+    for (; t + 4 < ntiles; t += 4) {
+      iter(t, 0);
+      iter(t + 1, 1);
+      iter(t + 2, 2);
+      iter(t + 3, 3);
+    }
+    for (; t + 1 < ntiles; ++t) iter(t, t & 3);
+    {  // the last tile
+      int koA[2], vv[4];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) koA[ks] = ko[ks] + (t & 3) * TILE;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) vv[db] = vo[db] + (t & 1) * TILE;
+      qk6<true, PS, RS, EV>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
+      pv6<true, K1, PS, RS, EV>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sm6_fin<RS>(sm6_exp<PS>(SA, 1, i, c2, nmcA), i, accA, pA1);
+      f32x2 d2[2];
+      Pf6 dpf;
+      pv6<false, K2, PS, RS>(sV, vv, OA, pA0, pA1, SA, 0, c2, nmcA, d2, dpf, vk, RA);
+    }
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      // RS: every lane holds its query's whole row sum; a quarter each for the epilogue's
+      // sum over the four lanes of a query (exact)
+      pA[qh] = RS ? 0.25f * RA[qh][0] : accA[qh][0] + accA[qh][1];
+      pB[qh] = RS ? 0.25f * RB[qh][0] : accB[qh][0] + accB[qh][1];
+    }
+  }
+
+  // ---- serial path: every tile again with the per-tile deferred-max bookkeeping, when a
+  // lane's row-sum share left 2^64 (the workgroup starts over) -----------------------------
+  const bool bad = !(pA[0] <= kLimit) || !(pA[1] <= kLimit) || !(pB[0] <= kLimit) || !(pB[1] <= kLimit);
+  if (__syncthreads_or(bad)) {
+    zero_o();
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      mA[qh] = mB[qh] = -INFINITY;
+      pA[qh] = pB[qh] = 0.f;
+    }
+    for (int t = 0; t < ntiles; ++t) {
+      __syncthreads();  // every wave is done with the previous tile
+      dma_k(sK, t * ktile_b);
+      dma_v(sV, t * vtile_b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        Blk6 S;
+        f32x2 acc[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+        Pf6 plo, phi, dpf;
+        const float z[2] = {0.f, 0.f};
+        qk6<false, false>(sK, ko, blk ? qfB : qfA, S, ci0, S, 0, c2, z, acc, dpf);
+        float(&m)[2] = blk ? mB : mA;
+        float(&l)[2] = blk ? pB : pA;
+        f32x4(&O)[4][2] = blk ? OB : OA;
+        float nmc[2];
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const float tmax = quad_max(lane_max6(S, qh));
+          if (__builtin_amdgcn_ballot_w64((tmax - m[qh]) * c2e > kThr)) {
+            const float m_new = fmaxf(m[qh], tmax);
+            const float alpha = m[qh] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m[qh] - m_new) * c2e);
+            m[qh] = m_new;
+#pragma unroll
+            for (int db = 0; db < 4; ++db) O[db][qh] *= alpha;
+            l[qh] *= alpha;
+          }
+          nmc[qh] = -(m[qh] * c2e);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm6_fin(sm6_exp<false>(S, 0, i, c2e, nmc), i, acc, plo);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm6_fin(sm6_exp<false>(S, 1, i, c2e, nmc), i, acc, phi);
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) l[qh] += acc[qh][0] + acc[qh][1];
+        f32x2 d2[2];
+        f32x4 dR[2];
+        pv6<false, 0, false>(sV, vo, O, plo, phi, S, 0, c2, nmc, d2, dpf, vk, dR);
+      }
+    }
+  }
+
+  // ---- epilogue ------------------------------------------------------------------------
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int q = qw + 32 * blk + 16 * qh + i16;
+      const float l = quad_sum(blk ? pB[qh] : pA[qh]);
+      const float m = blk ? mB[qh] : mA[qh];
+      const float inv = 1.f / l;
+      const f32x4(&O)[4][2] = blk ? OB : OA;
+      if (q < N) {
+        bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)q * p.so[2];
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+          store4(Og + 16 * db + 4 * g, O[db][qh][0] * inv, O[db][qh][1] * inv, O[db][qh][2] * inv,
+                 O[db][qh][3] * inv, true);
+        if (g == 0) {
+          const int64_t row = (int64_t)bh * N + q;
+          if (p.m) p.m[row] = m * (PS ? p.scale / c2 : p.scale);
+          if (p.l) p.l[row] = l;
+        }
+      }
+    }
+  }
+}
+
+// d = 64, non-causal, N % 64 == 0, N >= 128, every per-head K/V offset (two tiles past N)
+// inside the 31-bit buffer range.
+hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled) {
+  *handled = false;
+  if (causal || a.d != 64 || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
+  const int64_t lim = (int64_t)1 << 31;
+  if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
+    return hipSuccess;
+  *handled = true;
+  const size_t smem = (size_t)(kKSlots + kVSlots) * TILE * sizeof(bf16);
+  void (*kern)(AttnArgs, int) = nullptr;
+  switch (var) {
+    case 0: kern = fa_fwd_bf16_v6<0>; break;
+    case 2: kern = fa_fwd_bf16_v6<2>; break;
+    case 6: kern = fa_fwd_bf16_v6<6>; break;
+    case 10: kern = fa_fwd_bf16_v6<10>; break;
+#ifdef MT_DIAGNOSTICS
+    case 1: kern = fa_fwd_bf16_v6<1>; break;
+#endif
+    default: return hipErrorInvalidValue;
+  }
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (e != hipSuccess) return e;
+  const int nqb = (a.N + kBQ - 1) / kBQ;
+  const int64_t nblk = (int64_t)nqb * a.B * a.H;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64 * kNW), smem, st, a, nqb);
+  return hipGetLastError();
+}
+
+}  // namespace mt

@@ -1,20 +1,22 @@
 # PMC counter passes on the forward kernel (one rocprofv3 --pmc pass per group, kernel
 # trace only: never combined with sys/runtime tracing).
 # Env: POL (kernel policy, default 0), TAG (output tag), CAUSAL=1 for the causal leg,
-#      PMC_GROUPS=all|traffic (traffic = FETCH_SIZE and WRITE_SIZE passes only).
+#      PMC_GROUPS=all|sq|traffic (sq = the three SQ passes, traffic = FETCH_SIZE and WRITE_SIZE).
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 POL=${POL:-0}
 TAG=${TAG:-p$POL}
 EXTRA=""
 [ "${CAUSAL:-0}" = "1" ] && EXTRA="--causal"
-if [ "${PMC_GROUPS:-all}" = "traffic" ]; then
+SQ1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
+SQ2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS"
+SQ3="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM"
+if [ "${PMC_GROUPS:-all}" = "sq" ]; then
+  set -- "$SQ1" "$SQ2" "$SQ3"
+elif [ "${PMC_GROUPS:-all}" = "traffic" ]; then
   set -- "FETCH_SIZE" "WRITE_SIZE"
 else
-  set -- "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-         "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS" \
-         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM" \
-         "FETCH_SIZE" "WRITE_SIZE"
+  set -- "$SQ1" "$SQ2" "$SQ3" "FETCH_SIZE" "WRITE_SIZE"
 fi
 i=0
 for grp in "$@"; do
