@@ -94,6 +94,7 @@ enum : int {
   // on the MFMA pipe, 103 = 102 without the Vᵀ reuse
   kPolV6 = 100, kPolV6RowSum = 102, kPolV6RowSumNoKeep = 103,
   kPolV6RowSumEven = 104,  // 102 with one exponential per MFMA slot
+  kPolV6Split = 105,       // 102 with the keys split between the workgroup halves (v5's 76)
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -103,7 +104,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -206,6 +207,7 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
     case kPolV6RowSum: e = launch_fwd_v6(a, causal, 2, st, handled); break;
     case kPolV6RowSumNoKeep: e = launch_fwd_v6(a, causal, 6, st, handled); break;
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
+    case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
 #ifdef MT_DIAGNOSTICS
     case 101: e = launch_fwd_v6(a, causal, 1, st, handled); break;  // reduced precision (timing)
 #endif
@@ -223,6 +225,13 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
     // 1129 vs 1089 TF/s for v5 at C3, 1169 vs 1111 at (1,16,8192,64), profiles/r2_ab_v6.txt).
     // Shapes it does not take (N % 64 != 0, N < 128) fall through to v5 / v4.
     e = launch_fwd_v6(a, false, 2, st, handled);
+  else if (!causal && !*handled && pol == kPolDefault && a.d == 64 &&
+           (int64_t)((N + 255) / 256) * a.B * a.H >= 256)
+    // fewer 8-wave workgroups than CUs, but at least one per CU once the keys are split
+    // between the workgroup halves (256 queries per workgroup; the 8-GPU strong shard of C3,
+    // (1,16,4096,64)): v6 with split keys, policy 105 (1004 vs 973 TF/s for v5's split;
+    // below one split workgroup per CU v5's split stays ahead by 8 %, r2_ab_v6.txt).
+    e = launch_fwd_v6(a, false, 18, st, handled);
   if (!causal && !*handled) {  // non-causal-only v5 forms
     int var = -1, ahead = 2;
     switch (pol) {

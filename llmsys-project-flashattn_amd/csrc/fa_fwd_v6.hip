@@ -202,17 +202,28 @@ __device__ __forceinline__ void dma6(bf16* dst_rows, __amdgpu_buffer_rsrc_t rs, 
 // the (m, l) tolerance of the parity tests, so it exists only in the diagnostics build.
 // RS (VAR 2): row sums on the MFMA pipe (pv6). NK (VAR 4): no Vᵀ reuse (P4 re-reads V).
 // EV (VAR 8, with RS): one exponential per MFMA slot (sm6_slot).
+// SPLIT (VAR 16): the keys split between the two halves of the workgroup (v5's VAR 131072):
+// waves w and w + 4 take the same 64 queries over the first and the second half of the keys,
+// each half with its own K/V rings and staging under the same barriers; the second half
+// hands (m, row-sum share, O) to the first through LDS at the end. 256 queries per
+// workgroup, for grids with fewer 8-wave workgroups than CUs.
 template <int VAR>
 __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nqb) {
-  constexpr bool PS = VAR & 1, RS = VAR & 2, EV = RS && (VAR & 8);
+  constexpr bool PS = VAR & 1, RS = VAR & 2, EV = RS && (VAR & 8), SPLIT = VAR & 16;
   constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
+  constexpr int NWQ = SPLIT ? 4 : kNW;  // waves sharing one query block and its key tiles
+  constexpr int LPT = kNW / NWQ;        // LDS-DMA instructions per wave per tile
+  constexpr int BQ = 64 * NWQ;          // queries per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  bf16* const sK = (bf16*)smem_raw;      // [kKSlots][TILE]
-  bf16* const sV = sK + kKSlots * TILE;  // [kVSlots][TILE]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
   const int N = p.N;
+  const int half = SPLIT ? (__builtin_amdgcn_readfirstlane(wave) >> 2) : 0;
+  const int wq = SPLIT ? (wave & 3) : wave;  // this wave's 64 queries within the block
+  const int Nk = SPLIT ? N / 2 : N;          // keys this wave's half walks
+  bf16* const sK = (bf16*)smem_raw + half * (kKSlots + kVSlots) * TILE;  // [kKSlots][TILE]
+  bf16* const sV = sK + kKSlots * TILE;                                  // [kVSlots][TILE]
 
   const int nblk = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
@@ -221,13 +232,13 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   const int b = bh / p.H, hh = bh % p.H;
 
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
-  const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
-  const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const bf16* Kg = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1] + (int64_t)half * Nk * p.sk[2];
+  const bf16* Vg = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1] + (int64_t)half * Nk * p.sv[2];
   const int skn = (int)p.sk[2], svn = (int)p.sv[2];
   const __amdgpu_buffer_rsrc_t rk =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Kg, (short)0, ((N - 1) * skn + D) * 2, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)Kg, (short)0, ((Nk - 1) * skn + D) * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rv =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Vg, (short)0, ((N - 1) * svn + D) * 2, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)Vg, (short)0, ((Nk - 1) * svn + D) * 2, 0x00020000);
 
   int ko[2], vo[4];
 #pragma unroll
@@ -238,21 +249,29 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     for (int db = 0; db < 4; ++db)
       vo[db] = row * D + (((2 * db + (pp >> 1)) ^ (((row >> 1) & 3) << 1)) * 8) + 4 * (pp & 1);
   }
-  // LDS-DMA: wave w's instruction fills rows 8w .. 8w + 7 of a tile in lane order, so lane
-  // l fetches the source chunk the swizzle puts at chunk l % 8 of row 8w + l / 8
-  int kdo, vdo;
-  {
-    const int dr = 8 * wave + (lane >> 3), dc = lane & 7;
-    kdo = (dr * skn + (dc ^ ((dr >> 1) & 7)) * 8) * 2;
-    vdo = (dr * svn + (dc ^ (((dr >> 1) & 3) << 1)) * 8) * 2;
+  // LDS-DMA: instruction i of wave w fills rows 8 (LPT w + i) .. + 7 of a tile in lane
+  // order, so lane l fetches the source chunk the swizzle puts at chunk l % 8 of row
+  // 8 (LPT w + i) + l / 8
+  int kdo[LPT], vdo[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int dr = 8 * (LPT * wq + i) + (lane >> 3), dc = lane & 7;
+    kdo[i] = (dr * skn + (dc ^ ((dr >> 1) & 7)) * 8) * 2;
+    vdo[i] = (dr * svn + (dc ^ (((dr >> 1) & 3) << 1)) * 8) * 2;
   }
   const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
-  auto dma_k = [&](bf16* sl, int step) __attribute__((always_inline)) { dma6(sl + 8 * wave * D, rk, kdo, step); };
-  auto dma_v = [&](bf16* sl, int step) __attribute__((always_inline)) { dma6(sl + 8 * wave * D, rv, vdo, step); };
+  auto dma_k = [&](bf16* sl, int step) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) dma6(sl + 8 * (LPT * wq + i) * D, rk, kdo[i], step);
+  };
+  auto dma_v = [&](bf16* sl, int step) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) dma6(sl + 8 * (LPT * wq + i) * D, rv, vdo[i], step);
+  };
   const float c2 = p.scale_log2;
 
-  const int q0 = qb * kBQ;
-  const int qw = q0 + wave * 64;  // first query of this wave (block A; block B = +32)
+  const int q0 = qb * BQ;
+  const int qw = q0 + wq * 64;  // first query of this wave (block A; block B = +32)
   bf16x8 qfA[2][2], qfB[2][2];    // [qh][ks]
 #pragma unroll
   for (int qh = 0; qh < 2; ++qh) {
@@ -273,7 +292,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   }
   const float c2e = PS ? 1.f : c2;  // the factor from an MFMA score to log2 units
   const f32x4 ci0[2] = {f32x4{}, f32x4{}};
-  const int ntiles = N / kBK;
+  const int ntiles = Nk / kBK;
 
   f32x4 OA[4][2], OB[4][2];
   auto zero_o = [&]() __attribute__((always_inline)) {
@@ -431,6 +450,44 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     }
   }
 
+  if (SPLIT) {  // merge the second half's (m, row-sum share, O) into the first half's
+    __syncthreads();  // every wave is done with its half's LDS tiles
+    float4* xch = (float4*)smem_raw + wq * 18 * 64 + lane;
+    if (half) {
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const f32x4 a = OA[db][qh], o = OB[db][qh];
+          xch[(2 * db + qh) * 64] = make_float4(a[0], a[1], a[2], a[3]);
+          xch[(8 + 2 * db + qh) * 64] = make_float4(o[0], o[1], o[2], o[3]);
+        }
+      xch[16 * 64] = make_float4(mA[0], mA[1], mB[0], mB[1]);
+      xch[17 * 64] = make_float4(pA[0], pA[1], pB[0], pB[1]);
+    }
+    __syncthreads();
+    if (half) return;
+    const float4 tm = xch[16 * 64], tp = xch[17 * 64];
+    const float om[4] = {tm.x, tm.y, tm.z, tm.w}, op[4] = {tp.x, tp.y, tp.z, tp.w};
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        float& m = blk ? mB[qh] : mA[qh];
+        float& l = blk ? pB[qh] : pA[qh];
+        const float n = fmaxf(m, om[2 * blk + qh]);
+        const float a0 = __builtin_amdgcn_exp2f((m - n) * c2e), a1 = __builtin_amdgcn_exp2f((om[2 * blk + qh] - n) * c2e);
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const float4 u = xch[((blk ? 8 : 0) + 2 * db + qh) * 64];
+          f32x4& o = (blk ? OB : OA)[db][qh];
+          o = o * a0 + f32x4{u.x, u.y, u.z, u.w} * a1;
+        }
+        l = l * a0 + op[2 * blk + qh] * a1;
+        m = n;
+      }
+  }
+
   // ---- epilogue ------------------------------------------------------------------------
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
@@ -457,22 +514,26 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   }
 }
 
-// d = 64, non-causal, N % 64 == 0, N >= 128, every per-head K/V offset (two tiles past N)
-// inside the 31-bit buffer range.
+// d = 64, non-causal, N % 64 == 0, N >= 128 (split keys: N % 128 == 0, N >= 256, so each
+// half walks two whole tiles or more), every per-head K/V offset (two tiles past N) inside
+// the 31-bit buffer range.
 hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled) {
   *handled = false;
+  const bool split = (var & 16) != 0;
   if (causal || a.d != 64 || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
+  if (split && (a.N % (2 * kBK) != 0 || a.N < 4 * kBK)) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
-  const size_t smem = (size_t)(kKSlots + kVSlots) * TILE * sizeof(bf16);
+  const size_t smem = (size_t)(split ? 2 : 1) * (kKSlots + kVSlots) * TILE * sizeof(bf16);
   void (*kern)(AttnArgs, int) = nullptr;
   switch (var) {
     case 0: kern = fa_fwd_bf16_v6<0>; break;
     case 2: kern = fa_fwd_bf16_v6<2>; break;
     case 6: kern = fa_fwd_bf16_v6<6>; break;
     case 10: kern = fa_fwd_bf16_v6<10>; break;
+    case 18: kern = fa_fwd_bf16_v6<18>; break;
 #ifdef MT_DIAGNOSTICS
     case 1: kern = fa_fwd_bf16_v6<1>; break;
 #endif
@@ -480,7 +541,8 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   }
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
-  const int nqb = (a.N + kBQ - 1) / kBQ;
+  const int bq = split ? kBQ / 2 : kBQ;
+  const int nqb = (a.N + bq - 1) / bq;
   const int64_t nblk = (int64_t)nqb * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64 * kNW), smem, st, a, nqb);

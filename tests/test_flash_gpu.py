@@ -305,7 +305,7 @@ def test_v5_causal_pairs_vs_oracle(torch_dev, policy, parity_record):
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
-@pytest.mark.parametrize("policy", [0, 76, 100, 102, 103])
+@pytest.mark.parametrize("policy", [0, 76, 100, 102, 103, 105])
 def test_v5_split_keys_vs_oracle(torch_dev, policy, parity_record):
     """v5 with the keys split between the two halves of an 8-wave workgroup (policy 76; the
     default for grids of fewer 8-wave workgroups than CUs): every head, every row against
@@ -395,7 +395,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # causal heavy + light query-block pairs, 100 v6. Every one computes the same attention.
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
                  44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
-                 67, 68, 76, 78, 79, 100, 102, 103)
+                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
