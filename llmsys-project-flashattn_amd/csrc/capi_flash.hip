@@ -95,6 +95,7 @@ enum : int {
   kPolV6 = 100, kPolV6RowSum = 102, kPolV6RowSumNoKeep = 103,
   kPolV6RowSumEven = 104,  // 102 with one exponential per MFMA slot
   kPolV6Split = 105,       // 102 with the keys split between the workgroup halves (v5's 76)
+  kPolV6Causal = 106,      // 102's causal form (v5's paired causal schedule, policy 67)
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -104,7 +105,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -208,6 +209,9 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
     case kPolV6RowSumNoKeep: e = launch_fwd_v6(a, causal, 6, st, handled); break;
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
     case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
+    case kPolV6Causal:
+      if (causal) e = launch_fwd_v6(a, true, 34, st, handled);
+      break;
 #ifdef MT_DIAGNOSTICS
     case 101: e = launch_fwd_v6(a, causal, 1, st, handled); break;  // reduced precision (timing)
 #endif
@@ -294,7 +298,13 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
     // query blocks and each wave's masked diagonal tile inside its pipelined loop (982 vs
     // 819 TF/s for v4 at C3 causal, 1072 vs 916 at (1,16,16384,64); with fewer workgroups
     // than CUs v4's 256-query blocks fill the chip better: profiles/r2_ab_causal_v5.txt).
-    e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
+    // Since round 2l the same schedule on v6 (16x16x32 MFMA, row sums on the MFMA pipe,
+    // policy 106): 1137 vs 1084 TF/s at (1,16,16384,64), even at C3 causal (980 vs 981,
+    // profiles/r2_ab_v6.txt); v5 stays for the shapes v6 does not take.
+  {
+    e = launch_fwd_v6(a, true, 34, st, handled);
+    if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
+  }
   if (!*handled && pol == kPolDefault && a.d == 64)
     // causal, ragged N or short N: v4. Causal pairs a heavy and a light query block per
     // workgroup, light block first (860 vs 806 TF/s unpaired at C3; 4 waves below

@@ -202,6 +202,8 @@ __device__ __forceinline__ void dma6(bf16* dst_rows, __amdgpu_buffer_rsrc_t rs, 
 // the (m, l) tolerance of the parity tests, so it exists only in the diagnostics build.
 // RS (VAR 2): row sums on the MFMA pipe (pv6). NK (VAR 4): no Vᵀ reuse (P4 re-reads V).
 // EV (VAR 8, with RS): one exponential per MFMA slot (sm6_slot).
+// CAUSAL (VAR 32): v5's causal schedule (paired light / heavy query blocks, each wave's
+// masked diagonal tile peeled from its own pipelined loop, finished waves keep staging).
 // SPLIT (VAR 16): the keys split between the two halves of the workgroup (v5's VAR 131072):
 // waves w and w + 4 take the same 64 queries over the first and the second half of the keys,
 // each half with its own K/V rings and staging under the same barriers; the second half
@@ -209,17 +211,19 @@ __device__ __forceinline__ void dma6(bf16* dst_rows, __amdgpu_buffer_rsrc_t rs, 
 // workgroup, for grids with fewer 8-wave workgroups than CUs.
 template <int VAR>
 __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nqb) {
-  constexpr bool PS = VAR & 1, RS = VAR & 2, EV = RS && (VAR & 8), SPLIT = VAR & 16;
+  constexpr bool PS = VAR & 1, RS = VAR & 2, EV = RS && (VAR & 8), SPLIT = VAR & 16, CAUSAL = VAR & 32;
+  static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
   constexpr int NWQ = SPLIT ? 4 : kNW;  // waves sharing one query block and its key tiles
   constexpr int LPT = kNW / NWQ;        // LDS-DMA instructions per wave per tile
   constexpr int BQ = 64 * NWQ;          // queries per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int g = lane >> 4, i16 = lane & 15;
   const int N = p.N;
-  const int half = SPLIT ? (__builtin_amdgcn_readfirstlane(wave) >> 2) : 0;
+  const int half = SPLIT ? (wave >> 2) : 0;
   const int wq = SPLIT ? (wave & 3) : wave;  // this wave's 64 queries within the block
   const int Nk = SPLIT ? N / 2 : N;          // keys this wave's half walks
   bf16* const sK = (bf16*)smem_raw + half * (kKSlots + kVSlots) * TILE;  // [kKSlots][TILE]
@@ -228,7 +232,12 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   const int nblk = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
   const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  const int bh = logical / nqb, qb = logical % nqb;
+  // Non-causal: one query block per workgroup. Causal: a pair of query blocks of one head,
+  // the light block u first, then the heavy block nqb - 1 - u (every workgroup walks about
+  // nqb + 1 blocks' worth of key tiles; the heavy block finds the light block's tiles still
+  // in the XCD's L2).
+  const int nunit = CAUSAL ? (nqb + 1) / 2 : nqb;
+  const int bh = logical / nunit, qb = logical % nunit;
   const int b = bh / p.H, hh = bh % p.H;
 
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
@@ -270,9 +279,10 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   };
   const float c2 = p.scale_log2;
 
-  const int q0 = qb * BQ;
+  // One query block [q0, q0 + BQ) of head bh.
+  auto run_block = [&](const int q0) __attribute__((always_inline)) {
   const int qw = q0 + wq * 64;  // first query of this wave (block A; block B = +32)
-  bf16x8 qfA[2][2], qfB[2][2];    // [qh][ks]
+  bf16x8 qfA[2][2], qfB[2][2];  // [qh][ks]
 #pragma unroll
   for (int qh = 0; qh < 2; ++qh) {
     const bf16* ra = Qg + (int64_t)min(qw + 16 * qh + i16, N - 1) * p.sq[2];
@@ -292,7 +302,14 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   }
   const float c2e = PS ? 1.f : c2;  // the factor from an MFMA score to log2 units
   const f32x4 ci0[2] = {f32x4{}, f32x4{}};
-  const int ntiles = Nk / kBK;
+  // Tiles the workgroup stages: non-causal all Nk / 64; causal the keys below its last
+  // query. Tiles this wave computes: non-causal all; causal [0, tD] with tD = qw / 64 its
+  // diagonal tile (the last, masked; none when the wave's queries are past N). A causal wave
+  // that is done keeps staging its share of the later tiles and joins every barrier (the
+  // tail loop), so all waves of the workgroup take the same barriers.
+  const int ntiles = CAUSAL ? min(N, q0 + BQ) / kBK : Nk / kBK;
+  const int tD = qw / kBK;
+  const int nbulk = CAUSAL ? (qw < N ? tD + 1 : 0) : ntiles;
 
   f32x4 OA[4][2], OB[4][2];
   auto zero_o = [&]() __attribute__((always_inline)) {
@@ -302,16 +319,30 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       for (int qh = 0; qh < 2; ++qh) { OA[db][qh] = f32x4{}; OB[db][qh] = f32x4{}; }
   };
   zero_o();
-  float mA[2], mB[2], pA[2], pB[2];  // per query half: reference max, row-sum share
+  // per query half: reference max, row-sum share
+  float mA[2] = {0.f, 0.f}, mB[2] = {0.f, 0.f}, pA[2] = {0.f, 0.f}, pB[2] = {0.f, 0.f};
   bf16x8 vk[8];
+  // causal: the wave's diagonal tile holds keys qw .. qw + 63; key 16 kb + 4 g + r of it is
+  // above query lq0 + 16 qh + i16 of the wave (lq0 = 0 for block A, 32 for block B) when
+  // larger
+  auto mask_diag = [&](Blk6& S, int lq0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * kb + 4 * g + r > lq0 + 16 * qh + i16) S.s[kb][qh][r] = -INFINITY;
+  };
 
-  // ---- pass 0: the pipelined loop with the frozen first-tile reference ---------------------
+  // ---- pass 0: the pipelined loop with the frozen first-tile reference over the tiles
+  //      [0, nbulk); causal: its last tile is the wave's masked diagonal --------------------
   dma_k(sK, 0);
   dma_v(sV, 0);
   dma_k(sK + TILE, ktile_b);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  {
+  if (nbulk >= 1) {  // non-causal: the launcher guarantees N >= 128
     Blk6 SA, SB;
     {
       f32x2 dacc[2];
@@ -319,6 +350,10 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       const float z[2] = {0.f, 0.f};
       qk6<false, false>(sK, ko, qfA, SA, ci0, SA, 0, c2, z, dacc, dpf);
       qk6<false, false>(sK, ko, qfB, SB, ci0, SB, 0, c2, z, dacc, dpf);
+    }
+    if (CAUSAL && tD == 0) {  // tile 0 is this wave's diagonal: reference over visible keys
+      mask_diag(SA, 0);
+      mask_diag(SB, 32);
     }
     float nmcA[2], nmcB[2];
     f32x4 ciA[2], ciB[2];
@@ -367,20 +402,22 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       __syncthreads();
     };
     int t = 0;
-    for (; t + 4 < ntiles; t += 4) {
+    for (; t + 4 < nbulk; t += 4) {
       iter(t, 0);
       iter(t + 1, 1);
       iter(t + 2, 2);
       iter(t + 3, 3);
     }
-    for (; t + 1 < ntiles; ++t) iter(t, t & 3);
-    {  // the last tile
+    for (; t + 1 < nbulk; ++t) iter(t, t & 3);
+    {  // the last tile (causal: the wave's diagonal)
       int koA[2], vv[4];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) koA[ks] = ko[ks] + (t & 3) * TILE;
 #pragma unroll
       for (int db = 0; db < 4; ++db) vv[db] = vo[db] + (t & 1) * TILE;
+      if (CAUSAL) mask_diag(SB, 32);  // S_B(tD): keys 32-63 are block B's diagonal
       qk6<true, PS, RS, EV>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
+      if (CAUSAL) mask_diag(SA, 0);  // S_A(tD): keys 0-31 its diagonal, 32-63 above it
       pv6<true, K1, PS, RS, EV>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);
 #pragma unroll
       for (int i = 0; i < 8; ++i) sm6_fin<RS>(sm6_exp<PS>(SA, 1, i, c2, nmcA), i, accA, pA1);
@@ -394,6 +431,15 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       // sum over the four lanes of a query (exact)
       pA[qh] = RS ? 0.25f * RA[qh][0] : accA[qh][0] + accA[qh][1];
       pB[qh] = RS ? 0.25f * RB[qh][0] : accB[qh][0] + accB[qh][1];
+    }
+  }
+  if (CAUSAL) {
+    // tail: this wave's share of the staging of the tiles the other waves still need
+    for (int t = nbulk > 0 ? nbulk - 1 : 0; t + 1 < ntiles; ++t) {
+      dma_k(sK + ((t + 2) & 3) * TILE, (t + 2) * ktile_b);
+      dma_v(sV + ((t + 1) & 1) * TILE, (t + 1) * vtile_b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
   }
 
@@ -415,11 +461,22 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       __syncthreads();
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk) {
+        const int qf0 = qw + 32 * blk;  // the block's first query (wave-uniform)
+        if (CAUSAL && (qf0 + 31 < t * kBK || qf0 >= N)) continue;  // all masked / past N
         Blk6 S;
         f32x2 acc[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
         Pf6 plo, phi, dpf;
         const float z[2] = {0.f, 0.f};
         qk6<false, false>(sK, ko, blk ? qfB : qfA, S, ci0, S, 0, c2, z, acc, dpf);
+        if (CAUSAL && t * kBK + kBK - 1 > qf0) {
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (t * kBK + 16 * kb + 4 * g + r > qf0 + 16 * qh + i16) S.s[kb][qh][r] = -INFINITY;
+        }
         float(&m)[2] = blk ? mB : mA;
         float(&l)[2] = blk ? pB : pA;
         f32x4(&O)[4][2] = blk ? OB : OA;
@@ -449,7 +506,6 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       }
     }
   }
-
   if (SPLIT) {  // merge the second half's (m, row-sum share, O) into the first half's
     __syncthreads();  // every wave is done with its half's LDS tiles
     float4* xch = (float4*)smem_raw + wq * 18 * 64 + lane;
@@ -466,7 +522,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       xch[17 * 64] = make_float4(pA[0], pA[1], pB[0], pB[1]);
     }
     __syncthreads();
-    if (half) return;
+    if (half) return;  // (non-causal only: one block per workgroup)
     const float4 tm = xch[16 * 64], tp = xch[17 * 64];
     const float om[4] = {tm.x, tm.y, tm.z, tm.w}, op[4] = {tp.x, tp.y, tp.z, tp.w};
 #pragma unroll
@@ -512,15 +568,27 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       }
     }
   }
+  };  // run_block
+
+  if (CAUSAL) {  // the light query block first, then the heavy one of the same head
+    const int heavy = nqb - 1 - qb;
+    run_block(qb * BQ);
+    if (heavy != qb) {
+      __syncthreads();  // every wave is done with the light block's LDS tiles
+      run_block(heavy * BQ);
+    }
+  } else {
+    run_block(qb * BQ);
+  }
 }
 
-// d = 64, non-causal, N % 64 == 0, N >= 128 (split keys: N % 128 == 0, N >= 256, so each
+// d = 64, N % 64 == 0, N >= 128, causal only with VAR 32 (split keys: N % 128 == 0, N >= 256, so each
 // half walks two whole tiles or more), every per-head K/V offset (two tiles past N) inside
 // the 31-bit buffer range.
 hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled) {
   *handled = false;
   const bool split = (var & 16) != 0;
-  if (causal || a.d != 64 || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
+  if (causal != ((var & 32) != 0) || a.d != 64 || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
   if (split && (a.N % (2 * kBK) != 0 || a.N < 4 * kBK)) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
@@ -534,6 +602,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 6: kern = fa_fwd_bf16_v6<6>; break;
     case 10: kern = fa_fwd_bf16_v6<10>; break;
     case 18: kern = fa_fwd_bf16_v6<18>; break;
+    case 34: kern = fa_fwd_bf16_v6<34>; break;
 #ifdef MT_DIAGNOSTICS
     case 1: kern = fa_fwd_bf16_v6<1>; break;
 #endif
@@ -543,7 +612,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   if (e != hipSuccess) return e;
   const int bq = split ? kBQ / 2 : kBQ;
   const int nqb = (a.N + bq - 1) / bq;
-  const int64_t nblk = (int64_t)nqb * a.B * a.H;
+  const int64_t nblk = (int64_t)(causal ? (nqb + 1) / 2 : nqb) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64 * kNW), smem, st, a, nqb);
   return hipGetLastError();

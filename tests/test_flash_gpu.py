@@ -271,7 +271,7 @@ def test_long_causal_paired_default(torch_dev, d):
     _subset_check_fwd(torch, q, k, v, o, True, [(0, 0), (0, 2)], 1e-3, 2.0 ** -7)
 
 
-@pytest.mark.parametrize("policy", [0, 67, 68])
+@pytest.mark.parametrize("policy", [0, 67, 68, 106])
 def test_v5_causal_pairs_vs_oracle(torch_dev, policy, parity_record):
     """The v5 causal form (paired light/heavy query blocks per workgroup, each wave's
     pipelined loop ending on its own masked diagonal tile, finished waves staging for the
@@ -395,7 +395,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # causal heavy + light query-block pairs, 100 v6. Every one computes the same attention.
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
                  44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
-                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105)
+                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106)
 
 
 @pytest.mark.parametrize("policy", FAST_POLICIES)
