@@ -17,9 +17,14 @@
 //    second time inside the backward, :229/:310; this is the exact gradient of the forward.)
 //
 // MI355X design: one wave64 per row with butterfly reductions (no cub/cooperative-group
-// dependency), grid-stride over rows, 16-B vector loads when the row length allows, and a
-// deterministic two-stage column reduction for dγ/dβ (per-block partials in a caller-given
-// workspace, then one pass) instead of atomics.
+// dependency), grid-stride over rows, and a deterministic two-stage column reduction for
+// dγ/dβ (per-block partials in a caller-given workspace, then one pass) instead of atomics.
+// These kernels are HBM-bound, so each row is read from HBM exactly once: when the row
+// length is a multiple of 4 and at most 4096, a lane keeps its 16-B pieces of the row in
+// registers (NV float4 per lane, templated) between the reduction and the output pass
+// (softmax fw/bw, LayerNorm fw, LayerNorm bw dx), and the LayerNorm backward computes dx and
+// its rows' dγ/dβ partials in one pass for hidden <= 1024. Other shapes take the scalar
+// kernels, which re-read the row (from L2 in practice).
 #include <stdio.h>
 #include <string.h>
 
@@ -215,6 +220,255 @@ __global__ __launch_bounds__(256) void ln_bw_dgb_final(float* dgamma, float* dbe
 
 static int64_t ln_chunks(int64_t rows) { return (rows + kLnRowsPerChunk - 1) / kLnRowsPerChunk; }
 
+// ---------------------------------------------------- register-resident row kernels (NV)
+// Lane l owns the float4 pieces at columns 4 (l + 64 k), k < NV, of its wave's row; pieces
+// past the row length are never read or written (len % 4 == 0, so a piece is all in or out).
+template <int NV>
+__global__ __launch_bounds__(256) void softmax_fw_vec(SoftmaxArgs a, int mvec) {
+  const int lane = threadIdx.x & 63;
+  const int64_t rows = a.B * a.nh * a.from;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    const int64_t i = r % a.from, bh = r / a.from, h = bh % a.nh, b = bh / a.nh;
+    const float* x = a.inp + r * a.to;
+    const float* mrow = a.mask ? a.mask + b * a.ms[0] + h * a.ms[1] + i * a.ms[2] : nullptr;
+    float4 v[NV];
+    float mx = kMaskedLogit;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (lane + 64 * k);
+      if (c < a.to) {
+        v[k] = *(const float4*)(x + c);
+        if (mrow) {
+          if (mvec) {
+            const float4 m = *(const float4*)(mrow + c);
+            v[k].x += m.x; v[k].y += m.y; v[k].z += m.z; v[k].w += m.w;
+          } else {
+            v[k].x += mrow[c * a.ms[3]];
+            v[k].y += mrow[(c + 1) * a.ms[3]];
+            v[k].z += mrow[(c + 2) * a.ms[3]];
+            v[k].w += mrow[(c + 3) * a.ms[3]];
+          }
+        }
+        if (a.mask_future) {
+          if (c > i) v[k].x = kMaskedLogit;
+          if (c + 1 > i) v[k].y = kMaskedLogit;
+          if (c + 2 > i) v[k].z = kMaskedLogit;
+          if (c + 3 > i) v[k].w = kMaskedLogit;
+        }
+        mx = fmaxf(mx, fmaxf(fmaxf(v[k].x, v[k].y), fmaxf(v[k].z, v[k].w)));
+      }
+    }
+    mx = wave_max(mx);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      if (4 * (lane + 64 * k) < a.to) {
+        v[k].x = __expf(v[k].x - mx); v[k].y = __expf(v[k].y - mx);
+        v[k].z = __expf(v[k].z - mx); v[k].w = __expf(v[k].w - mx);
+        s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+      }
+    }
+    const float inv = 1.f / (wave_sum(s) + kSoftmaxEps);
+    float* y = a.out + r * a.to;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (lane + 64 * k);
+      if (c < a.to) *(float4*)(y + c) = make_float4(v[k].x * inv, v[k].y * inv, v[k].z * inv, v[k].w * inv);
+    }
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void softmax_bw_vec(float* dinp, const float* dout, const float* soft,
+                                                      int64_t rows, int64_t len) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    float4 dy[NV], y[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (lane + 64 * k);
+      if (c < len) {
+        dy[k] = *(const float4*)(dout + r * len + c);
+        y[k] = *(const float4*)(soft + r * len + c);
+        s += (dy[k].x * y[k].x + dy[k].y * y[k].y) + (dy[k].z * y[k].z + dy[k].w * y[k].w);
+      }
+    }
+    s = wave_sum(s);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (lane + 64 * k);
+      if (c < len)
+        *(float4*)(dinp + r * len + c) = make_float4(y[k].x * (dy[k].x - s), y[k].y * (dy[k].y - s),
+                                                     y[k].z * (dy[k].z - s), y[k].w * (dy[k].w - s));
+    }
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fw_vec(float* ln, float* var_out, float* mean_out,
+                                                 const float* inp, const float* gamma,
+                                                 const float* beta, int64_t rows, int64_t H) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    float4 v[NV];
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (lane + 64 * k);
+      if (c < H) {
+        v[k] = *(const float4*)(inp + r * H + c);
+        s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+        ss += (v[k].x * v[k].x + v[k].y * v[k].y) + (v[k].z * v[k].z + v[k].w * v[k].w);
+      }
+    }
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+    const float mean = s / (float)H;
+    const float var = ss / (float)H - mean * mean + kLnEps;
+    const float rsd = 1.f / sqrtf(var);
+    if (lane == 0) { mean_out[r] = mean; var_out[r] = var; }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (lane + 64 * k);
+      if (c < H) {
+        const float4 g = *(const float4*)(gamma + c), bb = *(const float4*)(beta + c);
+        *(float4*)(ln + r * H + c) = make_float4(g.x * ((v[k].x - mean) * rsd) + bb.x,
+                                                 g.y * ((v[k].y - mean) * rsd) + bb.y,
+                                                 g.z * ((v[k].z - mean) * rsd) + bb.z,
+                                                 g.w * ((v[k].w - mean) * rsd) + bb.w);
+      }
+    }
+  }
+}
+
+// LayerNorm backward, dx for every row and (PARTIAL) this block's dγ/dβ partial sums over its
+// rows: ws[block][0][H] = Σ dy, ws[block][1][H] = Σ dy·x̂ (the four waves' register partials
+// added in LDS in wave order: deterministic).
+template <int NV, bool PARTIAL>
+__global__ __launch_bounds__(256) void ln_bw_vec(float* dinp, float* ws, const float* dout,
+                                                 const float* inp, const float* gamma,
+                                                 const float* var, const float* mean, int64_t rows,
+                                                 int64_t H) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float4 db[PARTIAL ? NV : 1], dg[PARTIAL ? NV : 1];
+  if (PARTIAL) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) { db[k] = make_float4(0.f, 0.f, 0.f, 0.f); dg[k] = db[k]; }
+  }
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += nw) {
+    const float mu = mean[r], rsd = 1.f / sqrtf(var[r]);
+    float4 dy[NV], xh[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (lane + 64 * k);
+      if (c < H) {
+        dy[k] = *(const float4*)(dout + r * H + c);
+        const float4 x = *(const float4*)(inp + r * H + c), g = *(const float4*)(gamma + c);
+        xh[k] = make_float4((x.x - mu) * rsd, (x.y - mu) * rsd, (x.z - mu) * rsd, (x.w - mu) * rsd);
+        const float4 dyg = make_float4(dy[k].x * g.x, dy[k].y * g.y, dy[k].z * g.z, dy[k].w * g.w);
+        s1 += (dyg.x + dyg.y) + (dyg.z + dyg.w);
+        s2 += (dyg.x * xh[k].x + dyg.y * xh[k].y) + (dyg.z * xh[k].z + dyg.w * xh[k].w);
+        if (PARTIAL) {
+          db[k].x += dy[k].x; db[k].y += dy[k].y; db[k].z += dy[k].z; db[k].w += dy[k].w;
+          dg[k].x += dy[k].x * xh[k].x; dg[k].y += dy[k].y * xh[k].y;
+          dg[k].z += dy[k].z * xh[k].z; dg[k].w += dy[k].w * xh[k].w;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / (float)H;
+    s2 = wave_sum(s2) / (float)H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (lane + 64 * k);
+      if (c < H) {
+        const float4 g = *(const float4*)(gamma + c);
+        *(float4*)(dinp + r * H + c) = make_float4((dy[k].x * g.x - s1 - xh[k].x * s2) * rsd,
+                                                   (dy[k].y * g.y - s1 - xh[k].y * s2) * rsd,
+                                                   (dy[k].z * g.z - s1 - xh[k].z * s2) * rsd,
+                                                   (dy[k].w * g.w - s1 - xh[k].w * s2) * rsd);
+      }
+    }
+  }
+  if (PARTIAL) {
+    __shared__ float4 sp[4][2][64 * NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      sp[wave][0][lane + 64 * k] = db[k];
+      sp[wave][1][lane + 64 * k] = dg[k];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < 2 * (H / 4); j += 256) {
+      const int w = j / (H / 4), c4 = j % (H / 4);
+      float4 t = sp[0][w][c4];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        const float4 u = sp[q][w][c4];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      }
+      *(float4*)(ws + ((int64_t)blockIdx.x * 2 + w) * H + 4 * c4) = t;
+    }
+  }
+}
+
+// The blocks' [2][H] slabs summed in segments of 64 slabs: block (column group x, segment y),
+// wave w adds slabs 64 y + w + 4 k in order, the four waves are added in wave order
+// (deterministic); out[y][2][H].
+constexpr int kSlabSeg = 64;
+__global__ __launch_bounds__(256) void ln_bw_vec_seg(float* out, const float* ws, int64_t H, int64_t nb) {
+  __shared__ float red[4][2][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t s0 = (int64_t)blockIdx.y * kSlabSeg, s1 = min(nb, s0 + kSlabSeg);
+  float db = 0.f, dg = 0.f;
+  if (col < H) {
+#pragma unroll 4
+    for (int64_t c = s0 + wave; c < s1; c += 4) {
+      db += ws[(2 * c) * H + col];
+      dg += ws[(2 * c + 1) * H + col];
+    }
+  }
+  red[wave][0][lane] = db;
+  red[wave][1][lane] = dg;
+  __syncthreads();
+  if (wave == 0 && col < H) {
+    out[(2 * blockIdx.y) * H + col] = ((red[0][0][lane] + red[1][0][lane]) + red[2][0][lane]) + red[3][0][lane];
+    out[(2 * blockIdx.y + 1) * H + col] = ((red[0][1][lane] + red[1][1][lane]) + red[2][1][lane]) + red[3][1][lane];
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bw_vec_final(float* dgamma, float* dbeta, const float* ws,
+                                                       int64_t H, int64_t nb) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= H) return;
+  float db = 0.f, dg = 0.f;
+  for (int64_t c = 0; c < nb; ++c) {
+    db += ws[(2 * c) * H + col];
+    dg += ws[(2 * c + 1) * H + col];
+  }
+  dbeta[col] = db;
+  dgamma[col] = dg;
+}
+
+// float4 pieces per lane for a row of `len` (a multiple of 4): 1, 2, 4, 8 or 16; 0 when the
+// row needs the scalar kernels (len % 4 != 0 or len > 4096)
+static int row_nv(int64_t len) {
+  if (len % 4 != 0 || len > 4096) return 0;
+  const int64_t p = (len / 4 + 63) / 64;
+  return p <= 1 ? 1 : p <= 2 ? 2 : p <= 4 ? 4 : p <= 8 ? 8 : 16;
+}
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+// blocks of the fused LayerNorm backward: its dγ/dβ partials are one [2][H] slab per block
+static int64_t ln_vec_blocks(int64_t rows) {
+  const int64_t g = (rows + 3) / 4;
+  return g > 1024 ? 1024 : (g < 1 ? 1 : g);
+}
+
 }  // namespace mt
 
 using namespace mt;
@@ -234,29 +488,65 @@ int mt_attn_softmax_fw(float* out, const float* inp, const float* mask, int64_t 
   if (mask)
     for (int i = 0; i < 4; ++i) a.ms[i] = mask_strides[i];
   a.mask_future = mask_future;
-  hipLaunchKernelGGL(softmax_fw_kernel, dim3(row_grid(B * nh * from_len)), dim3(256), 0,
-                     (hipStream_t)stream, a);
+  const dim3 grid(row_grid(B * nh * from_len));
+  hipStream_t st = (hipStream_t)stream;
+  const int nv = (al16(out) && al16(inp)) ? row_nv(to_len) : 0;
+  const int mvec = mask && a.ms[3] == 1 && a.ms[0] % 4 == 0 && a.ms[1] % 4 == 0 && a.ms[2] % 4 == 0 &&
+                   al16(mask);
+  switch (nv) {
+    case 1: hipLaunchKernelGGL(softmax_fw_vec<1>, grid, dim3(256), 0, st, a, mvec); break;
+    case 2: hipLaunchKernelGGL(softmax_fw_vec<2>, grid, dim3(256), 0, st, a, mvec); break;
+    case 4: hipLaunchKernelGGL(softmax_fw_vec<4>, grid, dim3(256), 0, st, a, mvec); break;
+    case 8: hipLaunchKernelGGL(softmax_fw_vec<8>, grid, dim3(256), 0, st, a, mvec); break;
+    case 16: hipLaunchKernelGGL(softmax_fw_vec<16>, grid, dim3(256), 0, st, a, mvec); break;
+    default: hipLaunchKernelGGL(softmax_fw_kernel, grid, dim3(256), 0, st, a); break;
+  }
   return check_hip(hipGetLastError(), "mt_attn_softmax_fw");
 }
 
 int mt_attn_softmax_bw(float* dinp, const float* dout, const float* soft, int64_t rows,
                        int64_t softmax_len, void* stream) {
   if (rows <= 0 || softmax_len <= 0) return set_error("mt_attn_softmax_bw: bad sizes");
-  hipLaunchKernelGGL(softmax_bw_kernel, dim3(row_grid(rows)), dim3(256), 0, (hipStream_t)stream,
-                     dinp, dout, soft, rows, softmax_len);
+  const dim3 grid(row_grid(rows));
+  hipStream_t st = (hipStream_t)stream;
+  const int nv = (al16(dinp) && al16(dout) && al16(soft)) ? row_nv(softmax_len) : 0;
+  switch (nv) {
+    case 1: hipLaunchKernelGGL(softmax_bw_vec<1>, grid, dim3(256), 0, st, dinp, dout, soft, rows, softmax_len); break;
+    case 2: hipLaunchKernelGGL(softmax_bw_vec<2>, grid, dim3(256), 0, st, dinp, dout, soft, rows, softmax_len); break;
+    case 4: hipLaunchKernelGGL(softmax_bw_vec<4>, grid, dim3(256), 0, st, dinp, dout, soft, rows, softmax_len); break;
+    case 8: hipLaunchKernelGGL(softmax_bw_vec<8>, grid, dim3(256), 0, st, dinp, dout, soft, rows, softmax_len); break;
+    case 16: hipLaunchKernelGGL(softmax_bw_vec<16>, grid, dim3(256), 0, st, dinp, dout, soft, rows, softmax_len); break;
+    default: hipLaunchKernelGGL(softmax_bw_kernel, grid, dim3(256), 0, st, dinp, dout, soft, rows, softmax_len); break;
+  }
   return check_hip(hipGetLastError(), "mt_attn_softmax_bw");
 }
 
 int mt_layernorm_fw(float* ln_res, float* var, float* mean, const float* inp, const float* gamma,
                     const float* beta, int64_t rows, int64_t hidden, void* stream) {
   if (rows <= 0 || hidden <= 0) return set_error("mt_layernorm_fw: bad sizes");
-  hipLaunchKernelGGL(ln_fw_kernel, dim3(row_grid(rows)), dim3(256), 0, (hipStream_t)stream,
-                     ln_res, var, mean, inp, gamma, beta, rows, hidden);
+  const dim3 grid(row_grid(rows));
+  hipStream_t st = (hipStream_t)stream;
+  const int nv = (al16(ln_res) && al16(inp) && al16(gamma) && al16(beta)) ? row_nv(hidden) : 0;
+#define MT_LN_FW(NV) hipLaunchKernelGGL(ln_fw_vec<NV>, grid, dim3(256), 0, st, ln_res, var, mean, inp, gamma, beta, rows, hidden)
+  switch (nv) {
+    case 1: MT_LN_FW(1); break;
+    case 2: MT_LN_FW(2); break;
+    case 4: MT_LN_FW(4); break;
+    case 8: MT_LN_FW(8); break;
+    case 16: MT_LN_FW(16); break;
+    default:
+      hipLaunchKernelGGL(ln_fw_kernel, grid, dim3(256), 0, st, ln_res, var, mean, inp, gamma, beta, rows, hidden);
+      break;
+  }
+#undef MT_LN_FW
   return check_hip(hipGetLastError(), "mt_layernorm_fw");
 }
 
 int64_t mt_layernorm_bw_workspace_bytes(int64_t rows, int64_t hidden) {
-  return 2 * ln_chunks(rows) * hidden * (int64_t)sizeof(float);
+  // fused path: one [2][H] slab per block plus one per 64-slab segment
+  const int64_t nb = ln_vec_blocks(rows), vec = nb + (nb + kSlabSeg - 1) / kSlabSeg;
+  const int64_t slabs = ln_chunks(rows) > vec ? ln_chunks(rows) : vec;
+  return 2 * slabs * hidden * (int64_t)sizeof(float);
 }
 
 int mt_layernorm_bw(float* gamma_grad, float* beta_grad, float* inp_grad, const float* out_grad,
@@ -267,6 +557,28 @@ int mt_layernorm_bw(float* gamma_grad, float* beta_grad, float* inp_grad, const 
   if (rows <= 0 || hidden <= 0) return set_error("mt_layernorm_bw: bad sizes");
   if (!workspace) return set_error("mt_layernorm_bw: null workspace");
   hipStream_t st = (hipStream_t)stream;
+  const int nv = (al16(inp_grad) && al16(out_grad) && al16(inp) && al16(gamma) && al16(workspace))
+                     ? row_nv(hidden) : 0;
+  if (nv >= 1 && nv <= 4) {  // one pass: dx and the per-block dγ/dβ partials, then the blocks' sum
+    const int64_t nb = ln_vec_blocks(rows);
+    float* ws = (float*)workspace;
+#define MT_LN_BW(NV) hipLaunchKernelGGL((ln_bw_vec<NV, true>), dim3((unsigned)nb), dim3(256), 0, st, inp_grad, ws, out_grad, inp, gamma, var, mean, rows, hidden)
+    switch (nv) {
+      case 1: MT_LN_BW(1); break;
+      case 2: MT_LN_BW(2); break;
+      default: MT_LN_BW(4); break;
+    }
+#undef MT_LN_BW
+    if (check_hip(hipGetLastError(), "mt_layernorm_bw(fused)")) return 1;
+    const int64_t nseg = (nb + kSlabSeg - 1) / kSlabSeg;
+    float* ws2 = ws + 2 * nb * hidden;
+    hipLaunchKernelGGL(ln_bw_vec_seg, dim3((unsigned)((hidden + 63) / 64), (unsigned)nseg), dim3(256), 0, st,
+                       ws2, (const float*)ws, hidden, nb);
+    if (check_hip(hipGetLastError(), "mt_layernorm_bw(segments)")) return 1;
+    hipLaunchKernelGGL(ln_bw_vec_final, dim3((unsigned)((hidden + 255) / 256)), dim3(256), 0, st,
+                       gamma_grad, beta_grad, (const float*)ws2, hidden, nseg);
+    return check_hip(hipGetLastError(), "mt_layernorm_bw(final)");
+  }
   const int64_t chunks = ln_chunks(rows);
   if (chunks > 65535) return set_error("mt_layernorm_bw: too many rows");
   hipLaunchKernelGGL(ln_bw_dgb_partial, dim3((unsigned)((hidden + 63) / 64), (unsigned)chunks),
@@ -276,8 +588,15 @@ int mt_layernorm_bw(float* gamma_grad, float* beta_grad, float* inp_grad, const 
   hipLaunchKernelGGL(ln_bw_dgb_final, dim3((unsigned)((hidden + 255) / 256)), dim3(256), 0, st,
                      gamma_grad, beta_grad, (const float*)workspace, hidden, chunks);
   if (check_hip(hipGetLastError(), "mt_layernorm_bw(final)")) return 1;
-  hipLaunchKernelGGL(ln_bw_dinp_kernel, dim3(row_grid(rows)), dim3(256), 0, st, inp_grad,
-                     out_grad, inp, gamma, var, mean, rows, hidden);
+  if (nv == 8)
+    hipLaunchKernelGGL((ln_bw_vec<8, false>), dim3(row_grid(rows)), dim3(256), 0, st, inp_grad, nullptr,
+                       out_grad, inp, gamma, var, mean, rows, hidden);
+  else if (nv == 16)
+    hipLaunchKernelGGL((ln_bw_vec<16, false>), dim3(row_grid(rows)), dim3(256), 0, st, inp_grad, nullptr,
+                       out_grad, inp, gamma, var, mean, rows, hidden);
+  else
+    hipLaunchKernelGGL(ln_bw_dinp_kernel, dim3(row_grid(rows)), dim3(256), 0, st, inp_grad,
+                       out_grad, inp, gamma, var, mean, rows, hidden);
   return check_hip(hipGetLastError(), "mt_layernorm_bw(dinp)");
 }
 
