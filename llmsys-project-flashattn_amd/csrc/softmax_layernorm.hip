@@ -22,9 +22,10 @@
 // These kernels are HBM-bound, so each row is read from HBM exactly once: when the row
 // length is a multiple of 4 and at most 4096, a lane keeps its 16-B pieces of the row in
 // registers (NV float4 per lane, templated) between the reduction and the output pass
-// (softmax fw/bw, LayerNorm fw, LayerNorm bw dx), and the LayerNorm backward computes dx and
-// its rows' dγ/dβ partials in one pass for hidden <= 1024. Other shapes take the scalar
-// kernels, which re-read the row (from L2 in practice).
+// (softmax fw/bw, LayerNorm fw, LayerNorm bw), and the LayerNorm backward computes dx and
+// its rows' dγ/dβ partials in one pass (a wave per row up to hidden 1024, a workgroup per
+// row above). Other shapes take the scalar kernels, which re-read the row (from L2 in
+// practice).
 #include <stdio.h>
 #include <string.h>
 
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(256) void ln_fw_vec(float* ln, float* var_out, floa
   }
 }
 
-// LayerNorm backward, dx for every row and (PARTIAL) this block's dγ/dβ partial sums over its
+// LayerNorm backward (hidden <= 1024), dx for every row and (PARTIAL) this block's dγ/dβ partial sums over its
 // rows: ws[block][0][H] = Σ dy, ws[block][1][H] = Σ dy·x̂ (the four waves' register partials
 // added in LDS in wave order: deterministic).
 template <int NV, bool PARTIAL>
@@ -416,6 +417,122 @@ __global__ __launch_bounds__(256) void ln_bw_vec(float* dinp, float* ws, const f
   }
 }
 
+// LayerNorm forward for 1024 < hidden <= 4096 (hidden % 4 == 0): a workgroup per row, thread t
+// owning the float4 pieces t + 256 k (k < NV), γ and β in registers; the row sums go through
+// LDS (one barrier per row, exchange slots alternating by row parity).
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fw_row(float* ln, float* var_out, float* mean_out,
+                                                 const float* inp, const float* gamma,
+                                                 const float* beta, int64_t rows, int64_t H) {
+  __shared__ float red[2][4][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float4 gm[NV], bt[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t c = 4 * (tid + 256 * k);
+    gm[k] = c < H ? *(const float4*)(gamma + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bt[k] = c < H ? *(const float4*)(beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  int par = 0;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x, par ^= 1) {
+    float4 v[NV];
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (tid + 256 * k);
+      if (c < H) {
+        v[k] = *(const float4*)(inp + r * H + c);
+        s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+        ss += (v[k].x * v[k].x + v[k].y * v[k].y) + (v[k].z * v[k].z + v[k].w * v[k].w);
+      }
+    }
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+    if (lane == 0) { red[par][wave][0] = s; red[par][wave][1] = ss; }
+    __syncthreads();
+    s = ((red[par][0][0] + red[par][1][0]) + red[par][2][0]) + red[par][3][0];
+    ss = ((red[par][0][1] + red[par][1][1]) + red[par][2][1]) + red[par][3][1];
+    const float mean = s / (float)H;
+    const float var = ss / (float)H - mean * mean + kLnEps;
+    const float rsd = 1.f / sqrtf(var);
+    if (tid == 0) { mean_out[r] = mean; var_out[r] = var; }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (tid + 256 * k);
+      if (c < H)
+        *(float4*)(ln + r * H + c) = make_float4(gm[k].x * ((v[k].x - mean) * rsd) + bt[k].x,
+                                                 gm[k].y * ((v[k].y - mean) * rsd) + bt[k].y,
+                                                 gm[k].z * ((v[k].z - mean) * rsd) + bt[k].z,
+                                                 gm[k].w * ((v[k].w - mean) * rsd) + bt[k].w);
+    }
+  }
+}
+
+// LayerNorm backward for 1024 < hidden <= 4096 (hidden % 4 == 0): a workgroup per row, thread
+// t owning the float4 pieces t + 256 k (k < NV) of every row it visits, so its dγ/dβ
+// partials stay in registers; the row sums go through LDS (one barrier per row, the
+// exchange slots alternating by row parity). Writes dx and the block's [2][H] slab.
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bw_row(float* dinp, float* ws, const float* dout,
+                                                 const float* inp, const float* gamma,
+                                                 const float* var, const float* mean, int64_t rows,
+                                                 int64_t H) {
+  __shared__ float red[2][4][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float4 db[NV], dg[NV], gm[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    db[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    dg[k] = db[k];
+    const int64_t c = 4 * (tid + 256 * k);
+    gm[k] = c < H ? *(const float4*)(gamma + c) : db[k];
+  }
+  int par = 0;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x, par ^= 1) {
+    const float mu = mean[r], rsd = 1.f / sqrtf(var[r]);
+    float4 dy[NV], xh[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (tid + 256 * k);
+      if (c < H) {
+        dy[k] = *(const float4*)(dout + r * H + c);
+        const float4 x = *(const float4*)(inp + r * H + c);
+        xh[k] = make_float4((x.x - mu) * rsd, (x.y - mu) * rsd, (x.z - mu) * rsd, (x.w - mu) * rsd);
+        const float4 g = make_float4(dy[k].x * gm[k].x, dy[k].y * gm[k].y, dy[k].z * gm[k].z, dy[k].w * gm[k].w);
+        s1 += (g.x + g.y) + (g.z + g.w);
+        s2 += (g.x * xh[k].x + g.y * xh[k].y) + (g.z * xh[k].z + g.w * xh[k].w);
+        db[k].x += dy[k].x; db[k].y += dy[k].y; db[k].z += dy[k].z; db[k].w += dy[k].w;
+        dg[k].x += dy[k].x * xh[k].x; dg[k].y += dy[k].y * xh[k].y;
+        dg[k].z += dy[k].z * xh[k].z; dg[k].w += dy[k].w * xh[k].w;
+      }
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) { red[par][wave][0] = s1; red[par][wave][1] = s2; }
+    __syncthreads();  // (the other parity's slots were last read before this barrier)
+    s1 = (((red[par][0][0] + red[par][1][0]) + red[par][2][0]) + red[par][3][0]) / (float)H;
+    s2 = (((red[par][0][1] + red[par][1][1]) + red[par][2][1]) + red[par][3][1]) / (float)H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = 4 * (tid + 256 * k);
+      if (c < H)
+        *(float4*)(dinp + r * H + c) = make_float4((dy[k].x * gm[k].x - s1 - xh[k].x * s2) * rsd,
+                                                   (dy[k].y * gm[k].y - s1 - xh[k].y * s2) * rsd,
+                                                   (dy[k].z * gm[k].z - s1 - xh[k].z * s2) * rsd,
+                                                   (dy[k].w * gm[k].w - s1 - xh[k].w * s2) * rsd);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t c = 4 * (tid + 256 * k);
+    if (c < H) {
+      *(float4*)(ws + ((int64_t)blockIdx.x * 2) * H + c) = db[k];
+      *(float4*)(ws + ((int64_t)blockIdx.x * 2 + 1) * H + c) = dg[k];
+    }
+  }
+}
+
 // The blocks' [2][H] slabs summed in segments of 64 slabs: block (column group x, segment y),
 // wave w adds slabs 64 y + w + 4 k in order, the four waves are added in wave order
 // (deterministic); out[y][2][H].
@@ -463,10 +580,11 @@ static int row_nv(int64_t len) {
   return p <= 1 ? 1 : p <= 2 ? 2 : p <= 4 ? 4 : p <= 8 ? 8 : 16;
 }
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
-// blocks of the fused LayerNorm backward: its dγ/dβ partials are one [2][H] slab per block
-static int64_t ln_vec_blocks(int64_t rows) {
-  const int64_t g = (rows + 3) / 4;
-  return g > 1024 ? 1024 : (g < 1 ? 1 : g);
+// blocks of the fused LayerNorm backward (its dγ/dβ partials are one [2][H] slab per block):
+// a wave per row up to hidden 1024, a workgroup per row above
+static int64_t ln_vec_blocks(int64_t rows, int64_t H) {
+  const int64_t g = H <= 1024 ? (rows + 3) / 4 : rows, cap = H <= 1024 ? 1024 : 512;
+  return g > cap ? cap : (g < 1 ? 1 : g);
 }
 
 }  // namespace mt
@@ -532,8 +650,14 @@ int mt_layernorm_fw(float* ln_res, float* var, float* mean, const float* inp, co
     case 1: MT_LN_FW(1); break;
     case 2: MT_LN_FW(2); break;
     case 4: MT_LN_FW(4); break;
-    case 8: MT_LN_FW(8); break;
-    case 16: MT_LN_FW(16); break;
+    case 8:  // 1024 < hidden <= 2048: a workgroup per row
+      hipLaunchKernelGGL(ln_fw_row<2>, dim3((unsigned)(rows < 2048 ? rows : 2048)), dim3(256), 0, st, ln_res, var,
+                         mean, inp, gamma, beta, rows, hidden);
+      break;
+    case 16:
+      hipLaunchKernelGGL(ln_fw_row<4>, dim3((unsigned)(rows < 2048 ? rows : 2048)), dim3(256), 0, st, ln_res, var,
+                         mean, inp, gamma, beta, rows, hidden);
+      break;
     default:
       hipLaunchKernelGGL(ln_fw_kernel, grid, dim3(256), 0, st, ln_res, var, mean, inp, gamma, beta, rows, hidden);
       break;
@@ -544,7 +668,7 @@ int mt_layernorm_fw(float* ln_res, float* var, float* mean, const float* inp, co
 
 int64_t mt_layernorm_bw_workspace_bytes(int64_t rows, int64_t hidden) {
   // fused path: one [2][H] slab per block plus one per 64-slab segment
-  const int64_t nb = ln_vec_blocks(rows), vec = nb + (nb + kSlabSeg - 1) / kSlabSeg;
+  const int64_t nb = ln_vec_blocks(rows, hidden), vec = nb + (nb + kSlabSeg - 1) / kSlabSeg;
   const int64_t slabs = ln_chunks(rows) > vec ? ln_chunks(rows) : vec;
   return 2 * slabs * hidden * (int64_t)sizeof(float);
 }
@@ -559,16 +683,20 @@ int mt_layernorm_bw(float* gamma_grad, float* beta_grad, float* inp_grad, const 
   hipStream_t st = (hipStream_t)stream;
   const int nv = (al16(inp_grad) && al16(out_grad) && al16(inp) && al16(gamma) && al16(workspace))
                      ? row_nv(hidden) : 0;
-  if (nv >= 1 && nv <= 4) {  // one pass: dx and the per-block dγ/dβ partials, then the blocks' sum
-    const int64_t nb = ln_vec_blocks(rows);
+  if (nv >= 1) {  // one pass: dx and the per-block dγ/dβ partials, then the blocks' sum
+    const int64_t nb = ln_vec_blocks(rows, hidden);
     float* ws = (float*)workspace;
 #define MT_LN_BW(NV) hipLaunchKernelGGL((ln_bw_vec<NV, true>), dim3((unsigned)nb), dim3(256), 0, st, inp_grad, ws, out_grad, inp, gamma, var, mean, rows, hidden)
+#define MT_LN_BW_ROW(NV) hipLaunchKernelGGL(ln_bw_row<NV>, dim3((unsigned)nb), dim3(256), 0, st, inp_grad, ws, out_grad, inp, gamma, var, mean, rows, hidden)
     switch (nv) {
       case 1: MT_LN_BW(1); break;
       case 2: MT_LN_BW(2); break;
-      default: MT_LN_BW(4); break;
+      case 4: MT_LN_BW(4); break;
+      case 8: MT_LN_BW_ROW(2); break;   // hidden <= 2048: 2 float4 per thread
+      default: MT_LN_BW_ROW(4); break;  // hidden <= 4096
     }
 #undef MT_LN_BW
+#undef MT_LN_BW_ROW
     if (check_hip(hipGetLastError(), "mt_layernorm_bw(fused)")) return 1;
     const int64_t nseg = (nb + kSlabSeg - 1) / kSlabSeg;
     float* ws2 = ws + 2 * nb * hidden;
@@ -588,15 +716,8 @@ int mt_layernorm_bw(float* gamma_grad, float* beta_grad, float* inp_grad, const 
   hipLaunchKernelGGL(ln_bw_dgb_final, dim3((unsigned)((hidden + 255) / 256)), dim3(256), 0, st,
                      gamma_grad, beta_grad, (const float*)workspace, hidden, chunks);
   if (check_hip(hipGetLastError(), "mt_layernorm_bw(final)")) return 1;
-  if (nv == 8)
-    hipLaunchKernelGGL((ln_bw_vec<8, false>), dim3(row_grid(rows)), dim3(256), 0, st, inp_grad, nullptr,
-                       out_grad, inp, gamma, var, mean, rows, hidden);
-  else if (nv == 16)
-    hipLaunchKernelGGL((ln_bw_vec<16, false>), dim3(row_grid(rows)), dim3(256), 0, st, inp_grad, nullptr,
-                       out_grad, inp, gamma, var, mean, rows, hidden);
-  else
-    hipLaunchKernelGGL(ln_bw_dinp_kernel, dim3(row_grid(rows)), dim3(256), 0, st, inp_grad,
-                       out_grad, inp, gamma, var, mean, rows, hidden);
+  hipLaunchKernelGGL(ln_bw_dinp_kernel, dim3(row_grid(rows)), dim3(256), 0, st, inp_grad,
+                     out_grad, inp, gamma, var, mean, rows, hidden);
   return check_hip(hipGetLastError(), "mt_layernorm_bw(dinp)");
 }
 

@@ -2,8 +2,8 @@
 each code path: the register-resident row kernels for every NV (row length a multiple of 4,
 1 .. 16 float4 per lane, partial last pieces), the scalar kernels (row length not a multiple
 of 4, longer than 4096, or a misaligned base), broadcast and full masks, the future mask, the
-fused LayerNorm backward (hidden <= 1024, row counts not a multiple of 4 and larger than the
-1024-block grid) and its two-kernel form (hidden > 1024). References are float64 NumPy
+fused LayerNorm backward (a wave per row up to hidden 1024, a workgroup per row above; row
+counts not a multiple of 4 and larger than the grid) and its scalar form (hidden % 4 != 0). References are float64 NumPy
 restatements of the contracts the kernels cite (reference src/softmax_kernel.cu:35-224,
 :308-341; src/layernorm_kernel.cu:36-98, :192-368), at the reference kernel tests' tolerances
 (kernel_tests/test_softmax_fw.py:14 1e-3, test_softmax_bw.py:14 1e-2/1e-3,
@@ -94,7 +94,7 @@ def test_softmax_misaligned_base(hip):
     np.testing.assert_allclose(out.cpu().numpy()[1:].reshape(1, 4, 8, 256), y, atol=1e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("rows,H", [(5, 32), (64, 256), (999, 512), (4103, 1024), (7, 1026),
+@pytest.mark.parametrize("rows,H", [(5, 32), (64, 256), (999, 512), (4103, 1024), (7, 1026), (1500, 2048),
                                     (13, 2048), (6, 4096), (3, 4100), (9, 36)])
 def test_layernorm_fw_bw(hip, rows, H):
     torch, _hip = hip
