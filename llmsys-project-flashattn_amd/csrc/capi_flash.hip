@@ -96,6 +96,8 @@ enum : int {
   kPolV6RowSumEven = 104,  // 102 with one exponential per MFMA slot
   kPolV6Split = 105,       // 102 with the keys split between the workgroup halves (v5's 76)
   kPolV6Causal = 106,      // 102's causal form (v5's paired causal schedule, policy 67)
+  // causal bwd: the default forms with paired light/heavy key (dK/dV) and query (dQ) blocks
+  kPolBwdPair = 107, kPolBwdPair8 = 108,  // 108: with the 8-wave dQ
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -105,7 +107,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -423,7 +425,7 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
     // per SIMD, 4 64-query steps with LDS-DMA Q/dO, 5 the same with 8 waves (256 keys per
     // dK/dV workgroup, 256 queries per dQ workgroup). Default: 5 non-causal (1.868 vs
     // 1.937 ms for 4 at C3, profiles/r2_ab_bwd.txt), 0 causal (1.12 vs 1.31 ms: the masked
-    // diagonal steps spill in the 64-query form). An in-wave interleaved dQ tile measured
+    // diagonal steps spill in the 64-query form), paired (18) on large causal grids. An in-wave interleaved dQ tile measured
     // 1.7 % slower than the plain tile and was removed (profiles/r1_ab_bwd_dq.txt).
     const int variant = pol == kPolBwdPipe        ? 1
                         : pol == kPolBwdQ64OneWave ? 3
@@ -436,11 +438,17 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
                         : pol == kPolBwdMix0       ? 15
                         : pol == kPolBwdMix4       ? 16
                         : pol == kPolBwdQ128       ? 17
+                        : pol == kPolBwdPair       ? 18
+                        : pol == kPolBwdPair8      ? 19
 #ifdef MT_DIAGNOSTICS
                         : (pol >= 87 && pol <= 90)  ? pol - 81  // dK/dV ablations (wrong results)
 #endif
                         : pol == kPolBwdQ32        ? 0
-                                                   : (causal ? 0 : 5);
+                        : !causal                  ? 5
+                        // causal: paired light/heavy blocks (policy 107: 1.065 vs 1.172 ms at C3
+                        // causal, profiles/r2m_ab_bwd_pair.txt) once the paired dK/dV grid fills
+                        // two workgroups per CU; below that pairing would idle half the CUs
+                        : (int64_t)((N + 255) / 256) * a.B * a.H >= 512 ? 18 : 0;
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }
