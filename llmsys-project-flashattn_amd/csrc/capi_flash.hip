@@ -15,7 +15,7 @@
 
 namespace mt {
 hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
-                              hipStream_t st);
+                              hipStream_t st, int ring);
 hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStream_t st,
                            bool* handled);
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
@@ -28,7 +28,7 @@ hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hip
                            bool* handled, int pair = 0);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
-                              hipStream_t st);
+                              hipStream_t st, int pair);
 #ifdef MT_DIAGNOSTICS
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 #endif
@@ -98,6 +98,12 @@ enum : int {
   kPolV6Causal = 106,      // 102's causal form (v5's paired causal schedule, policy 67)
   // causal bwd: the default forms with paired light/heavy key (dK/dV) and query (dQ) blocks
   kPolBwdPair = 107, kPolBwdPair8 = 108,  // 108: with the 8-wave dQ
+  // fp32 forward (d <= 64, 16-B rows): 109 the round-2 two-barrier kernel, 110 the register-Q
+  // ring unpaired, 111 the ring with paired query blocks (the default pairs only causal grids)
+  kPolFwdF32TwoBarrier = 109, kPolFwdF32Ring = 110, kPolFwdF32RingPair = 111,
+  // generic (fp32) causal backward: 112 unpaired, 113 always paired (default: paired on
+  // grids that keep two paired workgroups per CU)
+  kPolBwdGenNoPair = 112, kPolBwdGenPair = 113,
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -107,7 +113,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -387,7 +393,14 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
     const hipError_t e = fwd_bf16_dispatch(a, causal != 0, pol, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(bf16)");
   }
-  return check_hip(launch_fwd_generic(a, dtype == MT_BF16, vec, causal != 0, st),
+  return check_hip(launch_fwd_generic(a, dtype == MT_BF16, vec, causal != 0, st,
+                                      pol == kPolFwdF32TwoBarrier ? 0
+                                      : pol == kPolFwdF32Ring     ? 1
+                                      : pol == kPolFwdF32RingPair ? 2
+                                      // default: the paired ring when causal (C2 causal 0.317 ->
+                                      // 0.192 ms), the two-barrier kernel otherwise (0.3228 vs
+                                      // 0.3256 ms, profiles/r2m_ab_fp32_fwd.txt)
+                                      : causal ? 2 : 0),
                    "mt_flash_attn_fwd");
 }
 
@@ -452,7 +465,8 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }
-  return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream),
+  return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream,
+                                      pol == kPolBwdGenNoPair ? 0 : pol == kPolBwdGenPair ? 1 : 2),
                    "mt_flash_attn_bwd");
 }
 

@@ -57,7 +57,9 @@ __global__ __launch_bounds__(256) void fa_bwd_prep(AttnArgs p) {
 
 // ---------------------------------------------------------------------------
 // dK, dV: grid (ceil(N/128), B*H, ceil(d/DT)).
-template <typename T, int DT, int QB, bool VEC, bool CAUSAL>
+// PAIR (causal): a workgroup runs key blocks nkb - 1 - u (light) and then u (heavy) of one
+// head in turn, so the grid is balanced (fa_bwd_bf16.hip, policy 107, same scheme).
+template <typename T, int DT, int QB, bool VEC, bool CAUSAL, bool PAIR = false>
 __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
   constexpr int BKV = 128, BQ = 32 * QB;
   constexpr int PAD = 16 / sizeof(T);
@@ -73,10 +75,18 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
-  int kblk, bh;
-  xcd_order(kblk, bh);
-  const int k0 = kblk * BKV;
+  int ublk, bh;
+  xcd_order(ublk, bh);
   const int b = bh / p.H, hh = bh % p.H;
+  const int nkb = (N + BKV - 1) / BKV;
+#pragma nounroll
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+  const int kblk = !PAIR ? ublk : pass == 0 ? nkb - 1 - ublk : ublk;
+  if (PAIR && pass == 1) {
+    if (kblk == nkb - 1 - ublk) break;  // odd nkb: the middle block runs alone
+    __syncthreads();                     // the first block's LDS reads are done
+  }
+  const int k0 = kblk * BKV;
   const int oc = blockIdx.z * DT;
   const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
   const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
@@ -238,11 +248,13 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
         }
       }
   }
+  }  // pass
 }
 
 // ---------------------------------------------------------------------------
 // dQ: grid (ceil(N/128), B*H, ceil(d/DT)).
-template <typename T, int DT, int KB, bool VEC, bool CAUSAL>
+// PAIR (causal): query blocks u (light) and then nqb - 1 - u (heavy) of one head in turn.
+template <typename T, int DT, int KB, bool VEC, bool CAUSAL, bool PAIR = false>
 __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
   constexpr int BQ = 128, BK = 32 * KB;
   constexpr int PAD = 16 / sizeof(T);
@@ -256,10 +268,18 @@ __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
-  int qblk, bh;
-  xcd_order(qblk, bh);
-  const int q0 = qblk * BQ;
+  int ublk, bh;
+  xcd_order(ublk, bh);
   const int b = bh / p.H, hh = bh % p.H;
+  const int nqb = (N + BQ - 1) / BQ;
+#pragma nounroll
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+  const int qblk = !PAIR ? ublk : pass == 0 ? ublk : nqb - 1 - ublk;
+  if (PAIR && pass == 1) {
+    if (qblk == ublk) break;  // odd nqb: the middle block runs alone
+    __syncthreads();          // the first block's LDS reads are done
+  }
+  const int q0 = qblk * BQ;
   const int oc = blockIdx.z * DT;
   const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
   const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
@@ -392,14 +412,15 @@ __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
         }
       }
   }
+  }  // pass
 }
 
 // ---------------------------------------------------------------------------
-template <typename T, int DT, int QB, int KB, bool VEC, bool CAUSAL>
+template <typename T, int DT, int QB, int KB, bool VEC, bool CAUSAL, bool PAIR>
 static hipError_t launch_bwd_t(const AttnArgs& a, hipStream_t st) {
   constexpr int LD = DT + 16 / sizeof(T);
   const int nz = (a.d + DT - 1) / DT;
-  const int nblk = (a.N + 127) / 128;
+  const int nblk = PAIR ? ((a.N + 127) / 128 + 1) / 2 : (a.N + 127) / 128;
   {
     const int64_t rows = (int64_t)a.B * a.H * a.N;
     hipLaunchKernelGGL(fa_bwd_prep<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
@@ -408,7 +429,7 @@ static hipError_t launch_bwd_t(const AttnArgs& a, hipStream_t st) {
   }
   {
     const size_t smem = sizeof(T) * (size_t)LD * (2 * 128 + 2 * 32 * QB) + 2 * sizeof(float) * 32 * QB;
-    auto kfn = fa_bwd_dkv<T, DT, QB, VEC, CAUSAL>;
+    auto kfn = fa_bwd_dkv<T, DT, QB, VEC, CAUSAL, PAIR>;
     hipError_t e = hipFuncSetAttribute((const void*)kfn,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
@@ -418,7 +439,7 @@ static hipError_t launch_bwd_t(const AttnArgs& a, hipStream_t st) {
   }
   {
     const size_t smem = sizeof(T) * (size_t)LD * (2 * 128 + 2 * 32 * KB);
-    auto kfn = fa_bwd_dq<T, DT, KB, VEC, CAUSAL>;
+    auto kfn = fa_bwd_dq<T, DT, KB, VEC, CAUSAL, PAIR>;
     hipError_t e = hipFuncSetAttribute((const void*)kfn,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
@@ -428,22 +449,27 @@ static hipError_t launch_bwd_t(const AttnArgs& a, hipStream_t st) {
 }
 
 template <typename T, int DT, int QB, int KB>
-static hipError_t dispatch_bwd(const AttnArgs& a, bool vec, bool causal, hipStream_t st) {
+static hipError_t dispatch_bwd(const AttnArgs& a, bool vec, bool causal, bool pair, hipStream_t st) {
+  if (causal && pair)
+    return vec ? launch_bwd_t<T, DT, QB, KB, true, true, true>(a, st)
+               : launch_bwd_t<T, DT, QB, KB, false, true, true>(a, st);
   if (vec)
-    return causal ? launch_bwd_t<T, DT, QB, KB, true, true>(a, st)
-                  : launch_bwd_t<T, DT, QB, KB, true, false>(a, st);
-  return causal ? launch_bwd_t<T, DT, QB, KB, false, true>(a, st)
-                : launch_bwd_t<T, DT, QB, KB, false, false>(a, st);
+    return causal ? launch_bwd_t<T, DT, QB, KB, true, true, false>(a, st)
+                  : launch_bwd_t<T, DT, QB, KB, true, false, false>(a, st);
+  return causal ? launch_bwd_t<T, DT, QB, KB, false, true, false>(a, st)
+                : launch_bwd_t<T, DT, QB, KB, false, false, false>(a, st);
 }
 
+// pair: 0 never, 1 always (causal), 2 when the paired grid keeps >= 2 workgroups per CU
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
-                              hipStream_t st) {
+                              hipStream_t st, int pair) {
+  const bool pr = pair == 1 || (pair == 2 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
   if (bf16_io) {
-    if (a.d <= 64) return dispatch_bwd<bf16, 64, 2, 2>(a, vec, causal, st);
-    return dispatch_bwd<bf16, 128, 1, 1>(a, vec, causal, st);
+    if (a.d <= 64) return dispatch_bwd<bf16, 64, 2, 2>(a, vec, causal, pr, st);
+    return dispatch_bwd<bf16, 128, 1, 1>(a, vec, causal, pr, st);
   }
   // fp32 keeps 64-column chunks: a 128-column fp32 K+V pair would not fit the LDS.
-  return dispatch_bwd<float, 64, 1, 1>(a, vec, causal, st);
+  return dispatch_bwd<float, 64, 1, 1>(a, vec, causal, pr, st);
 }
 
 }  // namespace mt

@@ -192,6 +192,198 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
   }
 }
 
+
+// One d-chunk with 16-B rows (the fp32 path of minitorch's MHA at d <= 64, config 2): the
+// wave's Q fragments live in registers for the whole launch and K/V go through a two-slot
+// LDS ring, so a tile takes one barrier instead of two. Tile t + 1 was loaded into
+// registers during tile t - 1 and is written to the other slot after tile t computes (that
+// slot was last read in tile t - 1, before the previous barrier); tile t + 2 is then loaded.
+// Same math, masks, m/l contract and block order as fa_fwd_generic.
+// PAIR: a workgroup runs query blocks u and nqb - 1 - u of one head in turn (causal: a
+// light and a heavy block, every workgroup walks nqb + 1 key-tile pairs' worth; non-causal:
+// half the workgroups, each filling the ring for its second block while it drains the first).
+template <typename T, int DT, int KB, bool CAUSAL, bool PAIR>
+__global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
+  constexpr int BQ = 128, BK = 32 * KB;
+  constexpr int PAD = 16 / sizeof(T);
+  constexpr int LD = DT + PAD;
+  constexpr int SLOT = 2 * BK * LD;  // K then V
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* ring = (T*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N, d = p.d;
+  const int ngx = gridDim.x, nbh = gridDim.y;
+  const int hw = blockIdx.y * ngx + blockIdx.x, nblk = ngx * nbh;
+  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
+  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
+  const int u = logical % ngx, nqb = (N + BQ - 1) / BQ;
+  const int bh = logical / ngx, b = bh / p.H, hh = bh % p.H;
+  const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const int dpad = (d + 15) & ~15;
+  const int ksteps = dpad / 16;
+  constexpr int EPC = 16 / sizeof(T), CPR = DT / EPC, NCK = BK * CPR / 256;
+#pragma nounroll
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+  if (PAIR && pass == 1 && nqb - 1 - u == u) break;  // odd nqb: the middle block runs alone
+  const int q0 = (pass == 0 ? u : nqb - 1 - u) * BQ;
+  const int my_q = q0 + wave * 32 + c32;
+  const int wave_qmax = q0 + wave * 32 + 31;
+
+  // Q row my_q (clamped; rows past N are computed but not stored), k-step ks: elements
+  // 16 ks + 8 hf .. +7, zero past d (d is a multiple of 16 B here)
+  Frag<T> bq[DT / 16];
+  {
+    const T* qrow = Qg + (int64_t)min(my_q, N - 1) * p.sq[2];
+#pragma unroll
+    for (int ks = 0; ks < DT / 16; ++ks) {
+      uint4 ch[8 / EPC];
+#pragma unroll
+      for (int j = 0; j < 8 / EPC; ++j) {
+        const int col = 16 * ks + 8 * hf + j * EPC;
+        ch[j] = col < d ? *(const uint4*)(qrow + col) : make_uint4(0, 0, 0, 0);
+      }
+      bq[ks] = __builtin_bit_cast(Frag<T>, ch);
+    }
+  }
+
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x16 O[DT / 32];
+#pragma unroll
+  for (int i = 0; i < DT / 32; ++i) O[i] = f32x16{};
+
+  const int kend = CAUSAL ? min(N, q0 + BQ) : N;
+  const int ntiles = (kend + BK - 1) / BK;
+
+  uint4 pk[NCK], pv[NCK];
+  auto pre_load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCK; ++i) {
+      const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC, gr = k0 + r;
+      pk[i] = pv[i] = make_uint4(0, 0, 0, 0);
+      if (gr < N && cc < d) {
+        pk[i] = *(const uint4*)(Kg + (int64_t)gr * p.sk[2] + cc);
+        pv[i] = *(const uint4*)(Vg + (int64_t)gr * p.sv[2] + cc);
+      }
+    }
+  };
+  auto pre_store = [&](int s) __attribute__((always_inline)) {
+    T* sK = ring + s * SLOT;
+    T* sV = sK + BK * LD;
+#pragma unroll
+    for (int i = 0; i < NCK; ++i) {
+      const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC;
+      *(uint4*)(sK + r * LD + cc) = pk[i];
+      *(uint4*)(sV + r * LD + cc) = pv[i];
+    }
+  };
+  if (ntiles > 0) {
+    pre_load(0);
+    pre_store(0);
+    if (ntiles > 1) pre_load(BK);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * BK;
+    const T* sK = ring + (t & 1) * SLOT;
+    const T* sV = sK + BK * LD;
+    if (!(CAUSAL && k0 > wave_qmax)) {
+      f32x16 S[KB];
+#pragma unroll
+      for (int i = 0; i < KB; ++i) S[i] = f32x16{};
+      for (int ks = 0; ks < ksteps; ++ks) {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          Frag<T> ak = row_frag<T>(sK + (kb * 32 + c32) * LD + ks * 16 + 8 * hf);
+          mma(S[kb], ak, bq[ks]);
+        }
+      }
+      float smax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + kb * 32 + acc_row(r, hf);
+          float x = S[kb][r] * p.scale_log2;
+          if (key >= N || (CAUSAL && key > my_q)) x = -INFINITY;
+          S[kb][r] = x;
+          smax = fmaxf(smax, x);
+        }
+      smax = fmaxf(smax, __shfl_xor(smax, 32));
+      const float m_new = fmaxf(m_run, smax);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run - m_use);
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = exp2f(S[kb][r] - m_use);
+          S[kb][r] = e;
+          rs += e;
+        }
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < DT / 32; ++i) O[i] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          Frag<T> bp = acc_frag<T>(S[kb], s);
+#pragma unroll
+          for (int db = 0; db < DT / 32; ++db) {
+            Frag<T> av = col_frag<T>(sV, LD, kb * 32 + 16 * s + 4 * hf, db * 32, lane);
+            mma(O[db], av, bp);
+          }
+        }
+    }
+    if (t + 1 < ntiles) {
+      pre_store((t + 1) & 1);
+      if (t + 2 < ntiles) pre_load(k0 + 2 * BK);
+    }
+    __syncthreads();
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  const float inv_l = 1.f / l_tot;
+  if (my_q < N) {
+    T* Og = (T*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+#pragma unroll
+    for (int db = 0; db < DT / 32; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = db * 32 + 8 * g + 4 * hf;
+        if (col < d)  // d is a multiple of 4 here
+          store4(Og + col, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l, O[db][4 * g + 2] * inv_l,
+                 O[db][4 * g + 3] * inv_l, true);
+      }
+    if (hf == 0) {
+      const int64_t row = (int64_t)bh * N + my_q;
+      if (p.m) p.m[row] = m_run * kLn2;
+      if (p.l) p.l[row] = l_tot;
+    }
+  }
+  }  // pass
+}
+
+template <typename T, int DT, int KB, bool CAUSAL, bool PAIR>
+static hipError_t launch_fwd_ring_t(const AttnArgs& a, hipStream_t st) {
+  const size_t smem = sizeof(T) * (size_t)(DT + 16 / sizeof(T)) * 4 * 32 * KB;
+  auto kfn = fa_fwd_generic_ring<T, DT, KB, CAUSAL, PAIR>;
+  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)smem);
+  if (e != hipSuccess) return e;
+  const int nqb = (a.N + 127) / 128;
+  dim3 grid(PAIR ? (nqb + 1) / 2 : nqb, a.B * a.H, 1);
+  hipLaunchKernelGGL(kfn, grid, dim3(256), smem, st, a);
+  return hipGetLastError();
+}
+
 template <typename T, int DT, int KB>
 static size_t fwd_generic_smem() {
   constexpr int LD = DT + 16 / sizeof(T);
@@ -220,7 +412,17 @@ static hipError_t dispatch_fwd_generic(const AttnArgs& a, bool vec, bool causal,
 }
 
 hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
-                              hipStream_t st) {
+                              hipStream_t st, int ring) {
+  // fp32 with 16-B rows and d <= 64 (one d-chunk): the register-Q / two-slot ring kernel;
+  // ring = 1 unpaired, 2 paired query blocks, 3 paired when causal (0: fa_fwd_generic)
+  if (ring && vec && !bf16_io && a.d <= 64) {
+    const bool pair = ring == 2 || (ring == 3 && causal);
+    if (causal)
+      return pair ? launch_fwd_ring_t<float, 64, 2, true, true>(a, st)
+                  : launch_fwd_ring_t<float, 64, 2, true, false>(a, st);
+    return pair ? launch_fwd_ring_t<float, 64, 2, false, true>(a, st)
+                : launch_fwd_ring_t<float, 64, 2, false, false>(a, st);
+  }
   if (bf16_io) {
     if (a.d <= 64) return dispatch_fwd_generic<bf16, 64, 2>(a, vec, causal, st);
     return dispatch_fwd_generic<bf16, 128, 2>(a, vec, causal, st);

@@ -1,5 +1,5 @@
 """Interleaved in-process A/B timing of forward-kernel policies (diagnostics, GPU box).
-usage: python scripts/ab_fwd.py POL[,POL...] [causal] [B,H,N,d] [rounds]"""
+usage: python scripts/ab_fwd.py POL[,POL...] [causal] [B,H,N,d] [rounds]   (DTYPE=fp32 for fp32 I/O)"""
 import os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "llmsys-project-flashattn_amd"))
 import torch
@@ -9,7 +9,8 @@ causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
 B, H, N, d = (int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "8,16,4096,64").split(","))
 rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 7
 g = torch.Generator(device="cuda").manual_seed(0)
-q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
+dt = torch.float32 if os.environ.get("DTYPE") == "fp32" else torch.bfloat16
+q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(dt) for _ in range(3))
 o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
 flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
 t0 = time.time()
@@ -27,7 +28,7 @@ for rnd in range(rounds):
         e1.record(); torch.cuda.synchronize()
         res[p].append(e0.elapsed_time(e1) / reps)
 _hip.set_policy(0)
-print(f"shape {(B, H, N, d)} causal={causal} reps={reps} rounds={rounds}")
+print(f"shape {(B, H, N, d)} {dt} causal={causal} reps={reps} rounds={rounds}")
 for p in pols:
     t = sorted(res[p]); med = t[len(t) // 2]
     print(f"policy {p:3d}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s", flush=True)

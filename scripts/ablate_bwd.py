@@ -1,5 +1,5 @@
 """Interleaved in-process A/B timing of backward kernel policies (diagnostics).
-usage: python scripts/ablate_bwd.py p1,p2,... [causal]"""
+usage: python scripts/ablate_bwd.py p1,p2,... [causal]   (SHAPE=B,H,N,d, DTYPE=fp32)"""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "llmsys-project-flashattn_amd"))
 import torch
@@ -11,9 +11,10 @@ if os.environ.get("MT_DIAG") == "1":  # only when asked: the diag build can be s
     _hip.use_library(_DIAG)
 pols = [int(x) for x in sys.argv[1].split(",")]
 causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
-B, H, N, d = 8, 16, 4096, 64
+B, H, N, d = (int(x) for x in os.environ.get("SHAPE", "8,16,4096,64").split(","))
+dt = torch.float32 if os.environ.get("DTYPE") == "fp32" else torch.bfloat16
 g = torch.Generator(device="cuda").manual_seed(0)
-q, k, v, do = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(4))
+q, k, v, do = (torch.randn((B, H, N, d), device="cuda", generator=g).to(dt) for _ in range(4))
 o, m, l = _hip.flash_fwd(q, k, v, causal)
 ws = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(B, H, N, d) // 4, device="cuda")
 dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
@@ -31,6 +32,7 @@ for rnd in range(5):
         e1.record(); torch.cuda.synchronize()
         res[p].append(e0.elapsed_time(e1) / 5)
 _hip.set_policy(0)
+print(f"shape {(B, H, N, d)} {dt} causal={causal}")
 for p in pols:
     t = sorted(res[p]); med = t[len(t) // 2]
     print(f"bwd policy {p:3d}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s (FA-2 convention)")

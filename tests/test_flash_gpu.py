@@ -478,6 +478,60 @@ def test_spiked_rescale(torch_dev, policy, d):
         _hip.set_policy(0)
 
 
+@pytest.mark.parametrize("policy", (0, 112, 113))
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_generic_causal_bwd_pairing_vs_oracle(torch_dev, policy, dtype):
+    """Generic causal backward (fp32; bf16 at d != 64): 0 default, 112 unpaired, 113 paired
+    light/heavy key and query blocks; odd block counts (N = 777: 7 blocks of 128), one
+    block (N = 100), d = 48 / 128, against the oracle at the fp32 gradient bound."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(47)
+    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    try:
+        _hip.set_policy(policy)
+        for (B, H, N, d) in ((1, 2, 1024, 64), (1, 1, 777, 64), (1, 1, 100, 48), (1, 2, 640, 128)):
+            q, k, v, do = (rng.standard_normal((B, H, N, d)).astype(np.float32) for _ in range(4))
+            if dtype == "bf16":
+                q, k, v, do = (A.bf16_round(x) for x in (q, k, v, do))
+            tq, tk, tv, tdo = (_dev(torch, x, tdt) for x in (q, k, v, do))
+            o, m, l = _hip.flash_fwd(tq, tk, tv, True)
+            dq, dk, dv = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, True)
+            torch.cuda.synchronize()
+            o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, True)
+            refs = A.attention_bwd(q, k, v, o_ref, do, m_ref, l_ref, True)
+            scale = max(1.0, *(float(np.abs(r).max()) for r in refs))
+            tol = (2e-5 if dtype == "fp32" else 6e-2) * scale
+            for got, ref, name in zip((dq, dk, dv), refs, ("dq", "dk", "dv")):
+                err = float(np.abs(_np(got) - ref).max())
+                assert err <= tol, f"{name} {(B, H, N, d)} max-abs {err:.3e} > {tol:.3e}"
+    finally:
+        _hip.set_policy(0)
+
+
+@pytest.mark.parametrize("policy", (0, 109, 110, 111))
+@pytest.mark.parametrize("causal", [False, True])
+def test_fp32_fwd_policies_vs_oracle(torch_dev, policy, causal):
+    """fp32 forward kernels (the reference's precision): 0 default (register-Q ring, paired
+    query blocks when causal), 109 two-barrier kernel, 110 ring unpaired, 111 ring paired;
+    odd query-block counts (N = 777), a single block, d = 32, at the fp32 bound 1e-5."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(43)
+    try:
+        _hip.set_policy(policy)
+        for (B, H, N, d) in ((1, 2, 1024, 64), (1, 1, 777, 64), (2, 1, 200, 32), (1, 1, 64, 64),
+                             (1, 3, 384, 48)):
+            q, k, v = (rng.standard_normal((B, H, N, d)).astype(np.float32) for _ in range(3))
+            o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.float32) for x in (q, k, v)), causal)
+            torch.cuda.synchronize()
+            o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
+            np.testing.assert_allclose(_np(o), o_ref, atol=1e-5, rtol=0, err_msg=str((B, H, N, d)))
+            _check_ml(_np(m), _np(l), m_ref, l_ref, exact=True)
+    finally:
+        _hip.set_policy(0)
+
+
 @pytest.mark.parametrize("policy", (0, 40, 43, 62, 66, 69, 70, 71, 72, 73, 74, 75, 77, 107, 108))
 @pytest.mark.parametrize("causal", [False, True])
 def test_bf16_bwd_policies_vs_oracle(torch_dev, policy, causal):
