@@ -392,6 +392,12 @@ def extra_legs(torch, _hip, time_fn):
                                             dv=g2[2], workspace=ws2), 10, 2)
     extra["c2_fp32_bwd_ms"] = round(c2b_ms, 4)
     extra["c2_fp32_bwd_tflops"] = round(2.5 * fwd_flops(*c2) / (c2b_ms * 1e-3) / 1e12, 2)
+    # the causal fp32 pair minitorch's decoder self-attention runs (flash_attention_causal_*)
+    c2c_ms = time_fn(lambda: _hip.flash_fwd(q2, k2, v2, True, out=o2, m=m2, l=l2), 20, 3)
+    extra["c2_fp32_causal_fwd_ms"] = round(c2c_ms, 4)
+    c2cb_ms = time_fn(lambda: _hip.flash_bwd(q2, k2, v2, o2, do2, m2, l2, True, dq=g2[0], dk=g2[1],
+                                             dv=g2[2], workspace=ws2), 10, 2)
+    extra["c2_fp32_causal_bwd_ms"] = round(c2cb_ms, 4)
     del q2, k2, v2, do2, o2, m2, l2, ws2, g2
     # config 4's per-GPU shard at 8 GPUs: (8,16,16384,128) bf16 forward (1/8 of B = 64)
     c4 = (8, 16, 16384, 128)

@@ -202,6 +202,8 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
 // PAIR: a workgroup runs query blocks u and nqb - 1 - u of one head in turn (causal: a
 // light and a heavy block, every workgroup walks nqb + 1 key-tile pairs' worth; non-causal:
 // half the workgroups, each filling the ring for its second block while it drains the first).
+// (32-key slots at four workgroups per CU, 128 VGPRs with 9 spilled, measured 4.8 % slower
+// non-causal and 22 % slower causal: profiles/r2m_ab_fp32_fwd_ring32.txt; not kept.)
 template <typename T, int DT, int KB, bool CAUSAL, bool PAIR>
 __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
   constexpr int BQ = 128, BK = 32 * KB;
