@@ -397,10 +397,10 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
                                       pol == kPolFwdF32TwoBarrier ? 0
                                       : pol == kPolFwdF32Ring     ? 1
                                       : pol == kPolFwdF32RingPair ? 2
-                                      // default: the paired ring when causal (C2 causal 0.317 ->
-                                      // 0.192 ms), the two-barrier kernel otherwise (0.3228 vs
-                                      // 0.3256 ms, profiles/r2m_ab_fp32_fwd.txt)
-                                      : causal ? 2 : 0),
+                                      // default: the ring, paired on large grids (C2 0.3209 ->
+                                      // 0.2775 ms, causal 0.317 -> 0.163 ms,
+                                      // profiles/r2m_ab_fp32_fwd_ring2.txt)
+                                      : 3),
                    "mt_flash_attn_fwd");
 }
 

@@ -225,8 +225,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
   const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
   const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
   const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
-  const int dpad = (d + 15) & ~15;
-  const int ksteps = dpad / 16;
   constexpr int EPC = 16 / sizeof(T), CPR = DT / EPC, NCK = BK * CPR / 256;
 #pragma nounroll
   for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
@@ -297,34 +295,45 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
       f32x16 S[KB];
 #pragma unroll
       for (int i = 0; i < KB; ++i) S[i] = f32x16{};
-      for (int ks = 0; ks < ksteps; ++ks) {
+      // all DT / 16 k-steps, unrolled: bq[] indexed by a constant (a runtime index makes hipcc
+      // move each fragment through s_set_gpr_idx, and a runtime trip count copies S between
+      // branches); columns past d are zero in both Q and K, so they add nothing
+#pragma unroll
+      for (int ks = 0; ks < DT / 16; ++ks) {
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
           Frag<T> ak = row_frag<T>(sK + (kb * 32 + c32) * LD + ks * 16 + 8 * hf);
           mma(S[kb], ak, bq[ks]);
         }
       }
+      // masks only on the ragged last tile and on tiles that reach past the wave's first
+      // query (causal); the row max is taken on the raw scores (the scale c2 > 0), and
+      // exp2(c2·s − m) is one fma into one v_exp_f32
+      const float c2 = p.scale_log2;
+      if (k0 + BK > N || (CAUSAL && k0 + BK - 1 > q0 + wave * 32)) {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kb * 32 + acc_row(r, hf);
+            if (key >= N || (CAUSAL && key > my_q)) S[kb][r] = -INFINITY;
+          }
+      }
       float smax = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = k0 + kb * 32 + acc_row(r, hf);
-          float x = S[kb][r] * p.scale_log2;
-          if (key >= N || (CAUSAL && key > my_q)) x = -INFINITY;
-          S[kb][r] = x;
-          smax = fmaxf(smax, x);
-        }
+        for (int r = 0; r < 16; ++r) smax = fmaxf(smax, S[kb][r]);
       smax = fmaxf(smax, __shfl_xor(smax, 32));
-      const float m_new = fmaxf(m_run, smax);
+      const float m_new = fmaxf(m_run, smax * c2);
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_run - m_use);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
       float rs = 0.f;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = exp2f(S[kb][r] - m_use);
+          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(S[kb][r], c2, -m_use));
           S[kb][r] = e;
           rs += e;
         }
@@ -416,9 +425,10 @@ static hipError_t dispatch_fwd_generic(const AttnArgs& a, bool vec, bool causal,
 hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st, int ring) {
   // fp32 with 16-B rows and d <= 64 (one d-chunk): the register-Q / two-slot ring kernel;
-  // ring = 1 unpaired, 2 paired query blocks, 3 paired when causal (0: fa_fwd_generic)
+  // ring = 1 unpaired, 2 paired query blocks, 3 paired when the paired grid keeps two
+  // workgroups per CU (0: fa_fwd_generic)
   if (ring && vec && !bf16_io && a.d <= 64) {
-    const bool pair = ring == 2 || (ring == 3 && causal);
+    const bool pair = ring == 2 || (ring == 3 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
     if (causal)
       return pair ? launch_fwd_ring_t<float, 64, 2, true, true>(a, st)
                   : launch_fwd_ring_t<float, 64, 2, true, false>(a, st);
