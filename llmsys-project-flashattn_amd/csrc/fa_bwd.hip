@@ -170,31 +170,41 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
       }
       __syncthreads();
       const int ksteps = min(DT, dpad - c * DT) / 16;
-      if (active) {
-        for (int ks = 0; ks < ksteps; ++ks) {
-          const int col = ks * 16 + 8 * hf;
-          Frag<T> bk = row_frag<T>(sK + (wave * 32 + c32) * LD + col);
-          Frag<T> bv = row_frag<T>(sV + (wave * 32 + c32) * LD + col);
+      auto kstep = [&](int ks) __attribute__((always_inline)) {
+        const int col = ks * 16 + 8 * hf;
+        Frag<T> bk = row_frag<T>(sK + (wave * 32 + c32) * LD + col);
+        Frag<T> bv = row_frag<T>(sV + (wave * 32 + c32) * LD + col);
 #pragma unroll
-          for (int qb = 0; qb < QB; ++qb) {
-            Frag<T> aq = row_frag<T>(sQ + (qb * 32 + c32) * LD + col);
-            Frag<T> ao = row_frag<T>(sO + (qb * 32 + c32) * LD + col);
-            mma(S[qb], aq, bk);
-            mma(dP[qb], ao, bv);
-          }
+        for (int qb = 0; qb < QB; ++qb) {
+          Frag<T> aq = row_frag<T>(sQ + (qb * 32 + c32) * LD + col);
+          Frag<T> ao = row_frag<T>(sO + (qb * 32 + c32) * LD + col);
+          mma(S[qb], aq, bk);
+          mma(dP[qb], ao, bv);
+        }
+      };
+      if (active) {
+        if (pref) {  // one zero-padded d-chunk: all DT / 16 k-steps, unrolled
+#pragma unroll
+          for (int ks = 0; ks < DT / 16; ++ks) kstep(ks);
+        } else {
+          for (int ks = 0; ks < ksteps; ++ks) kstep(ks);
         }
       }
     }
     // Row c32-lane holds S[q][my_k] for q = qt + qb*32 + acc_row(r, hf).
     if (active) {
+      // p = exp2(c2·s − lse2): one fma into one v_exp_f32; masks only on tiles that reach
+      // past N or below the wave's keys (causal)
+      const float c2 = p.scale_log2;
+      const bool msk = qt + BQ > N || k0 + BKV > N || (CAUSAL && qt < wave_kmin + 31);
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ql = qb * 32 + acc_row(r, hf);
           const int q = qt + ql;
-          float pv = exp2f(S[qb][r] * p.scale_log2 - sLse[ql]);
-          if (q >= N || my_k >= N || (CAUSAL && my_k > q)) pv = 0.f;
+          float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[qb][r], c2, -sLse[ql]));
+          if (msk && (q >= N || my_k >= N || (CAUSAL && my_k > q))) pv = 0.f;
           S[qb][r] = pv;
           dP[qb][r] = pv * (dP[qb][r] - sDel[ql]);
         }
@@ -348,29 +358,37 @@ __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
       }
       __syncthreads();
       const int ksteps = min(DT, dpad - c * DT) / 16;
-      if (active) {
-        for (int ks = 0; ks < ksteps; ++ks) {
-          const int col = ks * 16 + 8 * hf;
-          Frag<T> bq = row_frag<T>(sQ + (wave * 32 + c32) * LD + col);
-          Frag<T> bo = row_frag<T>(sO + (wave * 32 + c32) * LD + col);
+      auto kstep = [&](int ks) __attribute__((always_inline)) {
+        const int col = ks * 16 + 8 * hf;
+        Frag<T> bq = row_frag<T>(sQ + (wave * 32 + c32) * LD + col);
+        Frag<T> bo = row_frag<T>(sO + (wave * 32 + c32) * LD + col);
 #pragma unroll
-          for (int kb = 0; kb < KB; ++kb) {
-            Frag<T> ak = row_frag<T>(sK + (kb * 32 + c32) * LD + col);
-            Frag<T> av = row_frag<T>(sV + (kb * 32 + c32) * LD + col);
-            mma(S[kb], ak, bq);
-            mma(dP[kb], av, bo);
-          }
+        for (int kb = 0; kb < KB; ++kb) {
+          Frag<T> ak = row_frag<T>(sK + (kb * 32 + c32) * LD + col);
+          Frag<T> av = row_frag<T>(sV + (kb * 32 + c32) * LD + col);
+          mma(S[kb], ak, bq);
+          mma(dP[kb], av, bo);
+        }
+      };
+      if (active) {
+        if (pref) {  // one zero-padded d-chunk: all DT / 16 k-steps, unrolled
+#pragma unroll
+          for (int ks = 0; ks < DT / 16; ++ks) kstep(ks);
+        } else {
+          for (int ks = 0; ks < ksteps; ++ks) kstep(ks);
         }
       }
     }
     if (active) {
+      const float c2 = p.scale_log2;
+      const bool msk = k0 + BK > N || (CAUSAL && k0 + BK - 1 > q0 + wave * 32);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = k0 + kb * 32 + acc_row(r, hf);
-          float pv = exp2f(S[kb][r] * p.scale_log2 - lse_q);
-          if (key >= N || (CAUSAL && key > my_q)) pv = 0.f;
+          float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[kb][r], c2, -lse_q));
+          if (msk && (key >= N || (CAUSAL && key > my_q))) pv = 0.f;
           dP[kb][r] = pv * (dP[kb][r] - del_q);
         }
     }
