@@ -28,7 +28,7 @@ hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hip
                            bool* handled, int pair = 0);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
-                              hipStream_t st, int pair);
+                              hipStream_t st, int pair, bool ring);
 #ifdef MT_DIAGNOSTICS
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 #endif
@@ -104,6 +104,7 @@ enum : int {
   // generic (fp32) causal backward: 112 unpaired, 113 always paired (default: paired on
   // grids that keep two paired workgroups per CU)
   kPolBwdGenNoPair = 112, kPolBwdGenPair = 113,
+  kPolBwdF32Lds = 114,  // fp32 backward: fa_bwd.hip's LDS-row kernels instead of the register-row ring
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -113,7 +114,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -466,7 +467,8 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }
   return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream,
-                                      pol == kPolBwdGenNoPair ? 0 : pol == kPolBwdGenPair ? 1 : 2),
+                                      pol == kPolBwdGenNoPair ? 0 : pol == kPolBwdGenPair ? 1 : 2,
+                                      pol != kPolBwdF32Lds),
                    "mt_flash_attn_bwd");
 }
 

@@ -8,8 +8,8 @@ timeout -k 10 600 python -u -m pytest tests/test_flash_gpu.py tests/test_minitor
 rc=$?
 tail -3 gpurun_out/tests_$TAG.log
 [ $rc -eq 0 ] || exit $rc
-SHAPE=8,16,1024,64 DTYPE=fp32 timeout -k 10 300 python scripts/ablate_bwd.py 0,112 causal > gpurun_out/ab_$TAG.txt 2>&1 \
- && SHAPE=8,16,1024,64 DTYPE=fp32 timeout -k 10 300 python scripts/ablate_bwd.py 0 >> gpurun_out/ab_$TAG.txt 2>&1 \
+SHAPE=8,16,1024,64 DTYPE=fp32 timeout -k 10 300 python scripts/ablate_bwd.py 0,114 causal > gpurun_out/ab_$TAG.txt 2>&1 \
+ && SHAPE=8,16,1024,64 DTYPE=fp32 timeout -k 10 300 python scripts/ablate_bwd.py 0,114 >> gpurun_out/ab_$TAG.txt 2>&1 \
  && SHAPE=8,16,4096,128 timeout -k 10 300 python scripts/ablate_bwd.py 0 causal >> gpurun_out/ab_$TAG.txt 2>&1
 rc=$?
 cat gpurun_out/ab_$TAG.txt

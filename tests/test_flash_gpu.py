@@ -478,12 +478,14 @@ def test_spiked_rescale(torch_dev, policy, d):
         _hip.set_policy(0)
 
 
-@pytest.mark.parametrize("policy", (0, 112, 113))
+@pytest.mark.parametrize("policy", (0, 112, 113, 114))
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_generic_causal_bwd_pairing_vs_oracle(torch_dev, policy, dtype):
-    """Generic causal backward (fp32; bf16 at d != 64): 0 default, 112 unpaired, 113 paired
-    light/heavy key and query blocks; odd block counts (N = 777: 7 blocks of 128), one
-    block (N = 100), d = 48 / 128, against the oracle at the fp32 gradient bound."""
+@pytest.mark.parametrize("causal", [True, False])
+def test_generic_causal_bwd_pairing_vs_oracle(torch_dev, policy, dtype, causal):
+    """Generic backward (fp32; bf16 at d != 64): 0 default (fp32 d <= 64: the register-row
+    ring kernels), 112 unpaired, 113 paired light/heavy key and query blocks, 114 the LDS-row
+    kernels; odd block counts (N = 777: 7 blocks of 128), one block (N = 100), d = 48 / 128,
+    against the oracle at the fp32 gradient bound."""
     from minitorch import _hip
     torch = torch_dev
     rng = np.random.default_rng(47)
@@ -495,11 +497,11 @@ def test_generic_causal_bwd_pairing_vs_oracle(torch_dev, policy, dtype):
             if dtype == "bf16":
                 q, k, v, do = (A.bf16_round(x) for x in (q, k, v, do))
             tq, tk, tv, tdo = (_dev(torch, x, tdt) for x in (q, k, v, do))
-            o, m, l = _hip.flash_fwd(tq, tk, tv, True)
-            dq, dk, dv = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, True)
+            o, m, l = _hip.flash_fwd(tq, tk, tv, causal)
+            dq, dk, dv = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, causal)
             torch.cuda.synchronize()
-            o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, True)
-            refs = A.attention_bwd(q, k, v, o_ref, do, m_ref, l_ref, True)
+            o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
+            refs = A.attention_bwd(q, k, v, o_ref, do, m_ref, l_ref, causal)
             scale = max(1.0, *(float(np.abs(r).max()) for r in refs))
             tol = (2e-5 if dtype == "fp32" else 6e-2) * scale
             for got, ref, name in zip((dq, dk, dv), refs, ("dq", "dk", "dv")):
