@@ -40,15 +40,20 @@ def _i64_cached(vals: tuple) -> ctypes.Array:
 
 def _i64(vals) -> ctypes.Array:
     """int64 array argument; shapes/strides repeat every step, so the ctypes arrays are
-    cached by value (the callee only reads them)."""
-    return _i64_cached(tuple(int(v) for v in vals))
+    cached by value (the callee only reads them). TensorData already holds them as tuples
+    of Python ints, which go to the cache as they are."""
+    if type(vals) is not tuple:
+        vals = tuple(int(v) for v in vals)
+    return _i64_cached(vals)
 
 
 def _out(like: Tensor, shape) -> Tensor:
     """Uninitialised dense fp32 device output (every kernel below writes all of it)."""
     import torch
     shape = tuple(int(s) for s in shape)
-    size = int(np.prod(shape)) if shape else 1
+    size = 1
+    for s in shape:
+        size *= s
     st = torch.empty(size, dtype=torch.float32, device="cuda")
     return Tensor(TensorData(st, shape), backend=like.backend)
 

@@ -88,12 +88,24 @@ class TensorData:
         strides = tuple(int(s) for s in strides)
         if len(strides) != len(shape):
             raise IndexingError(f"Len of strides {strides} must match {shape}.")
-        self._shape = np.array(shape, dtype=np.int64)
-        self._strides = np.array(strides, dtype=np.int64)
         self.shape = shape
         self.strides = strides
         self.dims = len(shape)
-        self.size = int(np.prod(shape)) if shape else 1
+        size = 1
+        for s in shape:
+            size *= s
+        self.size = size
+
+    # NumPy forms of shape / strides, built on first use (the index helpers and the CPU
+    # backend take them); the device path never needs them, and building two arrays per
+    # tensor was a measurable share of minitorch's per-op host time in the config-5 step
+    @property
+    def _shape(self) -> np.ndarray:
+        return np.array(self.shape, dtype=np.int64)
+
+    @property
+    def _strides(self) -> np.ndarray:
+        return np.array(self.strides, dtype=np.int64)
 
     # ---- placement --------------------------------------------------------------
     @property
@@ -126,7 +138,7 @@ class TensorData:
     # ---- layout -----------------------------------------------------------------
     def is_contiguous(self) -> bool:
         last = None
-        for st in self._strides:
+        for st in self.strides:
             if last is not None and st > last:
                 return False
             last = st
