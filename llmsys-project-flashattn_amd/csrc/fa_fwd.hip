@@ -133,13 +133,13 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
       smax = fmaxf(smax, __shfl_xor(smax, 32));
       const float m_new = fmaxf(m_run, smax);
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_run - m_use);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
       float rs = 0.f;
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = exp2f(S[kb][r] - m_use);
+          const float e = __builtin_amdgcn_exp2f(S[kb][r] - m_use);
           S[kb][r] = e;
           rs += e;
         }
