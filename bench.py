@@ -408,7 +408,48 @@ def extra_legs(torch, _hip, time_fn):
     c4_ms = time_fn(lambda: _hip.flash_fwd(q4, k4, v4, False, out=o4, m=m4, l=l4), 5, 1)
     extra["c4_shard_bf16_fwd_ms"] = round(c4_ms, 3)
     extra["c4_shard_bf16_fwd_tflops"] = round(fwd_flops(*c4) / (c4_ms * 1e-3) / 1e12, 2)
+    del q4, k4, v4, o4, m4, l4
+    try:  # a side leg: a failure here is reported, it does not void the headline line
+        extra.update(c5_step_leg(torch))
+    except Exception as e:  # noqa: BLE001
+        extra["c5_error"] = repr(e)[:200]
     return extra
+
+
+def c5_step_leg(torch, steps: int = 10) -> dict:
+    """Config 5: one DecoderLM training step (forward, backward, Adam) of the reference's
+    machine-translation setup (project/run_machine_translation.py:397-407: vocab 10000,
+    n_embd 256, 8 heads, batch 128, seq 39) on the HIP backend with fused LayerNorm + softmax
+    and flash attention, synthetic tokens, random init (scripts/mt_step_bench.py, same setup).
+    Host-bound in minitorch's Python autodiff; reported beside the kernels, not the headline."""
+    import numpy as np
+    import minitorch
+    B, T, V, E, H = 128, 39, 10000, 256, 8
+    backend = minitorch.TensorBackend(minitorch.HipKernelOps)
+    rng = np.random.default_rng(0)
+    lm = minitorch.DecoderLM(n_vocab=V, n_embd=E, n_head=H, n_positions=40, p_dropout=0.1,
+                             backend=backend, use_fused_kernel=True, use_flash_attention=True)
+    opt = minitorch.Adam(lm.parameters(), lr=1e-4)
+    x = minitorch.tensor_from_numpy(rng.integers(0, V, (B, T)).astype(np.float32), backend)
+    y = minitorch.tensor_from_numpy(rng.integers(0, V, (B * T,)).astype(np.float32), backend)
+
+    def step():
+        opt.zero_grad()
+        loss = minitorch.softmax_loss(lm(x).view(B * T, V), y).sum() / (B * T)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"c5_step_ms": round(ms, 2), "c5_tokens_per_s": round(B * T / ms * 1e3, 1),
+            "c5_loss": round(float(loss.item()), 4)}
 
 
 def parse_args(argv=None):
