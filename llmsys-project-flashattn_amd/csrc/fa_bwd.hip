@@ -22,17 +22,6 @@
 
 namespace mt {
 
-// XCD-aware block order for the (blocks per head, B·H) grids below: the grid's (x, y) is
-// flattened and dealt out so that the blocks of one (b,h) run on one XCD and share its L2.
-__device__ __forceinline__ void xcd_order(int& blk, int& bh) {
-  const int nx = gridDim.x, nblk = gridDim.x * gridDim.y;
-  const int hw = blockIdx.y * nx + blockIdx.x;
-  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
-  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  blk = logical % nx;
-  bh = logical / nx;
-}
-
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void fa_bwd_prep(AttnArgs p) {

@@ -21,15 +21,6 @@ namespace {
 constexpr int kDT = 64, kLD = kDT + 4;  // fp32 rows padded by 16 B
 constexpr int kCPR = kDT / 4;           // 16-B chunks per row
 
-__device__ __forceinline__ void ring_xcd_order(int& blk, int& bh) {
-  const int nx = gridDim.x, nblk = gridDim.x * gridDim.y;
-  const int hw = blockIdx.y * nx + blockIdx.x;
-  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
-  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  blk = logical % nx;
-  bh = logical / nx;
-}
-
 // the four k-step fragments of row r (zero past d, which is a multiple of 4 here)
 __device__ __forceinline__ void row_frags(f32x8 (&f)[4], const float* row, int d, int hf) {
 #pragma unroll
@@ -57,7 +48,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
   int ublk, bh;
-  ring_xcd_order(ublk, bh);
+  xcd_order(ublk, bh);
   const int b = bh / p.H, hh = bh % p.H;
   const int nkb = (N + BKV - 1) / BKV;
   const float* Qg = (const float*)p.q + b * p.sq[0] + hh * p.sq[1];
@@ -200,7 +191,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
   int ublk, bh;
-  ring_xcd_order(ublk, bh);
+  xcd_order(ublk, bh);
   const int b = bh / p.H, hh = bh % p.H;
   const int nqb = (N + BQ - 1) / BQ;
   const float* Qg = (const float*)p.q + b * p.sq[0] + hh * p.sq[1];

@@ -153,6 +153,18 @@ __device__ __forceinline__ void stage_tile(T* lds, int ld, const T* g, int64_t g
   }
 }
 
+// XCD-aware block order for (blocks per head, B·H) grids: the grid's (x, y) is flattened
+// and dealt out so that the blocks of one (b,h) run on one XCD and share its L2 (the
+// hardware hands consecutive workgroups to the 8 XCDs in turn).
+__device__ __forceinline__ void xcd_order(int& blk, int& bh) {
+  const int nx = gridDim.x, nblk = gridDim.x * gridDim.y;
+  const int hw = blockIdx.y * nx + blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
+  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
+  blk = logical % nx;
+  bh = logical / nx;
+}
+
 // Parameters shared by the forward / backward launches (all strides in elements;
 // the head dimension d is always unit-stride).
 struct AttnArgs {

@@ -216,12 +216,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
-  const int ngx = gridDim.x, nbh = gridDim.y;
-  const int hw = blockIdx.y * ngx + blockIdx.x, nblk = ngx * nbh;
-  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
-  const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  const int u = logical % ngx, nqb = (N + BQ - 1) / BQ;
-  const int bh = logical / ngx, b = bh / p.H, hh = bh % p.H;
+  int u, bh;
+  xcd_order(u, bh);
+  const int nqb = (N + BQ - 1) / BQ;
+  const int b = bh / p.H, hh = bh % p.H;
   const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
   const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
   const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
