@@ -427,6 +427,12 @@ hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
   // workgroups per CU (0: fa_fwd_generic)
   if (ring && vec && !bf16_io && a.d <= 64) {
     const bool pair = ring == 2 || (ring == 3 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
+    if (a.d <= 32)  // 32-column tiles: no zero-padded half of the QKᵀ and PV work (minitorch's
+                    // MHA at config 5 has d = 256 / 8 = 32)
+      return causal ? (pair ? launch_fwd_ring_t<float, 32, 2, true, true>(a, st)
+                            : launch_fwd_ring_t<float, 32, 2, true, false>(a, st))
+                    : (pair ? launch_fwd_ring_t<float, 32, 2, false, true>(a, st)
+                            : launch_fwd_ring_t<float, 32, 2, false, false>(a, st));
     if (causal)
       return pair ? launch_fwd_ring_t<float, 64, 2, true, true>(a, st)
                   : launch_fwd_ring_t<float, 64, 2, true, false>(a, st);
