@@ -18,13 +18,11 @@ namespace mt {
 
 namespace {
 
-constexpr int kDT = 64, kLD = kDT + 4;  // fp32 rows padded by 16 B
-constexpr int kCPR = kDT / 4;           // 16-B chunks per row
-
-// the four k-step fragments of row r (zero past d, which is a multiple of 4 here)
-__device__ __forceinline__ void row_frags(f32x8 (&f)[4], const float* row, int d, int hf) {
+// the KS k-step fragments of row r (zero past d, which is a multiple of 4 here)
+template <int KS>
+__device__ __forceinline__ void row_frags(f32x8 (&f)[KS], const float* row, int d, int hf) {
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
+  for (int ks = 0; ks < KS; ++ks) {
     uint4 ch[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -39,8 +37,10 @@ __device__ __forceinline__ void row_frags(f32x8 (&f)[4], const float* row, int d
 
 // dK, dV: grid (nkb or ceil(nkb / 2) when PAIR, B*H); 4 waves x 32 keys; Q/dO tiles of 32
 // queries (with their lse2 / delta) streamed through the ring.
-template <bool CAUSAL, bool PAIR>
+template <int DT, bool CAUSAL, bool PAIR>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
+  // DT = 64, or 32 for d <= 32; rows padded by 16 B; NCK 16-B chunks per thread per 32-row tile
+  constexpr int kLD = DT + 4, kCPR = DT / 4, NCK = 32 * kCPR / 256, KS = DT / 16, NDB = DT / 32;
   constexpr int BKV = 128, BQ = 32;
   constexpr int SLOT = 2 * BQ * kLD + 2 * BQ;  // Q, dO, lse2, delta (floats)
   extern __shared__ __attribute__((aligned(16))) float ring[];
@@ -69,21 +69,23 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
     const int k0 = kblk * BKV;
     const int my_k = k0 + wave * 32 + c32;
     const int wave_kmin = k0 + wave * 32;
-    f32x8 bk[4], bv[4];
+    f32x8 bk[KS], bv[KS];
     {
       const int kr = min(my_k, N - 1);
       row_frags(bk, Kg + (int64_t)kr * p.sk[2], d, hf);
       row_frags(bv, Vg + (int64_t)kr * p.sv[2], d, hf);
     }
-    f32x16 dK[2] = {f32x16{}, f32x16{}}, dV[2] = {f32x16{}, f32x16{}};
+    f32x16 dK[NDB], dV[NDB];
+#pragma unroll
+    for (int i = 0; i < NDB; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
 
     const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of BQ
     const int ntile = N > qstart ? (N - qstart + BQ - 1) / BQ : 0;
-    uint4 pq[2], po[2];
+    uint4 pq[NCK], po[NCK];
     float pl = 0.f, pd = 0.f;
     auto pre_load = [&](int qt) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NCK; ++i) {
         const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * 4, gr = qt + r;
         pq[i] = po[i] = make_uint4(0, 0, 0, 0);
         if (gr < N && cc < d) {
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
       float* sQ = ring + s * SLOT;
       float* sO = sQ + BQ * kLD;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NCK; ++i) {
         const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * 4;
         *(uint4*)(sQ + r * kLD + cc) = pq[i];
         *(uint4*)(sO + r * kLD + cc) = po[i];
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
         // Sᵀ and dPᵀ: the lane's column is key my_k, rows are queries qt + acc_row(r, hf)
         f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
+        for (int ks = 0; ks < KS; ++ks) {
           const int col = ks * 16 + 8 * hf;
           mma(S, row_frag<float>(sQ + c32 * kLD + col), bk[ks]);
           mma(dP, row_frag<float>(sO + c32 * kLD + col), bv[ks]);
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
         for (int s = 0; s < 2; ++s) {
           const f32x8 bp = acc_frag<float>(S, s), bs = acc_frag<float>(dP, s);
 #pragma unroll
-          for (int db = 0; db < 2; ++db) {
+          for (int db = 0; db < NDB; ++db) {
             mma(dV[db], col_frag<float>(sO, kLD, 16 * s + 4 * hf, db * 32, lane), bp);
             mma(dK[db], col_frag<float>(sQ, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
           }
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
       float* dVg = (float*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
       const float sc = p.scale;
 #pragma unroll
-      for (int db = 0; db < 2; ++db)
+      for (int db = 0; db < NDB; ++db)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int col = db * 32 + 8 * g + 4 * hf;
@@ -182,8 +184,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
 
 // dQ: grid (nqb or ceil(nqb / 2) when PAIR, B*H); 4 waves x 32 queries; K/V tiles of 32
 // keys streamed through the ring.
-template <bool CAUSAL, bool PAIR>
+template <int DT, bool CAUSAL, bool PAIR>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
+  // DT = 64, or 32 for d <= 32; rows padded by 16 B; NCK 16-B chunks per thread per 32-row tile
+  constexpr int kLD = DT + 4, kCPR = DT / 4, NCK = 32 * kCPR / 256, KS = DT / 16, NDB = DT / 32;
   constexpr int BQ = 128, BK = 32;
   constexpr int SLOT = 2 * BK * kLD;  // K, V (floats)
   extern __shared__ __attribute__((aligned(16))) float ring[];
@@ -210,7 +214,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
     const int q0 = qblk * BQ;
     const int my_q = q0 + wave * 32 + c32;
     const int wave_qmax = q0 + wave * 32 + 31;
-    f32x8 bq[4], bo[4];
+    f32x8 bq[KS], bo[KS];
     float lse_q, del_q;
     {
       const int qr = min(my_q, N - 1);
@@ -219,14 +223,16 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
       lse_q = p.lse2[(int64_t)bh * N + qr];
       del_q = p.delta[(int64_t)bh * N + qr];
     }
-    f32x16 dQ[2] = {f32x16{}, f32x16{}};
+    f32x16 dQ[NDB];
+#pragma unroll
+    for (int i = 0; i < NDB; ++i) dQ[i] = f32x16{};
 
     const int kend = CAUSAL ? min(N, q0 + BQ) : N;
     const int ntile = (kend + BK - 1) / BK;
-    uint4 pk[2], pv[2];
+    uint4 pk[NCK], pv[NCK];
     auto pre_load = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NCK; ++i) {
         const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * 4, gr = k0 + r;
         pk[i] = pv[i] = make_uint4(0, 0, 0, 0);
         if (gr < N && cc < d) {
@@ -239,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
       float* sK = ring + s * SLOT;
       float* sV = sK + BK * kLD;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NCK; ++i) {
         const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * 4;
         *(uint4*)(sK + r * kLD + cc) = pk[i];
         *(uint4*)(sV + r * kLD + cc) = pv[i];
@@ -260,7 +266,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
         // S and dP with the query on the lane: rows are keys k0 + acc_row(r, hf)
         f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
+        for (int ks = 0; ks < KS; ++ks) {
           const int col = ks * 16 + 8 * hf;
           mma(S, row_frag<float>(sK + c32 * kLD + col), bq[ks]);
           mma(dP, row_frag<float>(sV + c32 * kLD + col), bo[ks]);
@@ -277,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
         for (int s = 0; s < 2; ++s) {
           const f32x8 bs = acc_frag<float>(dP, s);
 #pragma unroll
-          for (int db = 0; db < 2; ++db)
+          for (int db = 0; db < NDB; ++db)
             mma(dQ[db], col_frag<float>(sK, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
         }
       }
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
       float* dQg = (float*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)my_q * p.sdq[2];
       const float sc = p.scale;
 #pragma unroll
-      for (int db = 0; db < 2; ++db)
+      for (int db = 0; db < NDB; ++db)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int col = db * 32 + 8 * g + 4 * hf;
@@ -304,13 +310,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
   }
 }
 
-template <bool CAUSAL, bool PAIR>
+template <int DT, bool CAUSAL, bool PAIR>
 static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
+  constexpr int kLD = DT + 4;
   const unsigned bhn = (unsigned)(a.B * a.H);
   {
     const int nkb = (a.N + 127) / 128;
     const size_t smem = sizeof(float) * (size_t)(2 * (2 * 32 * kLD + 2 * 32));
-    auto kfn = fa_bwd_dkv_ring<CAUSAL, PAIR>;
+    auto kfn = fa_bwd_dkv_ring<DT, CAUSAL, PAIR>;
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)smem);
     if (e != hipSuccess) return e;
@@ -321,7 +328,7 @@ static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
   {
     const int nqb = (a.N + 127) / 128;
     const size_t smem = sizeof(float) * (size_t)(2 * 2 * 32 * kLD);
-    auto kfn = fa_bwd_dq_ring<CAUSAL, PAIR>;
+    auto kfn = fa_bwd_dq_ring<DT, CAUSAL, PAIR>;
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)smem);
     if (e != hipSuccess) return e;
@@ -331,10 +338,16 @@ static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
 }
 
 // fp32, d <= 64, 16-B rows; the caller has run the prep kernel (lse2, delta).
-hipError_t launch_bwd_ring(const AttnArgs& a, bool causal, bool pair, hipStream_t st) {
+template <int DT>
+static hipError_t launch_bwd_ring_d(const AttnArgs& a, bool causal, bool pair, hipStream_t st) {
   if (causal)
-    return pair ? launch_bwd_ring_t<true, true>(a, st) : launch_bwd_ring_t<true, false>(a, st);
-  return pair ? launch_bwd_ring_t<false, true>(a, st) : launch_bwd_ring_t<false, false>(a, st);
+    return pair ? launch_bwd_ring_t<DT, true, true>(a, st) : launch_bwd_ring_t<DT, true, false>(a, st);
+  return pair ? launch_bwd_ring_t<DT, false, true>(a, st) : launch_bwd_ring_t<DT, false, false>(a, st);
+}
+
+hipError_t launch_bwd_ring(const AttnArgs& a, bool causal, bool pair, hipStream_t st) {
+  // d <= 32 (minitorch's MHA at config 5): 32-column tiles, no zero-padded half
+  return a.d <= 32 ? launch_bwd_ring_d<32>(a, causal, pair, st) : launch_bwd_ring_d<64>(a, causal, pair, st);
 }
 
 }  // namespace mt

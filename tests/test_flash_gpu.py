@@ -492,7 +492,8 @@ def test_generic_causal_bwd_pairing_vs_oracle(torch_dev, policy, dtype, causal):
     tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
     try:
         _hip.set_policy(policy)
-        for (B, H, N, d) in ((1, 2, 1024, 64), (1, 1, 777, 64), (1, 1, 100, 48), (1, 2, 640, 128)):
+        for (B, H, N, d) in ((1, 2, 1024, 64), (1, 1, 777, 64), (1, 1, 100, 48), (1, 2, 640, 128),
+                             (2, 1, 333, 32), (1, 2, 256, 16)):
             q, k, v, do = (rng.standard_normal((B, H, N, d)).astype(np.float32) for _ in range(4))
             if dtype == "bf16":
                 q, k, v, do = (A.bf16_round(x) for x in (q, k, v, do))
