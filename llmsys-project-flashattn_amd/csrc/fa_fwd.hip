@@ -425,6 +425,20 @@ hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
   // fp32 with 16-B rows and d <= 64 (one d-chunk): the register-Q / two-slot ring kernel;
   // ring = 1 unpaired, 2 paired query blocks, 3 paired when the paired grid keeps two
   // workgroups per CU (0: fa_fwd_generic)
+  // bf16 reaches this function only for head dims the MFMA fast paths do not take (d != 64,
+  // 128) or strided rows; d < 64 with 16-B rows takes the same ring kernel
+  if (ring && vec && bf16_io && a.d < 64) {
+    const bool pair = ring == 2 || (ring == 3 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
+    if (a.d <= 32)
+      return causal ? (pair ? launch_fwd_ring_t<bf16, 32, 2, true, true>(a, st)
+                            : launch_fwd_ring_t<bf16, 32, 2, true, false>(a, st))
+                    : (pair ? launch_fwd_ring_t<bf16, 32, 2, false, true>(a, st)
+                            : launch_fwd_ring_t<bf16, 32, 2, false, false>(a, st));
+    return causal ? (pair ? launch_fwd_ring_t<bf16, 64, 2, true, true>(a, st)
+                          : launch_fwd_ring_t<bf16, 64, 2, true, false>(a, st))
+                  : (pair ? launch_fwd_ring_t<bf16, 64, 2, false, true>(a, st)
+                          : launch_fwd_ring_t<bf16, 64, 2, false, false>(a, st));
+  }
   if (ring && vec && !bf16_io && a.d <= 64) {
     const bool pair = ring == 2 || (ring == 3 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
     if (a.d <= 32)  // 32-column tiles: no zero-padded half of the QKᵀ and PV work (minitorch's

@@ -85,6 +85,8 @@ CASES = [
     (1, 1, 130, 200, False),
     (1, 1, 70, 256, True),
     (1, 1, 33, 20, False),
+    (1, 2, 300, 48, False),   # d < 64 with 16-B rows: the ring forward (fp32 and bf16)
+    (2, 1, 1000, 32, True),   # 32-column ring tiles, paired causal blocks, ragged tail
 ]
 
 
