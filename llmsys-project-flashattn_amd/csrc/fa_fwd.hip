@@ -393,6 +393,7 @@ static hipError_t launch_fwd_ring_t(const AttnArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+
 template <typename T, int DT, int KB>
 static size_t fwd_generic_smem() {
   constexpr int LD = DT + 16 / sizeof(T);

@@ -8,8 +8,8 @@ timeout -k 10 600 python -u -m pytest tests/test_flash_gpu.py tests/test_minitor
 rc=$?
 tail -3 gpurun_out/tests_$TAG.log
 [ $rc -eq 0 ] || exit $rc
-DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,109,110,111 x 8,16,1024,64 9 > gpurun_out/ab_$TAG.txt 2>&1 \
- && DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,109,110,111 causal 8,16,1024,64 9 >> gpurun_out/ab_$TAG.txt 2>&1
+DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,115 x 8,16,1024,64 9 > gpurun_out/ab_$TAG.txt 2>&1 \
+ && DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,115 causal 8,16,1024,64 9 >> gpurun_out/ab_$TAG.txt 2>&1
 rc=$?
 cat gpurun_out/ab_$TAG.txt
 exit $rc
