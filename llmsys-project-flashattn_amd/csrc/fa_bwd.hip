@@ -467,19 +467,23 @@ static hipError_t dispatch_bwd(const AttnArgs& a, bool vec, bool causal, bool pa
                 : launch_bwd_t<T, DT, QB, KB, false, false, false>(a, st);
 }
 
-hipError_t launch_bwd_ring(const AttnArgs& a, bool causal, bool pair, hipStream_t st);
+hipError_t launch_bwd_ring(const AttnArgs& a, bool bf16_io, bool causal, bool pair, hipStream_t st);
 
 // pair: 0 never, 1 always (causal), 2 when the paired grid keeps >= 2 workgroups per CU.
-// ring: fp32 with one d-chunk of 16-B rows runs the register-row kernels of fa_bwd_ring.hip.
+// ring: one d-chunk of 16-B rows (fp32 d <= 64, bf16 d < 64) runs the register-row kernels of
+// fa_bwd_ring.hip.
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st, int pair, bool ring) {
   const bool pr = pair == 1 || (pair == 2 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
-  if (ring && !bf16_io && vec && a.d <= 64) {
+  if (ring && vec && (bf16_io ? a.d < 64 : a.d <= 64)) {
     const int64_t rows = (int64_t)a.B * a.H * a.N;
-    hipLaunchKernelGGL(fa_bwd_prep<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
+    if (bf16_io)
+      hipLaunchKernelGGL(fa_bwd_prep<bf16>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL(fa_bwd_prep<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_bwd_ring(a, causal, pr, st);
+    return launch_bwd_ring(a, bf16_io, causal, pr, st);
   }
   if (bf16_io) {
     if (a.d <= 64) return dispatch_bwd<bf16, 64, 2, 2>(a, vec, causal, pr, st);

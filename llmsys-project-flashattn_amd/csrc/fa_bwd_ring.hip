@@ -1,4 +1,4 @@
-// fp32 backward for one zero-padded d-chunk (d <= 64, 16-B rows): the FA-2 split of
+// fp32 (d <= 64) and bf16 (d < 64) backward for one zero-padded d-chunk of 16-B rows: the FA-2 split of
 // fa_bwd.hip (dK/dV with the key on the lane, dQ with the query on the lane; same math, same
 // masks, same block order and causal pairing) with the workgroup's own rows in registers.
 //
@@ -18,18 +18,19 @@ namespace mt {
 
 namespace {
 
-// the KS k-step fragments of row r (zero past d, which is a multiple of 4 here)
-template <int KS>
-__device__ __forceinline__ void row_frags(f32x8 (&f)[KS], const float* row, int d, int hf) {
+// the KS k-step fragments of row r (zero past d, which is a multiple of 16 B here)
+template <typename T, int KS>
+__device__ __forceinline__ void row_frags(Frag<T> (&f)[KS], const T* row, int d, int hf) {
+  constexpr int EPC = 16 / sizeof(T);
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    uint4 ch[2];
+    uint4 ch[8 / EPC];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = 16 * ks + 8 * hf + 4 * j;
+    for (int j = 0; j < 8 / EPC; ++j) {
+      const int col = 16 * ks + 8 * hf + j * EPC;
       ch[j] = col < d ? *(const uint4*)(row + col) : make_uint4(0, 0, 0, 0);
     }
-    f[ks] = __builtin_bit_cast(f32x8, ch);
+    f[ks] = __builtin_bit_cast(Frag<T>, ch);
   }
 }
 
@@ -37,13 +38,14 @@ __device__ __forceinline__ void row_frags(f32x8 (&f)[KS], const float* row, int 
 
 // dK, dV: grid (nkb or ceil(nkb / 2) when PAIR, B*H); 4 waves x 32 keys; Q/dO tiles of 32
 // queries (with their lse2 / delta) streamed through the ring.
-template <int DT, bool CAUSAL, bool PAIR>
+template <typename T, int DT, bool CAUSAL, bool PAIR>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
   // DT = 64, or 32 for d <= 32; rows padded by 16 B; NCK 16-B chunks per thread per 32-row tile
-  constexpr int kLD = DT + 4, kCPR = DT / 4, NCK = 32 * kCPR / 256, KS = DT / 16, NDB = DT / 32;
+  constexpr int EPC = 16 / sizeof(T), kLD = DT + EPC, kCPR = DT / EPC;
+  constexpr int NCK = (32 * kCPR + 255) / 256, KS = DT / 16, NDB = DT / 32;
   constexpr int BKV = 128, BQ = 32;
-  constexpr int SLOT = 2 * BQ * kLD + 2 * BQ;  // Q, dO, lse2, delta (floats)
-  extern __shared__ __attribute__((aligned(16))) float ring[];
+  constexpr int SLOT = 2 * BQ * kLD * (int)sizeof(T) + 2 * BQ * 4;  // Q, dO, lse2, delta (bytes)
+  extern __shared__ __attribute__((aligned(16))) char ring[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
@@ -51,10 +53,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
   xcd_order(ublk, bh);
   const int b = bh / p.H, hh = bh % p.H;
   const int nkb = (N + BKV - 1) / BKV;
-  const float* Qg = (const float*)p.q + b * p.sq[0] + hh * p.sq[1];
-  const float* Kg = (const float*)p.k + b * p.sk[0] + hh * p.sk[1];
-  const float* Vg = (const float*)p.v + b * p.sv[0] + hh * p.sv[1];
-  const float* dOg = (const float*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const T* dOg = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
   const float* lse2 = p.lse2 + (int64_t)bh * N;
   const float* delta = p.delta + (int64_t)bh * N;
   const float c2 = p.scale_log2;
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
     const int k0 = kblk * BKV;
     const int my_k = k0 + wave * 32 + c32;
     const int wave_kmin = k0 + wave * 32;
-    f32x8 bk[KS], bv[KS];
+    Frag<T> bk[KS], bv[KS];
     {
       const int kr = min(my_k, N - 1);
       row_frags(bk, Kg + (int64_t)kr * p.sk[2], d, hf);
@@ -86,9 +88,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
     auto pre_load = [&](int qt) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < NCK; ++i) {
-        const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * 4, gr = qt + r;
+        const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * EPC, gr = qt + r;
         pq[i] = po[i] = make_uint4(0, 0, 0, 0);
-        if (gr < N && cc < d) {
+        if (ch < 32 * kCPR && gr < N && cc < d) {
           pq[i] = *(const uint4*)(Qg + (int64_t)gr * p.sq[2] + cc);
           po[i] = *(const uint4*)(dOg + (int64_t)gr * p.sdo[2] + cc);
         }
@@ -100,17 +102,20 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
       }
     };
     auto pre_store = [&](int s) __attribute__((always_inline)) {
-      float* sQ = ring + s * SLOT;
-      float* sO = sQ + BQ * kLD;
+      T* sQ = (T*)(ring + s * SLOT);
+      T* sO = sQ + BQ * kLD;
 #pragma unroll
       for (int i = 0; i < NCK; ++i) {
-        const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * 4;
-        *(uint4*)(sQ + r * kLD + cc) = pq[i];
-        *(uint4*)(sO + r * kLD + cc) = po[i];
+        const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * EPC;
+        if (ch < 32 * kCPR) {
+          *(uint4*)(sQ + r * kLD + cc) = pq[i];
+          *(uint4*)(sO + r * kLD + cc) = po[i];
+        }
       }
       if (tid < BQ) {
-        sO[BQ * kLD + tid] = pl;
-        sO[BQ * kLD + BQ + tid] = pd;
+        float* sRow = (float*)(sO + BQ * kLD);
+        sRow[tid] = pl;
+        sRow[BQ + tid] = pd;
       }
     };
     if (ntile > 0) {
@@ -122,9 +127,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
 
     for (int t = 0; t < ntile; ++t) {
       const int qt = qstart + t * BQ;
-      const float* sQ = ring + (t & 1) * SLOT;
-      const float* sO = sQ + BQ * kLD;
-      const float* sLse = sO + BQ * kLD;
+      const T* sQ = (const T*)(ring + (t & 1) * SLOT);
+      const T* sO = sQ + BQ * kLD;
+      const float* sLse = (const float*)(sO + BQ * kLD);
       const float* sDel = sLse + BQ;
       if (!(CAUSAL && qt + BQ - 1 < wave_kmin)) {
         // Sᵀ and dPᵀ: the lane's column is key my_k, rows are queries qt + acc_row(r, hf)
@@ -132,8 +137,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int col = ks * 16 + 8 * hf;
-          mma(S, row_frag<float>(sQ + c32 * kLD + col), bk[ks]);
-          mma(dP, row_frag<float>(sO + c32 * kLD + col), bv[ks]);
+          mma(S, row_frag<T>(sQ + c32 * kLD + col), bk[ks]);
+          mma(dP, row_frag<T>(sO + c32 * kLD + col), bv[ks]);
         }
         const bool msk = qt + BQ > N || k0 + BKV > N || (CAUSAL && qt < wave_kmin + 31);
 #pragma unroll
@@ -147,11 +152,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const f32x8 bp = acc_frag<float>(S, s), bs = acc_frag<float>(dP, s);
+          const Frag<T> bp = acc_frag<T>(S, s), bs = acc_frag<T>(dP, s);
 #pragma unroll
           for (int db = 0; db < NDB; ++db) {
-            mma(dV[db], col_frag<float>(sO, kLD, 16 * s + 4 * hf, db * 32, lane), bp);
-            mma(dK[db], col_frag<float>(sQ, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+            mma(dV[db], col_frag<T>(sO, kLD, 16 * s + 4 * hf, db * 32, lane), bp);
+            mma(dK[db], col_frag<T>(sQ, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
           }
         }
       }
@@ -163,8 +168,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
     }
 
     if (my_k < N) {
-      float* dKg = (float*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
-      float* dVg = (float*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
+      T* dKg = (T*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
+      T* dVg = (T*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
       const float sc = p.scale;
 #pragma unroll
       for (int db = 0; db < NDB; ++db)
@@ -184,13 +189,15 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
 
 // dQ: grid (nqb or ceil(nqb / 2) when PAIR, B*H); 4 waves x 32 queries; K/V tiles of 32
 // keys streamed through the ring.
-template <int DT, bool CAUSAL, bool PAIR>
+template <typename T, int DT, bool CAUSAL, bool PAIR>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
   // DT = 64, or 32 for d <= 32; rows padded by 16 B; NCK 16-B chunks per thread per 32-row tile
-  constexpr int kLD = DT + 4, kCPR = DT / 4, NCK = 32 * kCPR / 256, KS = DT / 16, NDB = DT / 32;
+  constexpr int EPC = 16 / sizeof(T), kLD = DT + EPC, kCPR = DT / EPC;
+  constexpr int NCK = (32 * kCPR + 255) / 256, KS = DT / 16, NDB = DT / 32;
   constexpr int BQ = 128, BK = 32;
-  constexpr int SLOT = 2 * BK * kLD;  // K, V (floats)
-  extern __shared__ __attribute__((aligned(16))) float ring[];
+  constexpr int SLOT = 2 * BK * kLD;  // K, V (elements)
+  extern __shared__ __attribute__((aligned(16))) char ring_raw[];
+  T* ring = (T*)ring_raw;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
@@ -198,10 +205,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
   xcd_order(ublk, bh);
   const int b = bh / p.H, hh = bh % p.H;
   const int nqb = (N + BQ - 1) / BQ;
-  const float* Qg = (const float*)p.q + b * p.sq[0] + hh * p.sq[1];
-  const float* Kg = (const float*)p.k + b * p.sk[0] + hh * p.sk[1];
-  const float* Vg = (const float*)p.v + b * p.sv[0] + hh * p.sv[1];
-  const float* dOg = (const float*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const T* dOg = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
   const float c2 = p.scale_log2;
 
 #pragma nounroll
@@ -214,7 +221,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
     const int q0 = qblk * BQ;
     const int my_q = q0 + wave * 32 + c32;
     const int wave_qmax = q0 + wave * 32 + 31;
-    f32x8 bq[KS], bo[KS];
+    Frag<T> bq[KS], bo[KS];
     float lse_q, del_q;
     {
       const int qr = min(my_q, N - 1);
@@ -233,22 +240,24 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
     auto pre_load = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < NCK; ++i) {
-        const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * 4, gr = k0 + r;
+        const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * EPC, gr = k0 + r;
         pk[i] = pv[i] = make_uint4(0, 0, 0, 0);
-        if (gr < N && cc < d) {
+        if (ch < 32 * kCPR && gr < N && cc < d) {
           pk[i] = *(const uint4*)(Kg + (int64_t)gr * p.sk[2] + cc);
           pv[i] = *(const uint4*)(Vg + (int64_t)gr * p.sv[2] + cc);
         }
       }
     };
     auto pre_store = [&](int s) __attribute__((always_inline)) {
-      float* sK = ring + s * SLOT;
-      float* sV = sK + BK * kLD;
+      T* sK = ring + s * SLOT;
+      T* sV = sK + BK * kLD;
 #pragma unroll
       for (int i = 0; i < NCK; ++i) {
-        const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * 4;
-        *(uint4*)(sK + r * kLD + cc) = pk[i];
-        *(uint4*)(sV + r * kLD + cc) = pv[i];
+        const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * EPC;
+        if (ch < 32 * kCPR) {
+          *(uint4*)(sK + r * kLD + cc) = pk[i];
+          *(uint4*)(sV + r * kLD + cc) = pv[i];
+        }
       }
     };
     if (ntile > 0) {
@@ -260,16 +269,16 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
 
     for (int t = 0; t < ntile; ++t) {
       const int k0 = t * BK;
-      const float* sK = ring + (t & 1) * SLOT;
-      const float* sV = sK + BK * kLD;
+      const T* sK = ring + (t & 1) * SLOT;
+      const T* sV = sK + BK * kLD;
       if (!(CAUSAL && k0 > wave_qmax)) {
         // S and dP with the query on the lane: rows are keys k0 + acc_row(r, hf)
         f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int col = ks * 16 + 8 * hf;
-          mma(S, row_frag<float>(sK + c32 * kLD + col), bq[ks]);
-          mma(dP, row_frag<float>(sV + c32 * kLD + col), bo[ks]);
+          mma(S, row_frag<T>(sK + c32 * kLD + col), bq[ks]);
+          mma(dP, row_frag<T>(sV + c32 * kLD + col), bo[ks]);
         }
         const bool msk = k0 + BK > N || (CAUSAL && k0 + BK - 1 > q0 + wave * 32);
 #pragma unroll
@@ -281,10 +290,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const f32x8 bs = acc_frag<float>(dP, s);
+          const Frag<T> bs = acc_frag<T>(dP, s);
 #pragma unroll
           for (int db = 0; db < NDB; ++db)
-            mma(dQ[db], col_frag<float>(sK, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+            mma(dQ[db], col_frag<T>(sK, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
         }
       }
       if (t + 1 < ntile) {
@@ -295,7 +304,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
     }
 
     if (my_q < N) {
-      float* dQg = (float*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)my_q * p.sdq[2];
+      T* dQg = (T*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)my_q * p.sdq[2];
       const float sc = p.scale;
 #pragma unroll
       for (int db = 0; db < NDB; ++db)
@@ -310,14 +319,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
   }
 }
 
-template <int DT, bool CAUSAL, bool PAIR>
+template <typename T, int DT, bool CAUSAL, bool PAIR>
 static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
-  constexpr int kLD = DT + 4;
+  constexpr int kLD = DT + 16 / (int)sizeof(T);
   const unsigned bhn = (unsigned)(a.B * a.H);
   {
     const int nkb = (a.N + 127) / 128;
-    const size_t smem = sizeof(float) * (size_t)(2 * (2 * 32 * kLD + 2 * 32));
-    auto kfn = fa_bwd_dkv_ring<DT, CAUSAL, PAIR>;
+    const size_t smem = 2 * (2 * 32 * kLD * sizeof(T) + 2 * 32 * sizeof(float));
+    auto kfn = fa_bwd_dkv_ring<T, DT, CAUSAL, PAIR>;
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)smem);
     if (e != hipSuccess) return e;
@@ -327,8 +336,8 @@ static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
   }
   {
     const int nqb = (a.N + 127) / 128;
-    const size_t smem = sizeof(float) * (size_t)(2 * 2 * 32 * kLD);
-    auto kfn = fa_bwd_dq_ring<DT, CAUSAL, PAIR>;
+    const size_t smem = 2 * 2 * 32 * kLD * sizeof(T);
+    auto kfn = fa_bwd_dq_ring<T, DT, CAUSAL, PAIR>;
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)smem);
     if (e != hipSuccess) return e;
@@ -337,17 +346,22 @@ static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
   }
 }
 
-// fp32, d <= 64, 16-B rows; the caller has run the prep kernel (lse2, delta).
-template <int DT>
+template <typename T, int DT>
 static hipError_t launch_bwd_ring_d(const AttnArgs& a, bool causal, bool pair, hipStream_t st) {
   if (causal)
-    return pair ? launch_bwd_ring_t<DT, true, true>(a, st) : launch_bwd_ring_t<DT, true, false>(a, st);
-  return pair ? launch_bwd_ring_t<DT, false, true>(a, st) : launch_bwd_ring_t<DT, false, false>(a, st);
+    return pair ? launch_bwd_ring_t<T, DT, true, true>(a, st) : launch_bwd_ring_t<T, DT, true, false>(a, st);
+  return pair ? launch_bwd_ring_t<T, DT, false, true>(a, st) : launch_bwd_ring_t<T, DT, false, false>(a, st);
 }
 
-hipError_t launch_bwd_ring(const AttnArgs& a, bool causal, bool pair, hipStream_t st) {
-  // d <= 32 (minitorch's MHA at config 5): 32-column tiles, no zero-padded half
-  return a.d <= 32 ? launch_bwd_ring_d<32>(a, causal, pair, st) : launch_bwd_ring_d<64>(a, causal, pair, st);
+// 16-B rows, d <= 64 (fp32) or d < 64 (bf16, which the d = 64 MFMA backward does not take);
+// the caller has run the prep kernel (lse2, delta). d <= 32: 32-column tiles, no zero-padded
+// half (minitorch's MHA at config 5 has d = 32).
+hipError_t launch_bwd_ring(const AttnArgs& a, bool bf16_io, bool causal, bool pair, hipStream_t st) {
+  if (bf16_io)
+    return a.d <= 32 ? launch_bwd_ring_d<bf16, 32>(a, causal, pair, st)
+                     : launch_bwd_ring_d<bf16, 64>(a, causal, pair, st);
+  return a.d <= 32 ? launch_bwd_ring_d<float, 32>(a, causal, pair, st)
+                   : launch_bwd_ring_d<float, 64>(a, causal, pair, st);
 }
 
 }  // namespace mt
