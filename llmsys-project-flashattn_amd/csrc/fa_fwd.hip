@@ -454,6 +454,11 @@ hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
     return pair ? launch_fwd_ring_t<float, 64, 2, false, true>(a, st)
                 : launch_fwd_ring_t<float, 64, 2, false, false>(a, st);
   }
+  // fp32 64 < d <= 128: 128-column ring with 32-key slots, unpaired (the paired form spills
+  // 36-38 VGPRs at 256)
+  if (ring && vec && !bf16_io && a.d <= 128)
+    return causal ? launch_fwd_ring_t<float, 128, 1, true, false>(a, st)
+                  : launch_fwd_ring_t<float, 128, 1, false, false>(a, st);
   if (bf16_io) {
     if (a.d <= 64) return dispatch_fwd_generic<bf16, 64, 2>(a, vec, causal, st);
     return dispatch_fwd_generic<bf16, 128, 2>(a, vec, causal, st);

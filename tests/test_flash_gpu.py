@@ -526,7 +526,7 @@ def test_fp32_fwd_policies_vs_oracle(torch_dev, policy, causal):
     try:
         _hip.set_policy(policy)
         for (B, H, N, d) in ((1, 2, 1024, 64), (1, 1, 777, 64), (2, 1, 200, 32), (1, 1, 64, 64),
-                             (1, 3, 384, 48)):
+                             (1, 3, 384, 48), (1, 2, 300, 128), (1, 1, 257, 96)):
             q, k, v = (rng.standard_normal((B, H, N, d)).astype(np.float32) for _ in range(3))
             o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.float32) for x in (q, k, v)), causal)
             torch.cuda.synchronize()
