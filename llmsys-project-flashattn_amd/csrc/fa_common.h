@@ -165,6 +165,25 @@ __device__ __forceinline__ void xcd_order(int& blk, int& bh) {
   bh = logical / nx;
 }
 
+// xcd_order for causal grids that cannot pair blocks: when each XCD's chunk holds whole heads,
+// it takes the heaviest block of each of its heads first, then the next heaviest, ... (a
+// longest-first list schedule; "heavy" = the highest block index, as in a causal forward).
+__device__ __forceinline__ void xcd_order_heavy_first(int& blk, int& bh) {
+  const int nx = gridDim.x, nblk = gridDim.x * gridDim.y;
+  const int hw = blockIdx.y * nx + blockIdx.x;
+  const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
+  const int start = xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd;
+  const int len = xcd < rm ? qd + 1 : qd;
+  if (start % nx == 0 && len % nx == 0) {
+    const int nh = len / nx;
+    blk = nx - 1 - slot / nh;
+    bh = start / nx + slot % nh;
+  } else {
+    blk = (start + slot) % nx;
+    bh = (start + slot) / nx;
+  }
+}
+
 // Parameters shared by the forward / backward launches (all strides in elements;
 // the head dimension d is always unit-stride).
 struct AttnArgs {

@@ -217,7 +217,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N, d = p.d;
   int u, bh;
-  xcd_order(u, bh);
+  if (CAUSAL && !PAIR)
+    xcd_order_heavy_first(u, bh);
+  else
+    xcd_order(u, bh);
   const int nqb = (N + BQ - 1) / BQ;
   const int b = bh / p.H, hh = bh % p.H;
   const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
@@ -455,7 +458,7 @@ hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
                 : launch_fwd_ring_t<float, 64, 2, false, false>(a, st);
   }
   // fp32 64 < d <= 128: 128-column ring with 32-key slots, unpaired (the paired form spills
-  // 36-38 VGPRs at 256)
+  // 36-38 VGPRs at 256); causal grids go heaviest block first
   if (ring && vec && !bf16_io && a.d <= 128)
     return causal ? launch_fwd_ring_t<float, 128, 1, true, false>(a, st)
                   : launch_fwd_ring_t<float, 128, 1, false, false>(a, st);

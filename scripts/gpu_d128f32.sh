@@ -7,9 +7,9 @@ timeout -k 10 600 python -u -m pytest tests/test_flash_gpu.py -m gpu -v -x --tim
 rc=$?
 tail -3 gpurun_out/tests_d128f32.log
 [ $rc -eq 0 ] || exit $rc
-DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,109 x 8,16,1024,128 7 > gpurun_out/ab_d128f32.txt 2>&1 \
+DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,110 causal 8,16,1024,64 7 > gpurun_out/ab_d128f32.txt 2>&1 \
  && DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,109 causal 8,16,1024,128 7 >> gpurun_out/ab_d128f32.txt 2>&1 \
- && DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,109 x 4,8,1000,96 7 >> gpurun_out/ab_d128f32.txt 2>&1
+ && DTYPE=fp32 timeout -k 10 200 python scripts/ab_fwd.py 0,109 x 8,16,1024,128 7 >> gpurun_out/ab_d128f32.txt 2>&1
 rc=$?
 cat gpurun_out/ab_d128f32.txt
 exit $rc
