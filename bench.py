@@ -238,8 +238,10 @@ def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2):
     gathered = None
     if world > 1:
         # end to end: the forward plus the RCCL all-gather of the O shards, both inside the
-        # timed region (SURVEY.md §8(e) leg (ii))
-        # concatenated along the leading axis: rank order = global head order
+        # timed region (SURVEY.md §8(e) leg (ii)); serial = one gather after the whole
+        # forward, overlapped = the rank's rows in `chunks` block-cyclic pieces, each piece's
+        # gather issued asynchronously while the next piece computes (minitorch/shard.py
+        # chunk_rows: every gather lands in place in the global head order)
         gathered = torch.empty((world * o.shape[0],) + tuple(o.shape[1:]), dtype=o.dtype,
                                device=o.device)
 
@@ -251,14 +253,53 @@ def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2):
             step_gather()
         clock.sync()
         tg, _, _ = _timed_region(torch, clock, dist, world, step_gather, args.steps)
-        result["end_to_end"] = {
-            "what": "forward + all_gather_into_tensor of every rank's O shard, per step",
+        obytes = o.numel() * o.element_size()
+        serial = {
+            "what": "forward + one all_gather_into_tensor of every rank's O shard, per step",
             "ms_per_step": round(tg * 1e3 / args.steps, 4),
             "tflops": _sig(total_flops / tg / 1e12),
-            "gathered_bytes_per_rank": int(o.numel() * o.element_size() * world),
-            "allgather_gbps_per_rank": round(o.numel() * o.element_size() * (world - 1) * args.steps
+            "gathered_bytes_per_rank": int(obytes * world),
+            "allgather_gbps_per_rank": round(obytes * (world - 1) * args.steps
                                              / max(tg - wall, 1e-9) / 1e9, 2),
         }
+        result["end_to_end"] = serial
+        chunks = args.chunks if args.chunks is not None else (4 if args.config == "c4" else 2)
+        BHg = B * H
+        if chunks > 1 and BHg % (world * chunks) == 0:
+            from minitorch.shard import chunk_rows
+            rc = BHg // (world * chunks)
+            pieces = []
+            for c in range(chunks):
+                lo = chunk_rows(BHg, world, rank, chunks, c)[0]
+                qc, kc, vc = (make_shard(torch, (1, rc, N, d), lo, dtype, s_, device) for s_ in (1, 2, 3))
+                pieces.append((qc, kc, vc, torch.empty_like(qc)))
+            gathered_c = torch.empty_like(gathered)
+
+            def step_overlap():
+                works = []
+                for c, (qc, kc, vc, oc) in enumerate(pieces):
+                    attn_fwd(qc, kc, vc, args.causal, oc)
+                    n = world * rc
+                    works.append(dist.all_gather_into_tensor(
+                        gathered_c.view(BHg, N, d)[c * n:(c + 1) * n], oc.view(rc, N, d),
+                        async_op=True))
+                for w_ in works:
+                    w_.wait()
+
+            for _ in range(2):
+                step_overlap()
+            clock.sync()
+            tc, _, _ = _timed_region(torch, clock, dist, world, step_overlap, args.steps)
+            result["end_to_end"] = {
+                "what": f"forward + all-gather of O, the rank's rows in {chunks} chunks, each "
+                        "chunk's gather overlapping the next chunk's forward, per step",
+                "chunks": chunks,
+                "ms_per_step": round(tc * 1e3 / args.steps, 4),
+                "tflops": _sig(total_flops / tc / 1e12),
+                "gathered_bytes_per_rank": int(obytes * world),
+            }
+            result["end_to_end_serial"] = serial
+            gathered = gathered_c
     return result, (gathered if gathered is not None else o), (q, k, v)
 
 
@@ -464,6 +505,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra (bwd, fp32) legs")
     ap.add_argument("--policy", type=int, default=0, help="kernel policy (0 default)")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="end-to-end leg: chunks of the rank's rows whose all-gather overlaps "
+                         "the next chunk's forward (default 2 for c3, 4 for c4; 1 = serial)")
     ap.add_argument("--shape", type=int, nargs=4, default=None, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 

@@ -29,6 +29,7 @@ hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hip
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st, int pair, bool ring);
+int64_t bwd_fused_slab_bytes(int64_t B, int64_t H, int64_t N);
 #ifdef MT_DIAGNOSTICS
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 #endif
@@ -105,6 +106,7 @@ enum : int {
   // grids that keep two paired workgroups per CU)
   kPolBwdGenNoPair = 112, kPolBwdGenPair = 113,
   kPolBwdF32Lds = 114,  // fp32 backward: fa_bwd.hip's LDS-row kernels instead of the register-row ring
+  kPolBwdFused = 120,   // bf16 d = 64: dQ folded into the dK/dV pass (fa_bwd_fused.hip)
 };
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
@@ -114,7 +116,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused};
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
@@ -405,9 +407,15 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
                    "mt_flash_attn_fwd");
 }
 
+// The fused bf16 d = 64 backward keeps its dQ partial sums (bf16, N/256 per element) in the
+// workspace; their size grows as N^2, so it runs only up to N = 8192 (C3: 1 GiB).
+static bool fused_bwd_applies(int64_t N, int64_t d) { return d == 64 && N <= 8192; }
+static int64_t bwd_rows_bytes(int64_t B, int64_t H, int64_t N) {
+  return (2 * B * H * N * (int64_t)sizeof(float) + 255) / 256 * 256;
+}
+
 int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t d) {
-  (void)d;
-  return 2 * B * H * N * (int64_t)sizeof(float);
+  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(N, d) ? bwd_fused_slab_bytes(B, H, N) : 0);
 }
 
 int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const void* v,
@@ -424,6 +432,7 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
   a.m = (float*)m; a.l = (float*)l;
   a.lse2 = (float*)workspace;
   a.delta = a.lse2 + B * H * N;
+  a.slab = fused_bwd_applies(N, d) ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
   int64_t* dst[8] = {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv};
   for (int i = 0; i < 8; ++i) fill_strides(dst[i], strides ? strides + 3 * i : nullptr, H, N, d);
   a.B = (int)B; a.H = (int)H; a.N = (int)N; a.d = (int)d;
@@ -454,6 +463,7 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
                         : pol == kPolBwdQ128       ? 17
                         : pol == kPolBwdPair       ? 18
                         : pol == kPolBwdPair8      ? 19
+                        : pol == kPolBwdFused && a.slab ? 20
 #ifdef MT_DIAGNOSTICS
                         : (pol >= 87 && pol <= 90)  ? pol - 81  // dK/dV ablations (wrong results)
 #endif

@@ -1054,6 +1054,7 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb
 
 // ---------------------------------------------------------------------------------------
 hipError_t launch_dkv_w64(const AttnArgs& a, int nkb, unsigned nblk, size_t smem, hipStream_t st);
+hipError_t launch_bwd_fused(const AttnArgs& a, bool causal, bf16* slab, hipStream_t st);
 hipError_t launch_dq_pipe(const AttnArgs& a, int nqb, unsigned nblk, hipStream_t st);
 
 template <bool CAUSAL>
@@ -1063,6 +1064,8 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  // 20: dQ folded into the dK/dV pass (fa_bwd_fused.hip: 5 products instead of 7)
+  if (variant == 20) return launch_bwd_fused(a, CAUSAL, (bf16*)a.slab, st);
   // variant -> (dK/dV form, dQ form). dK/dV: 0 32-query steps (128 keys), 1 software-
   // pipelined, 3 / 4 64-query steps (one wave per SIMD / LDS-DMA), 5 the 8-wave LDS-DMA form
   // (256 keys), 11 staggered SIMD partners, 13 one wave per SIMD with 64 keys per wave.

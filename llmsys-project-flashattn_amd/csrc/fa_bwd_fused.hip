@@ -1,0 +1,424 @@
+// FlashAttention backward with dQ folded into the dK/dV pass: bf16 I/O, head dim 64.
+//
+// The split backward (fa_bwd_bf16.hip) runs dK/dV and dQ as two kernels, so the dQ pass
+// recomputes S = Q·Kᵀ and dP = dO·Vᵀ: 7 matrix products where the algorithm needs 5. Here
+// one pass computes all five, as the reference's backward_kernel does
+// (src/flashattention_kernel.cu:115-255; it accumulates dQ in HBM at :228-235):
+//     P = exp2(c2·S'),  dV += Pᵀ·dO,  dS = P ∘ dP',  dK += dSᵀ·Q,  dQ += dS·K
+// (S' and dP' start from the row constants −lse2/c2 and −δ, see fa_bwd_prep_bf16).
+//
+// Workgroup = 8 waves = 256 keys, a wave owns 32 keys (K, V rows as register-resident B
+// operands, the dKᵀ/dVᵀ accumulators), exactly like the split kernel's dK/dV pass. Step t =
+// 64 queries (two 32-query sub-tiles), staged by LDS-DMA one step ahead into a two-slot ring,
+// one barrier per step. dQ needs a sum over the key, which is the lane index of the S/dP
+// accumulators, so dS crosses LDS once:
+//  * every wave writes its bf16 dS (32 keys x 64 queries of the step) into a [key][query]
+//    image (double-buffered by step parity);
+//  * in step t + 1 every wave computes its 16-query x 32-d strip of dQᵀ(step t) = Kᵀ·dSᵀ
+//    over the workgroup's 256 keys (two 16x16x32 MFMA tiles, 8 k-steps of 32 keys: 16
+//    MFMAs, a quarter of the wave's step), interleaved with its dK/dV sub-tiles in the same
+//    basic block, from the dS image and a K image [key][d] written once at the start, both
+//    read with ds_read_b64_tr_b16;
+//  * the strip is a partial sum over this workgroup's keys: it goes to a bf16 slab
+//    [bh][step][key block][wave][lane][8] in the accumulator's own register order (one 16-B
+//    store per lane), and fa_bwd_dq_reduce sums the key blocks in a fixed order
+//    (deterministic, no atomics) and writes dQ.
+// Why slabs and not float atomics: at 256 keys per workgroup dQ is summed over N/256
+// workgroups, 2.1 GB of f32 adds at C3, whose floor at the chip's ≈1.3 TB/s atomic rate
+// (MI355X_MICROARCH.md, Global float atomics) is 1.65 ms, longer than the whole split
+// backward. The bf16 slabs are 1 GiB written during the pass and read once by the reduce
+// (≈0.17 ms at HBM rate); a bf16 partial adds one rounding of 2^-9 of the partial, inside
+// tests/bounds.py's 2^-7 (three roundings: dS, partial, output).
+//
+// LDS images are single copies read both by rows (ds_read_b128: the A operands of S, dP)
+// and by columns (ds_read_b64_tr_b16: dVᵀ, dKᵀ, dQᵀ), with the chunk swizzle
+// c ^ f(r), f(r) = x ^ ((x & 1) << 2), x = (r >> 1) & 7: f takes 8 distinct values on the
+// same-parity rows of every ds_read_b128 lane group (row reads conflict-free), and bit 2 of
+// f flips between rows 4m, 4m+1 and 4m+2, 4m+3 (transposed reads conflict-free); f(r + 8) =
+// f(r) ^ 4, so the transposed read of rows +8 takes its own offset (tlo / thi).
+#include "fa_bwd_bf16.h"
+
+namespace mt {
+
+using namespace bwdbf16;
+
+namespace {
+constexpr int kQT = 32;                             // queries per sub-tile
+constexpr int kStep = 64;                           // queries per barrier step
+constexpr int kKB = 256;                            // keys per workgroup
+constexpr int kImg = kQT * D;                       // elements of one sub-tile image
+constexpr int kSub = 2 * kImg * 2 + 2 * kQT * 4;    // bytes: Q image, dO image, row constants
+constexpr int kRingB = 4 * kSub;                    // 2 slots x 2 sub-tiles
+constexpr int kKImgB = kKB * D * 2;                 // K image [256][64]
+constexpr int kDsB = kKB * kStep * 2;               // dS image [256][64]
+constexpr int kSmemFused = kRingB + kKImgB + 2 * kDsB;
+static_assert(kSmemFused <= 160 * 1024, "LDS budget");
+static_assert(kSub % 16 == 0, "16-B aligned sub-tiles");
+
+__device__ __forceinline__ int swf(int r) {
+  const int x = (r >> 1) & 7;
+  return x ^ ((x & 1) << 2);
+}
+__device__ __forceinline__ int sw(int r, int c) { return r * D + ((c ^ swf(r)) << 3); }
+
+struct FCtx {
+  bf16x8 kf[4], vf[4];   // B operands: K / V rows of this lane's key
+  int roff[4];           // row reads: row c32, chunk 2ks + hf
+  int tlo[2], thi[2];    // transposed reads of column block db: rows 4hf.. / 8 + 4hf..
+};
+
+// Transposed fragment (ds_read_b64_tr_b16 x 2) of rows row0 + {0..15 in the accumulator
+// k order}, row0 a multiple of 16.
+__device__ __forceinline__ bf16x8 trf(const bf16* img, int row0, int lo, int hi) {
+  const bf16* a = img + row0 * D;
+  const s16x4 l = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + lo));
+  const s16x4 h = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + hi));
+  const s16x8 v = {l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ void tr_offsets(int lane, int db, int& lo, int& hi) {
+  const int hf = lane >> 5, i16 = lane & 15, g = (lane >> 4) & 1;
+  const int col = db * 32 + 16 * g + 4 * (i16 & 3), row = 4 * hf + (i16 >> 2);
+  lo = sw(row, col >> 3) + (col & 7);
+  hi = sw(row + 8, col >> 3) + (col & 7);
+}
+
+// One 32-query sub-tile u of the step: S, dP, P, dS, dVᵀ, dKᵀ, and dS into the dS image.
+// Keys past N need no mask here: their K image rows are zero, so their (finite) dS adds
+// nothing to dQ, and their dK/dV rows are not stored. (Non-causal, such a key's clamped score
+// is one the forward's LSE includes, so p <= 1; causal, it lies past every valid query and
+// the diagonal mask zeroes it.)
+template <bool CAUSAL, bool MASK>
+__device__ __forceinline__ void fdkv_tile(const char* sub, const FCtx& c, f32x16 (&dK)[2],
+                                          f32x16 (&dV)[2], float c2, int qt, int N, int my_k,
+                                          int hf, bf16* dsrow, int fk, int u) {
+  const bf16* Qi = (const bf16*)sub;
+  const bf16* Oi = Qi + kImg;
+  const float* nl = (const float*)(Qi + 2 * kImg);
+  const float* nd = nl + kQT;
+  f32x16 S, dP;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 a = *(const float4*)(nl + 8 * g + 4 * hf);
+    const float4 e = *(const float4*)(nd + 8 * g + 4 * hf);
+    S[4 * g] = a.x; S[4 * g + 1] = a.y; S[4 * g + 2] = a.z; S[4 * g + 3] = a.w;
+    dP[4 * g] = e.x; dP[4 * g + 1] = e.y; dP[4 * g + 2] = e.z; dP[4 * g + 3] = e.w;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Qi + c.roff[ks]), c.kf[ks], S, 0, 0, 0);
+    dP = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(Oi + c.roff[ks]), c.vf[ks], dP, 0, 0, 0);
+  }
+  if (MASK) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = qt + acc_row(r, hf);
+      if (q >= N || (CAUSAL && my_k > q)) S[r] = -INFINITY;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float pv = __builtin_amdgcn_exp2f(S[r] * c2);
+    S[r] = pv;
+    dP[r] = pv * dP[r];
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 pf = to_bf16x8(S, s);
+    const bf16x8 sf = to_bf16x8(dP, s);
+    // dS rows of this lane's key: queries 32u + 16s + 4hf + 0..3 and + 8 (chunks 4u + 2s, +1)
+    const uint4 w = __builtin_bit_cast(uint4, sf);
+    *(uint2*)(dsrow + (((4 * u + 2 * s) ^ fk) << 3) + 4 * hf) = make_uint2(w.x, w.y);
+    *(uint2*)(dsrow + (((4 * u + 2 * s + 1) ^ fk) << 3) + 4 * hf) = make_uint2(w.z, w.w);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      dV[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trf(Oi, 16 * s, c.tlo[db], c.thi[db]), pf, dV[db], 0, 0, 0);
+      dK[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trf(Qi, 16 * s, c.tlo[db], c.thi[db]), sf, dK[db], 0, 0, 0);
+    }
+  }
+}
+
+// dQ operands of a 16x16x32 MFMA from a [key][64] image: lane group G = l >> 4 supplies the
+// keys 4G + 0..3 (read 1) and 16 + 4G + 0..3 (read 2) of a 32-key step, the same k order
+// for the Kᵀ (A) and dSᵀ (B) fragments; lane l & 15 = column. Within a 32-lane half the
+// rows of one read are 8 consecutive rows, on which f is a bijection: conflict-free.
+__device__ __forceinline__ int dq_off(int lane, int col0) {
+  const int G = lane >> 4, i16 = lane & 15;
+  const int col = col0 + 4 * (i16 & 3);
+  return sw(4 * G + (i16 >> 2), col >> 3) + (col & 7);
+}
+__device__ __forceinline__ bf16x8 dq_frag(const bf16* p) {
+  const s16x4 l = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+  const s16x4 h = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 16 * D));
+  const s16x8 v = {l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+// k-steps [s0, s1) (32 keys each) of this wave's dQᵀ strip: d 32·d32 + 16t + .., q 16·q16 + ..
+__device__ __forceinline__ void dq_ksteps(const bf16* kimg, const bf16* si, int oa0, int oa1, int ob,
+                                          f32x4 (&acc)[2], int s0, int s1) {
+#pragma unroll
+  for (int s = s0; s < s1; ++s) {
+    const bf16x8 bq = dq_frag(si + 32 * s * kStep + ob);
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dq_frag(kimg + 32 * s * D + oa0), bq, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dq_frag(kimg + 32 * s * D + oa1), bq, acc[1], 0, 0, 0);
+  }
+}
+}  // namespace
+
+// grid: (N / 256 key blocks) x B·H, XCD-aware order (one head's blocks on one XCD); 512
+// threads; kSmemFused bytes of LDS. nsa = ceil(N / 64) query steps of the whole sequence (the
+// slab's step axis).
+// PAIR (causal): a workgroup owns key blocks nkb - 1 - u (light: the fewest query steps) and
+// then u (heavy) of one head, so every workgroup walks about nkb + 1 blocks' worth of steps
+// (the split kernels' pairing, fa_bwd_bf16.hip); the two blocks are two passes of one body.
+template <bool CAUSAL, bool PAIR = false>
+__global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb, int nsa, bf16* slab) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int nslot = PAIR ? (nkb + 1) / 2 : nkb;
+  const int bh = logical / nslot, u_ = logical % nslot;
+  const int b = bh / p.H, hh = bh % p.H;
+#pragma nounroll
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+  const int kb = PAIR ? (pass == 0 ? nkb - 1 - u_ : u_) : u_;
+  if (PAIR && pass == 1) {
+    if (kb == nkb - 1 - u_) break;  // odd nkb: the middle block has no partner
+    __syncthreads();                 // the first block's last LDS reads are done
+  }
+  const int k0 = kb * kKB;
+  const int krow = wave * 32 + c32;  // this lane's key row in the block
+  const int my_k = k0 + krow;
+  bf16* kimg = (bf16*)(smem + kRingB);
+  bf16* dsimg = (bf16*)(smem + kRingB + kKImgB);
+  const int fk = swf(krow);
+  bf16* const dsrow0 = dsimg + krow * kStep;  // step parity 0; parity 1 is + kKB * kStep
+
+  FCtx c;
+  {
+    const bool kval = my_k < N;
+    const int kr = min(my_k, N - 1);
+    const bf16* krp = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1] + (int64_t)kr * p.sk[2];
+    const bf16* vrp = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1] + (int64_t)kr * p.sv[2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      c.kf[ks] = *(const bf16x8*)(krp + 16 * ks + 8 * hf);
+      c.vf[ks] = *(const bf16x8*)(vrp + 16 * ks + 8 * hf);
+      c.roff[ks] = sw(c32, 2 * ks + hf);
+      // the K image for dQ (zero rows past N)
+      *(bf16x8*)(kimg + sw(krow, 2 * ks + hf)) = kval ? c.kf[ks] : bf16x8{};
+    }
+    tr_offsets(lane, 0, c.tlo[0], c.thi[0]);
+    tr_offsets(lane, 1, c.tlo[1], c.thi[1]);
+  }
+  // this wave's dQᵀ strip: queries 16·(wave & 3) .., d 32·(wave >> 2) ..
+  const int q16 = wave & 3, d32 = wave >> 2;
+  const int oa0 = dq_off(lane, 32 * d32), oa1 = dq_off(lane, 32 * d32 + 16), ob = dq_off(lane, 16 * q16);
+  bf16* const slab_w = slab + (((int64_t)bh * nsa * nkb + kb) * 8 + wave) * 512 + lane * 8;
+  const int64_t slab_step = (int64_t)nkb * 8 * 512;
+
+  // LDS-DMA staging: wave w fills rows 8(w & 3) .. + 7 of sub-tile w >> 2's Q and dO images
+  const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* Og = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int sqn = (int)p.sq[2], son = (int)p.sdo[2];
+  const __amdgpu_buffer_rsrc_t rq = head_rsrc(Qg, N, sqn), ro = head_rsrc(Og, N, son);
+  const int wq = wave & 3, wu = wave >> 2;
+  const uint32_t lds0 = lds_base(smem) + __builtin_amdgcn_readfirstlane(wq) * 8 * D * 2 +
+                        __builtin_amdgcn_readfirstlane(wu) * kSub;
+  int gq, go;
+  {
+    const int r = 8 * wq + (lane >> 3), pc = lane & 7;
+    const int cs = pc ^ swf(r);  // the logical chunk that lands in LDS chunk pc
+    gq = (r * sqn + cs * 8) * 2;
+    go = (r * son + cs * 8) * 2;
+  }
+  const float* nlse = p.lse2 + (int64_t)bh * N;
+  const float* ndel = p.delta + (int64_t)bh * N;
+
+  const int qt0 = CAUSAL ? k0 : 0;
+  const int step0 = qt0 / kStep;
+  const int nstep = N > qt0 ? (N - qt0 + kStep - 1) / kStep : 0;
+  float sv = 0.f;
+  auto stage = [&](int t, int slot) __attribute__((always_inline)) {
+    const int qs = qt0 + t * kStep + wu * kQT;
+    const uint32_t img = lds0 + slot * 2 * kSub;
+    dma_rows(img, rq, gq + qs * sqn * 2);
+    dma_rows(img + kImg * 2, ro, go + qs * son * 2);
+    if (tid < 4 * kQT) {
+      const int q = qt0 + t * kStep + (tid >> 6) * kQT + (tid & (kQT - 1));
+      sv = q < N ? ((tid & kQT) == 0 ? nlse[q] : ndel[q]) : 0.f;
+    }
+  };
+  auto publish = [&](int slot) __attribute__((always_inline)) {
+    if (tid < 4 * kQT)
+      ((float*)((bf16*)(smem + (2 * slot + (tid >> 6)) * kSub) + 2 * kImg))[tid & 63] = sv;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto dq_store = [&](const f32x4 (&acc)[2], int tl) __attribute__((always_inline)) {
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[i] = (bf16)acc[0][i]; o[4 + i] = (bf16)acc[1][i]; }
+    *(bf16x8*)(slab_w + (int64_t)(step0 + tl) * slab_step) = o;
+  };
+
+  f32x16 dK[2], dV[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
+  const float c2 = p.scale_log2;
+
+  if (nstep > 0) {
+    stage(0, 0);
+    publish(0);
+  }
+  __syncthreads();
+  // steps: [0, nhead) causal diagonal (masked), [nhead, nfull) mask-free, [nfull, nstep) tail.
+  // Step t > 0 also computes the dQ strip of step t - 1 (its dS image, the other parity):
+  // half its k-steps before each sub-tile. Masked sub-tiles are computed in full, also when
+  // every score of the wave is masked (causal, before the wave's keys; past N): their dS is
+  // then exactly zero, as the dS image needs, and a wave-level skip would be a branch around
+  // the accumulators (copies and spills in the masked steps).
+  const int nhead = CAUSAL ? min(nstep, kKB / kStep) : 0;
+  const int nfull = max(nhead, (N - qt0) / kStep);
+#define FSUB(MASK_, SLOT_, T_, U_)                                                       \
+  {                                                                                      \
+    const int qt_ = qt0 + (T_) * kStep + (U_) * kQT;                                     \
+    bf16* dsr_ = dsrow0 + (SLOT_) * (kKB * kStep);                                       \
+    fdkv_tile<CAUSAL, MASK_>(smem + (2 * (SLOT_) + (U_)) * kSub, c, dK, dV, c2, qt_, N,  \
+                             my_k, hf, dsr_, fk, U_);                                    \
+  }
+#define FSTEP(MASK_, SLOT_, T_, DQ_)                                                     \
+  {                                                                                      \
+    const int t_ = (T_);                                                                 \
+    const bool more_ = t_ + 1 < nstep;                                                   \
+    if (more_) stage(t_ + 1, (SLOT_) ^ 1);                                               \
+    f32x4 qa_[2] = {f32x4{}, f32x4{}};                                                   \
+    const bf16* si_ = dsimg + ((SLOT_) ^ 1) * (kKB * kStep);                             \
+    if (DQ_) dq_ksteps(kimg, si_, oa0, oa1, ob, qa_, 0, 4);                              \
+    FSUB(MASK_, SLOT_, t_, 0)                                                            \
+    if (DQ_) dq_ksteps(kimg, si_, oa0, oa1, ob, qa_, 4, 8);                              \
+    FSUB(MASK_, SLOT_, t_, 1)                                                            \
+    if (DQ_) dq_store(qa_, t_ - 1);                                                      \
+    if (more_) publish((SLOT_) ^ 1);                                                     \
+    __syncthreads();                                                                     \
+  }
+  if (nstep > 0) {
+    if (nhead > 0 || nfull == 0) FSTEP(true, 0, 0, false) else FSTEP(false, 0, 0, false)
+  }
+  int t = 1;
+  for (; t < nhead; ++t) {
+    if (t & 1) FSTEP(true, 1, t, true) else FSTEP(true, 0, t, true)
+  }
+  if ((t & 1) && t < nfull) {
+    FSTEP(false, 1, t, true)
+    ++t;
+  }
+  for (; t + 1 < nfull; t += 2) {
+    FSTEP(false, 0, t, true)
+    FSTEP(false, 1, t + 1, true)
+  }
+  for (; t < nstep; ++t) {
+    if (t < nfull) {
+      if (t & 1) FSTEP(false, 1, t, true) else FSTEP(false, 0, t, true)
+    } else {
+      if (t & 1) FSTEP(true, 1, t, true) else FSTEP(true, 0, t, true)
+    }
+  }
+#undef FSTEP
+#undef FSUB
+  if (nstep > 0) {  // the last step's dQ strip
+    f32x4 qa[2] = {f32x4{}, f32x4{}};
+    dq_ksteps(kimg, dsimg + ((nstep - 1) & 1) * (kKB * kStep), oa0, oa1, ob, qa, 0, 8);
+    dq_store(qa, nstep - 1);
+  }
+
+  if (my_k < N) {
+    bf16* dKg = (bf16*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
+    bf16* dVg = (bf16*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
+    const float sc = p.scale;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = db * 32 + 8 * g + 4 * hf;
+        store4(dKg + col, dK[db][4 * g] * sc, dK[db][4 * g + 1] * sc, dK[db][4 * g + 2] * sc,
+               dK[db][4 * g + 3] * sc, true);
+        store4(dVg + col, dV[db][4 * g], dV[db][4 * g + 1], dV[db][4 * g + 2], dV[db][4 * g + 3], true);
+      }
+  }
+  }  // pass
+}
+
+// dQ = scale · Σ_kb slab[bh][step][kb] in key-block order. One wave per (bh, step, strip w):
+// lane l holds d = 32·(w >> 2) + 4·(l >> 4) + 0..3 (+16 for its second 4) of query
+// 64·step + 16·(w & 3) + (l & 15) (the 16x16 dQᵀ accumulator layout). Causal: key block kb
+// holds partials only for steps >= 4·kb.
+__global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, const bf16* slab, int nkb,
+                                                        int nsa, int causal) {
+  const int lane = threadIdx.x & 63;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit >= (int64_t)p.B * p.H * nsa * 8) return;
+  const int w = (int)(unit & 7);
+  const int64_t bs = unit >> 3;
+  const int s = (int)(bs % nsa);
+  const int bh = (int)(bs / nsa);
+  const int q = s * kStep + 16 * (w & 3) + (lane & 15);
+  const int nk = causal ? min(nkb, s / (kKB / kStep) + 1) : nkb;
+  const bf16* src = slab + (bs * nkb * 8 + w) * 512 + lane * 8;
+  float a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.f;
+  int k = 0;
+  for (; k + 4 <= nk; k += 4) {  // four 16-B loads in flight per lane
+    bf16x8 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load((const bf16x8*)(src + (int64_t)(k + u) * 4096));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] += (float)x[u][i];
+  }
+  for (; k < nk; ++k) {
+    const bf16x8 x = __builtin_nontemporal_load((const bf16x8*)(src + (int64_t)k * 4096));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += (float)x[i];
+  }
+  if (q >= p.N) return;
+  const int b = bh / p.H, hh = bh % p.H;
+  bf16* dst = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)q * p.sdq[2] + 32 * (w >> 2) + 4 * (lane >> 4);
+  const float sc = p.scale;
+  store4(dst, a[0] * sc, a[1] * sc, a[2] * sc, a[3] * sc, true);
+  store4(dst + 16, a[4] * sc, a[5] * sc, a[6] * sc, a[7] * sc, true);
+}
+
+// Slab bytes the fused backward needs beyond the prep workspace.
+int64_t bwd_fused_slab_bytes(int64_t B, int64_t H, int64_t N) {
+  const int64_t nkb = (N + kKB - 1) / kKB, nsa = (N + kStep - 1) / kStep;
+  return B * H * nsa * nkb * 8 * 512 * 2;
+}
+
+// The fused pass and the dQ reduce (after fa_bwd_prep_bf16). slab: bwd_fused_slab_bytes
+// bytes, 16-B aligned.
+hipError_t launch_bwd_fused(const AttnArgs& a, bool causal, bf16* slab, hipStream_t st) {
+  const int nkb = (a.N + kKB - 1) / kKB, nsa = (a.N + kStep - 1) / kStep;
+  // causal: light/heavy pairs while the paired grid still has a workgroup per CU
+  const bool pair = causal && (int64_t)((nkb + 1) / 2) * a.B * a.H >= 256;
+  const int64_t nblk = (int64_t)(pair ? (nkb + 1) / 2 : nkb) * a.B * a.H;
+  const int64_t nunit = (int64_t)a.B * a.H * nsa * 8;
+  if (nblk > 0x7fffffff || (nunit + 3) / 4 > 0x7fffffff) return hipErrorInvalidValue;
+  auto kfn = pair ? fa_bwd_fused_bf16<true, true> : causal ? fa_bwd_fused_bf16<true> : fa_bwd_fused_bf16<false>;
+  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kSmemFused);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(512), kSmemFused, st, a, nkb, nsa, slab);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fa_bwd_dq_reduce, dim3((unsigned)((nunit + 3) / 4)), dim3(256), 0, st, a,
+                     (const bf16*)slab, nkb, nsa, causal ? 1 : 0);
+  return hipGetLastError();
+}
+
+}  // namespace mt

@@ -192,6 +192,7 @@ struct AttnArgs {
   void* dq; void* dk; void* dv;
   float* m; float* l;              // fwd outputs / bwd inputs, [B*H*N]
   float* lse2; float* delta;       // bwd workspace, [B*H*N]
+  void* slab;                      // bwd workspace: dQ partials of the fused bf16 backward
   int64_t sq[3], sk[3], sv[3], so[3], sdo[3], sdq[3], sdk[3], sdv[3];  // (b, h, n)
   int B, H, N, d;
   float scale;       // 1/sqrt(d)

@@ -56,11 +56,21 @@ def _local_or_shard(t, global_ndim: int, world: int, rank: int, rows: int):
                      f"got shape {tuple(t.shape)}")
 
 
-def _world_rank(group, world: Optional[int], rank: Optional[int]) -> Tuple[int, int]:
+def _world_rank(group, world: Optional[int], rank: Optional[int],
+                gather: bool = False) -> Tuple[int, int]:
+    """(world, rank): the process group's, or the explicit pair. An explicit pair with
+    ``gather`` must be this process's own group rank: the all-gather puts this process's
+    rows in its own group slot, so another rank's rows would land in the wrong place."""
     import torch.distributed as dist
     if world is not None or rank is not None:
         if world is None or rank is None:
             raise ValueError("give both world and rank, or neither")
+        if gather and world > 1:
+            if not dist_ready() or world != _group_world(group):
+                raise ValueError("gather=True needs an initialised process group of that world size")
+            if rank != dist.get_rank(group):
+                raise ValueError(f"gather=True with an explicit rank {rank} that is not this "
+                                 f"process's group rank {dist.get_rank(group)}")
         return world, rank
     if dist.is_initialized():
         return dist.get_world_size(group), dist.get_rank(group)
@@ -93,23 +103,68 @@ def _gather(local, world: int, group, bh: int, rank_sizes: Sequence[int]):
     return torch.cat([buf[r * mx: r * mx + n] for r, n in enumerate(rank_sizes)])
 
 
+def chunk_rows(bh: int, world: int, rank: int, chunks: int, c: int) -> Tuple[int, int]:
+    """[lo, hi) of the flattened B*H axis that ``rank`` computes as its chunk ``c`` of the
+    chunked (overlapped) forward: block-cyclic, chunk c of every rank together is the
+    contiguous range [c*W*Rc, (c+1)*W*Rc), Rc = BH / (W*chunks), so each chunk's
+    all-gather lands in place in the global output with no copy."""
+    rc = bh // (world * chunks)
+    lo = (c * world + rank) * rc
+    return lo, lo + rc
+
+
+def _chunked_gather_fwd(q, k, v, causal, group, world, rank, chunks, fn):
+    """The gathered forward with the all-gather of finished chunks overlapping the forward of
+    the next: chunk c's three all-gathers are issued asynchronously right after its forward
+    launches (the RCCL stream waits for exactly that work), then chunk c + 1's forward is
+    launched on the compute stream without waiting; the caller's stream waits for every
+    gather at the end. (gloo: the CPU forward and gloo's background gather overlap the same
+    way.)"""
+    import torch
+    import torch.distributed as dist
+    B, H, N, d = q.shape
+    bh = B * H
+    flat = [shard(t, 1, 0) for t in (q, k, v)]  # [BH, N, d] views (refuses non-viewable)
+    outs, works = None, []
+    for c in range(chunks):
+        lo, hi = chunk_rows(bh, world, rank, chunks, c)
+        res = fn(*(t[lo:hi][None] for t in flat), causal)
+        if outs is None:
+            outs = [torch.empty((bh,) + tuple(r.shape[2:]), dtype=r.dtype, device=r.device) for r in res]
+        n = world * (hi - lo)
+        for r, out in zip(res, outs):
+            works.append(dist.all_gather_into_tensor(out[c * n:(c + 1) * n], r[0].contiguous(),
+                                                     group=group, async_op=True))
+    for w in works:
+        w.wait()
+    return outs[0].view(B, H, N, d), outs[1].view(B, H, N), outs[2].view(B, H, N)
+
+
 def sharded_flash_fwd(q, k, v, causal: bool = False, group=None, gather: bool = True,
                       attn: Optional[Callable] = None, world: Optional[int] = None,
-                      rank: Optional[int] = None):
+                      rank: Optional[int] = None, chunks: int = 1):
     """Forward over this rank's B*H shard of the global [B,H,N,d] Q/K/V.
 
     Returns ``(O, m, l)``: with ``gather`` the full [B,H,N,d] / [B,H,N] results on every
     rank (one all-gather per output), otherwise this rank's shard [rows,N,d] / [rows,N]
     (at world size 1, the full tensors in their global shape).
 
+    ``chunks`` > 1 (with ``gather``): the rank computes its rows in ``chunks`` pieces and
+    all-gathers each piece while the next one computes ("chunk the shard
+    and overlap"); the rows are dealt block-cyclically (``chunk_rows``) so every gather lands
+    in place. Needs B*H divisible by world*chunks, else the forward runs unchunked. The
+    gathered result is bit-identical to the unchunked one.
+
     ``world``/``rank`` default to the process group's; giving them explicitly computes that
-    rank's shard without any collective (``gather=False`` only) — a single process can then
-    produce every rank's rows of a ragged split."""
-    world, rank = _world_rank(group, world, rank)
+    rank's shard without any collective (with ``gather``, ``rank`` must be this process's
+    group rank) — a single process can then produce every rank's rows of a ragged split."""
+    world, rank = _world_rank(group, world, rank, gather)
     if gather and world > 1 and not (dist_ready() and world == _group_world(group)):
         raise ValueError("gather=True needs an initialised process group of that world size")
     B, H, N, d = q.shape
     fn = attn or _hip_fwd
+    if gather and world > 1 and chunks > 1 and (B * H) % (world * chunks) == 0:
+        return _chunked_gather_fwd(q, k, v, causal, group, world, rank, chunks, fn)
     qs, ks, vs = (shard(t, world, rank) for t in (q, k, v))
     o, m, l = fn(qs[None], ks[None], vs[None], causal)
     o, m, l = o[0], m[0], l[0]
@@ -131,7 +186,7 @@ def sharded_flash_bwd(q, k, v, o, do, m, l, causal: bool = False, group=None, ga
     that never gathers O feeds its forward straight into the backward. Returns
     (dQ, dK, dV): gathered [B,H,N,d] with ``gather``, else this rank's [rows,N,d]
     (at world size 1, the global shape). ``world``/``rank``: as in sharded_flash_fwd."""
-    world, rank = _world_rank(group, world, rank)
+    world, rank = _world_rank(group, world, rank, gather)
     if gather and world > 1 and not (dist_ready() and world == _group_world(group)):
         raise ValueError("gather=True needs an initialised process group of that world size")
     B, H, N, d = q.shape

@@ -43,7 +43,11 @@ def test_python_binding_covers_header():
     lib = _hip.lib()  # also applies every argtypes declaration
     assert declared <= set(_hip.exported_symbols()), declared - set(_hip.exported_symbols())
     assert lib.mt_abi_version() >= 1
-    assert lib.mt_flash_attn_bwd_workspace_bytes(2, 3, 5, 7) == 2 * 2 * 3 * 5 * 4
+    # fp32 delta + log2-LSE per row, 256-B aligned; at d = 64 (N <= 8192) also the fused
+    # bf16 backward's dQ partial slab: B*H * ceil(N/64) * ceil(N/256) * 8 KiB
+    assert lib.mt_flash_attn_bwd_workspace_bytes(2, 3, 5, 7) == 256
+    assert lib.mt_flash_attn_bwd_workspace_bytes(8, 16, 4096, 64) == 2 * 128 * 4096 * 4 + 128 * 64 * 16 * 8192
+    assert lib.mt_flash_attn_bwd_workspace_bytes(1, 16, 16384, 64) == 2 * 16 * 16384 * 4
 
 
 def test_errors_are_reported_not_fatal():

@@ -102,6 +102,9 @@ def test_bench_multi_rank_cpu(world, split, causal):
         assert key in res, key
     assert res["n_gpus"] == world and res["scaling"] == split and res["steps"] == 2
     assert res["value"] > 0 and res["end_to_end"]["tflops"] > 0
+    # B*H divides world * 2: the end-to-end leg is the overlapped chunked gather (whose
+    # gathered output is checked below), with the serial gather reported beside it
+    assert res["end_to_end"]["chunks"] == 2 and res["end_to_end_serial"]["tflops"] > 0
     glob = (shape[0] * world,) + shape[1:] if split == "weak" else shape
     assert tuple(res["config"][k] for k in ("B", "H", "N", "d")) == glob
     # the gathered shards are the global attention, in global head order

@@ -129,3 +129,62 @@ def test_sharded_fwd_bwd_gloo_world2(shape, causal):
         errs.append(errq.get())
     assert not errs, errs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _chunk_worker(rank, world, port, shape, causal, chunks, errq):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "llmsys-project-flashattn_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from minitorch.shard import sharded_flash_fwd
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        g = torch.Generator().manual_seed(7)
+        q, k, v = (torch.randn(shape, generator=g) for _ in range(3))
+        one = sharded_flash_fwd(q, k, v, causal, attn=_oracle_fwd)
+        many = sharded_flash_fwd(q, k, v, causal, attn=_oracle_fwd, chunks=chunks)
+        for a, b in zip(one, many):  # the overlapped chunked gather changes nothing
+            assert a.shape == b.shape and torch.equal(a, b), "chunked gather differs"
+        # an explicit rank that is not this process's own, with gather: refused
+        with pytest.raises(ValueError, match="not this process's group rank"):
+            sharded_flash_fwd(q, k, v, causal, attn=_oracle_fwd, world=world, rank=(rank + 1) % world)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surfaced to the parent
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+@pytest.mark.parametrize("world,shape,causal,chunks", [(2, (2, 4, 40, 8), False, 2),
+                                                      (4, (2, 8, 24, 8), True, 2)])
+def test_chunked_overlapped_gather_bit_identical(world, shape, causal, chunks):
+    """The chunked forward (all-gather of finished chunks overlapping the next chunk's
+    forward, block-cyclic rows) returns exactly the unchunked gathered O, m, l."""
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chunk_worker, args=(r, world, port, shape, causal, chunks, errq))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_chunk_rows_cover_every_head_once():
+    from minitorch.shard import chunk_rows
+    for bh, world, chunks in ((128, 8, 2), (1024, 8, 4), (16, 2, 4)):
+        seen = sorted(r for rank in range(world) for c in range(chunks)
+                      for r in range(*chunk_rows(bh, world, rank, chunks, c)))
+        assert seen == list(range(bh))
+        # chunk c of all ranks is one contiguous range, rank order
+        for c in range(chunks):
+            spans = [chunk_rows(bh, world, rank, chunks, c) for rank in range(world)]
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
