@@ -54,7 +54,20 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
                       const int64_t* q_strides, const int64_t* k_strides,
                       const int64_t* v_strides, const int64_t* o_strides, void* stream);
 
-/* Scratch bytes mt_flash_attn_bwd needs (fp32 δ and log2-LSE per row). */
+/* The forward with key padding: kv_len is a device int32 [B] (NULL = none); keys
+ * j >= kv_len[b] (clamped to [0, N]) of batch row b are masked for every head and query, as
+ * the reference's [B, to_len] additive padding mask does in the fused softmax
+ * (src/softmax_kernel.cu:26-33). Queries are not masked (a padded query attends the valid
+ * keys). A row with kv_len = 0 gets O = 0, m = -inf, l = 0. bf16 runs the generic / ring
+ * kernels here (the d = 64 / 128 MFMA schedules have no per-row key bound). */
+int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k, const void* v,
+                             void* o, float* m, float* l, int64_t B, int64_t H, int64_t N,
+                             int64_t d, const int64_t* q_strides, const int64_t* k_strides,
+                             const int64_t* v_strides, const int64_t* o_strides,
+                             const int* kv_len, void* stream);
+
+/* Scratch bytes mt_flash_attn_bwd needs: fp32 δ and log2-LSE per row (256-B aligned) and,
+ * at d = 64 with N <= 8192, the bf16 dQ partial sums of the fused bf16 backward. */
 int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t d);
 
 /* dQ, dK, dV of the forward above, from Q, K, V, O, dO and the forward's (m, l).
@@ -63,6 +76,13 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
                       const void* o, const void* dout, const float* m, const float* l,
                       void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
                       int64_t d, const int64_t* strides, void* workspace, void* stream);
+/* The backward of mt_flash_attn_fwd_varlen (same kv_len): padding keys get dK = dV = 0 and
+ * add nothing to dQ. */
+int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k, const void* v,
+                             const void* o, const void* dout, const float* m, const float* l,
+                             void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
+                             int64_t d, const int64_t* strides, const int* kv_len,
+                             void* workspace, void* stream);
 
 /* ---- FlashAttention, reference-compatible host pointers (fp32) ------------ */
 /* reference src/flashattention_kernel.cu:259 */

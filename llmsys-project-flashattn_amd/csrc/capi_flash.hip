@@ -375,11 +375,21 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
                       void* o, float* m, float* l, int64_t B, int64_t H, int64_t N, int64_t d,
                       const int64_t* q_strides, const int64_t* k_strides,
                       const int64_t* v_strides, const int64_t* o_strides, void* stream) {
+  return mt_flash_attn_fwd_varlen(dtype, causal, q, k, v, o, m, l, B, H, N, d, q_strides,
+                                  k_strides, v_strides, o_strides, nullptr, stream);
+}
+
+int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k, const void* v,
+                             void* o, float* m, float* l, int64_t B, int64_t H, int64_t N,
+                             int64_t d, const int64_t* q_strides, const int64_t* k_strides,
+                             const int64_t* v_strides, const int64_t* o_strides,
+                             const int* kv_len, void* stream) {
   if (check_sizes(dtype, B, H, N, d)) return 1;
   if (!q || !k || !v || !o) return set_error("mt_flash_attn_fwd: null tensor pointer");
   AttnArgs a;
   memset(&a, 0, sizeof(a));
   a.q = q; a.k = k; a.v = v; a.out = o; a.m = m; a.l = l;
+  a.kv_len = kv_len;
   fill_strides(a.sq, q_strides, H, N, d);
   fill_strides(a.sk, k_strides, H, N, d);
   fill_strides(a.sv, v_strides, H, N, d);
@@ -391,7 +401,9 @@ int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const
   const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so}, {q, k, v, o});
   hipStream_t st = (hipStream_t)stream;
   const int pol = g_kernel_policy.load(std::memory_order_relaxed);
-  if (dtype == MT_BF16 && vec && pol != kPolGeneric) {
+  // key padding (kv_len): the generic / ring kernels, which mask keys >= kv_len[b] (the
+  // bf16 d = 64 / 128 MFMA schedules have no per-row key bound)
+  if (dtype == MT_BF16 && vec && pol != kPolGeneric && !kv_len) {
     bool handled = false;
     const hipError_t e = fwd_bf16_dispatch(a, causal != 0, pol, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(bf16)");
@@ -422,6 +434,15 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
                       const void* o, const void* dout, const float* m, const float* l,
                       void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
                       int64_t d, const int64_t* strides, void* workspace, void* stream) {
+  return mt_flash_attn_bwd_varlen(dtype, causal, q, k, v, o, dout, m, l, dq, dk, dv, B, H, N, d,
+                                  strides, nullptr, workspace, stream);
+}
+
+int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k, const void* v,
+                             const void* o, const void* dout, const float* m, const float* l,
+                             void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
+                             int64_t d, const int64_t* strides, const int* kv_len,
+                             void* workspace, void* stream) {
   if (check_sizes(dtype, B, H, N, d)) return 1;
   if (!q || !k || !v || !o || !dout || !m || !l || !dq || !dk || !dv || !workspace)
     return set_error("mt_flash_attn_bwd: null pointer argument");
@@ -430,6 +451,7 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
   a.q = q; a.k = k; a.v = v; a.o = o; a.dout = dout;
   a.dq = dq; a.dk = dk; a.dv = dv;
   a.m = (float*)m; a.l = (float*)l;
+  a.kv_len = kv_len;
   a.lse2 = (float*)workspace;
   a.delta = a.lse2 + B * H * N;
   a.slab = fused_bwd_applies(N, d) ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
@@ -442,7 +464,9 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
   const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv},
                           {q, k, v, o, dout, dq, dk, dv});
   const int pol = g_kernel_policy.load(std::memory_order_relaxed);
-  if (dtype == MT_BF16 && vec && pol != kPolGeneric) {
+  // key padding (kv_len): the fused bf16 d = 64 kernel or the generic / ring kernels, which
+  // mask keys >= kv_len[b]
+  if (dtype == MT_BF16 && vec && pol != kPolGeneric && (!kv_len || a.slab)) {
     bool handled = false;
     // dK/dV forms: 0 32-query steps, 1 software-pipelined, 3 64-query steps at one wave
     // per SIMD, 4 64-query steps with LDS-DMA Q/dO, 5 the same with 8 waves (256 keys per
@@ -450,7 +474,8 @@ int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const
     // 1.937 ms for 4 at C3, profiles/r2_ab_bwd.txt), 0 causal (1.12 vs 1.31 ms: the masked
     // diagonal steps spill in the 64-query form), paired (18) on large causal grids. An in-wave interleaved dQ tile measured
     // 1.7 % slower than the plain tile and was removed (profiles/r1_ab_bwd_dq.txt).
-    const int variant = pol == kPolBwdPipe        ? 1
+    const int variant = kv_len                    ? 20  // the fused kernel masks padding keys
+                        : pol == kPolBwdPipe        ? 1
                         : pol == kPolBwdQ64OneWave ? 3
                         : pol == kPolBwdQ64Dma     ? 4
                         : pol == kPolBwdQ64Dma8    ? 5

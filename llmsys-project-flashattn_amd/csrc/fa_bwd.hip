@@ -87,6 +87,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
   const int nch = (dpad + DT - 1) / DT;
   const int my_k = k0 + wave * 32 + c32;  // this lane's key
   const int wave_kmin = k0 + wave * 32;
+  const int Nk = kv_keys(p, b);  // keys >= Nk are padding: zero gradients
 
   f32x16 dK[DT / 32], dV[DT / 32];
 #pragma unroll
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
       // p = exp2(c2·s − lse2): one fma into one v_exp_f32; masks only on tiles that reach
       // past N or below the wave's keys (causal)
       const float c2 = p.scale_log2;
-      const bool msk = qt + BQ > N || k0 + BKV > N || (CAUSAL && qt < wave_kmin + 31);
+      const bool msk = qt + BQ > N || k0 + BKV > Nk || (CAUSAL && qt < wave_kmin + 31);
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkv(AttnArgs p) {
           const int ql = qb * 32 + acc_row(r, hf);
           const int q = qt + ql;
           float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[qb][r], c2, -sLse[ql]));
-          if (msk && (q >= N || my_k >= N || (CAUSAL && my_k > q))) pv = 0.f;
+          if (msk && (q >= N || my_k >= Nk || (CAUSAL && my_k > q))) pv = 0.f;
           S[qb][r] = pv;
           dP[qb][r] = pv * (dP[qb][r] - sDel[ql]);
         }
@@ -299,7 +300,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
     stage_tile<T, BQ, DT, 256, VEC>(sQ, LD, Qg, p.sq[2], q0, N, 0, d);
     stage_tile<T, BQ, DT, 256, VEC>(sO, LD, dOg, p.sdo[2], q0, N, 0, d);
   }
-  const int kend = CAUSAL ? min(N, q0 + BQ) : N;
+  const int Nk = kv_keys(p, b);  // keys >= Nk are padding
+  const int kend = CAUSAL ? min(Nk, q0 + BQ) : Nk;
   // one d-chunk with 16-B rows: the K / V tile of step k0 + BK is loaded into registers
   // while step k0 computes (fa_fwd.hip, same scheme)
   const bool pref = VEC && nch == 1;
@@ -370,14 +372,14 @@ __global__ __launch_bounds__(256) void fa_bwd_dq(AttnArgs p) {
     }
     if (active) {
       const float c2 = p.scale_log2;
-      const bool msk = k0 + BK > N || (CAUSAL && k0 + BK - 1 > q0 + wave * 32);
+      const bool msk = k0 + BK > Nk || (CAUSAL && k0 + BK - 1 > q0 + wave * 32);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = k0 + kb * 32 + acc_row(r, hf);
           float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[kb][r], c2, -lse_q));
-          if (msk && (key >= N || (CAUSAL && key > my_q))) pv = 0.f;
+          if (msk && (key >= Nk || (CAUSAL && key > my_q))) pv = 0.f;
           dP[kb][r] = pv * (dP[kb][r] - del_q);
         }
     }

@@ -85,14 +85,13 @@ __device__ __forceinline__ void tr_offsets(int lane, int db, int& lo, int& hi) {
 }
 
 // One 32-query sub-tile u of the step: S, dP, P, dS, dVᵀ, dKᵀ, and dS into the dS image.
-// Keys past N need no mask here: their K image rows are zero, so their (finite) dS adds
-// nothing to dQ, and their dK/dV rows are not stored. (Non-causal, such a key's clamped score
-// is one the forward's LSE includes, so p <= 1; causal, it lies past every valid query and
-// the diagonal mask zeroes it.)
+// MASK: queries past N, keys at or past Nk (N, or the batch row's kv_len) and, causal,
+// keys after the query get p = 0; a workgroup whose block holds a key >= Nk runs every step
+// masked.
 template <bool CAUSAL, bool MASK>
 __device__ __forceinline__ void fdkv_tile(const char* sub, const FCtx& c, f32x16 (&dK)[2],
-                                          f32x16 (&dV)[2], float c2, int qt, int N, int my_k,
-                                          int hf, bf16* dsrow, int fk, int u) {
+                                          f32x16 (&dV)[2], float c2, int qt, int N, int Nk,
+                                          int my_k, int hf, bf16* dsrow, int fk, int u) {
   const bf16* Qi = (const bf16*)sub;
   const bf16* Oi = Qi + kImg;
   const float* nl = (const float*)(Qi + 2 * kImg);
@@ -114,7 +113,7 @@ __device__ __forceinline__ void fdkv_tile(const char* sub, const FCtx& c, f32x16
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int q = qt + acc_row(r, hf);
-      if (q >= N || (CAUSAL && my_k > q)) S[r] = -INFINITY;
+      if (q >= N || my_k >= Nk || (CAUSAL && my_k > q)) S[r] = -INFINITY;
     }
   }
 #pragma unroll
@@ -194,6 +193,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   const int k0 = kb * kKB;
   const int krow = wave * 32 + c32;  // this lane's key row in the block
   const int my_k = k0 + krow;
+  const int Nk = kv_keys(p, b);      // keys >= Nk are padding (zero dK, dV; no dQ share)
   bf16* kimg = (bf16*)(smem + kRingB);
   bf16* dsimg = (bf16*)(smem + kRingB + kKImgB);
   const int fk = swf(krow);
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
 
   FCtx c;
   {
-    const bool kval = my_k < N;
+    const bool kval = my_k < Nk;
     const int kr = min(my_k, N - 1);
     const bf16* krp = (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1] + (int64_t)kr * p.sk[2];
     const bf16* vrp = (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1] + (int64_t)kr * p.sv[2];
@@ -242,7 +242,8 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
 
   const int qt0 = CAUSAL ? k0 : 0;
   const int step0 = qt0 / kStep;
-  const int nstep = N > qt0 ? (N - qt0 + kStep - 1) / kStep : 0;
+  // a block of padding keys only (k0 >= Nk) stores zero dK / dV and no dQ partials
+  const int nstep = N > qt0 && k0 < Nk ? (N - qt0 + kStep - 1) / kStep : 0;
   float sv = 0.f;
   auto stage = [&](int t, int slot) __attribute__((always_inline)) {
     const int qs = qt0 + t * kStep + wu * kQT;
@@ -282,14 +283,14 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   // every score of the wave is masked (causal, before the wave's keys; past N): their dS is
   // then exactly zero, as the dS image needs, and a wave-level skip would be a branch around
   // the accumulators (copies and spills in the masked steps).
-  const int nhead = CAUSAL ? min(nstep, kKB / kStep) : 0;
+  const int nhead = k0 + kKB > Nk ? nstep : CAUSAL ? min(nstep, kKB / kStep) : 0;
   const int nfull = max(nhead, (N - qt0) / kStep);
 #define FSUB(MASK_, SLOT_, T_, U_)                                                       \
   {                                                                                      \
     const int qt_ = qt0 + (T_) * kStep + (U_) * kQT;                                     \
     bf16* dsr_ = dsrow0 + (SLOT_) * (kKB * kStep);                                       \
     fdkv_tile<CAUSAL, MASK_>(smem + (2 * (SLOT_) + (U_)) * kSub, c, dK, dV, c2, qt_, N,  \
-                             my_k, hf, dsr_, fk, U_);                                    \
+                             Nk, my_k, hf, dsr_, fk, U_);                                \
   }
 #define FSTEP(MASK_, SLOT_, T_, DQ_)                                                     \
   {                                                                                      \
@@ -356,7 +357,8 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
 // dQ = scale · Σ_kb slab[bh][step][kb] in key-block order. One wave per (bh, step, strip w):
 // lane l holds d = 32·(w >> 2) + 4·(l >> 4) + 0..3 (+16 for its second 4) of query
 // 64·step + 16·(w & 3) + (l & 15) (the 16x16 dQᵀ accumulator layout). Causal: key block kb
-// holds partials only for steps >= 4·kb.
+// holds partials only for steps >= 4·kb; blocks of padding keys only (kb·256 >= kv_len)
+// hold none.
 __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, const bf16* slab, int nkb,
                                                         int nsa, int causal) {
   const int lane = threadIdx.x & 63;
@@ -367,7 +369,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, const bf16* 
   const int s = (int)(bs % nsa);
   const int bh = (int)(bs / nsa);
   const int q = s * kStep + 16 * (w & 3) + (lane & 15);
-  const int nk = causal ? min(nkb, s / (kKB / kStep) + 1) : nkb;
+  const int nkv = (kv_keys(p, bh / p.H) + kKB - 1) / kKB;
+  const int nk = min(nkv, causal ? min(nkb, s / (kKB / kStep) + 1) : nkb);
   const bf16* src = slab + (bs * nkb * 8 + w) * 512 + lane * 8;
   float a[8];
 #pragma unroll

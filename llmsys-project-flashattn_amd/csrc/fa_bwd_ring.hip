@@ -71,6 +71,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
     const int k0 = kblk * BKV;
     const int my_k = k0 + wave * 32 + c32;
     const int wave_kmin = k0 + wave * 32;
+    const int Nk = kv_keys(p, b);  // keys >= Nk are padding: zero gradients
     Frag<T> bk[KS], bv[KS];
     {
       const int kr = min(my_k, N - 1);
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
     for (int i = 0; i < NDB; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
 
     const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of BQ
-    const int ntile = N > qstart ? (N - qstart + BQ - 1) / BQ : 0;
+    const int ntile = N > qstart && k0 < Nk ? (N - qstart + BQ - 1) / BQ : 0;
     uint4 pq[NCK], po[NCK];
     float pl = 0.f, pd = 0.f;
     auto pre_load = [&](int qt) __attribute__((always_inline)) {
@@ -140,13 +141,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
           mma(S, row_frag<T>(sQ + c32 * kLD + col), bk[ks]);
           mma(dP, row_frag<T>(sO + c32 * kLD + col), bv[ks]);
         }
-        const bool msk = qt + BQ > N || k0 + BKV > N || (CAUSAL && qt < wave_kmin + 31);
+        const bool msk = qt + BQ > N || k0 + BKV > Nk || (CAUSAL && qt < wave_kmin + 31);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ql = acc_row(r, hf);
           const int q = qt + ql;
           float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[r], c2, -sLse[ql]));
-          if (msk && (q >= N || my_k >= N || (CAUSAL && my_k > q))) pv = 0.f;
+          if (msk && (q >= N || my_k >= Nk || (CAUSAL && my_k > q))) pv = 0.f;
           S[r] = pv;
           dP[r] = pv * (dP[r] - sDel[ql]);
         }
@@ -234,7 +235,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
 #pragma unroll
     for (int i = 0; i < NDB; ++i) dQ[i] = f32x16{};
 
-    const int kend = CAUSAL ? min(N, q0 + BQ) : N;
+    const int Nk = kv_keys(p, b);  // keys >= Nk are padding
+    const int kend = CAUSAL ? min(Nk, q0 + BQ) : Nk;
     const int ntile = (kend + BK - 1) / BK;
     uint4 pk[NCK], pv[NCK];
     auto pre_load = [&](int k0) __attribute__((always_inline)) {
@@ -280,12 +282,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
           mma(S, row_frag<T>(sK + c32 * kLD + col), bq[ks]);
           mma(dP, row_frag<T>(sV + c32 * kLD + col), bo[ks]);
         }
-        const bool msk = k0 + BK > N || (CAUSAL && k0 + BK - 1 > q0 + wave * 32);
+        const bool msk = k0 + BK > Nk || (CAUSAL && k0 + BK - 1 > q0 + wave * 32);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = k0 + acc_row(r, hf);
           float pvv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[r], c2, -lse_q));
-          if (msk && (key >= N || (CAUSAL && key > my_q))) pvv = 0.f;
+          if (msk && (key >= Nk || (CAUSAL && key > my_q))) pvv = 0.f;
           dP[r] = pvv * (dP[r] - del_q);
         }
 #pragma unroll

@@ -193,10 +193,17 @@ struct AttnArgs {
   float* m; float* l;              // fwd outputs / bwd inputs, [B*H*N]
   float* lse2; float* delta;       // bwd workspace, [B*H*N]
   void* slab;                      // bwd workspace: dQ partials of the fused bf16 backward
+  const int* kv_len;               // [B] valid keys per batch row (keys >= kv_len masked), or null
   int64_t sq[3], sk[3], sv[3], so[3], sdo[3], sdq[3], sdk[3], sdv[3];  // (b, h, n)
   int B, H, N, d;
   float scale;       // 1/sqrt(d)
   float scale_log2;  // log2(e)/sqrt(d)
 };
+
+// Keys of batch row b that attend: all N, or the first kv_len[b] (clamped to [0, N]) when a
+// key-padding length vector is given (mt_flash_attn_*_varlen).
+__device__ __forceinline__ int kv_keys(const AttnArgs& p, int b) {
+  return p.kv_len ? max(0, min(p.N, p.kv_len[b])) : p.N;
+}
 
 }  // namespace mt

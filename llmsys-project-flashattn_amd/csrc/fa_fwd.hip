@@ -51,13 +51,14 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
   const int nch = (dpad + DT - 1) / DT;
   const int my_q = q0 + wave * 32 + c32;
   const int wave_qmax = q0 + wave * 32 + 31;
+  const int Nk = kv_keys(p, b);  // keys >= Nk are padding
 
   float m_run = -INFINITY, l_run = 0.f;
   f32x16 O[DT / 32];
 #pragma unroll
   for (int i = 0; i < DT / 32; ++i) O[i] = f32x16{};
 
-  const int kend = CAUSAL ? min(N, q0 + BQ) : N;
+  const int kend = CAUSAL ? min(Nk, q0 + BQ) : Nk;
   const int ntiles = (kend + BK - 1) / BK;
 
   // One d-chunk with 16-B rows: the K / V tile t + 1 is loaded into registers while tile t
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
         for (int r = 0; r < 16; ++r) {
           const int key = k0 + kb * 32 + acc_row(r, hf);
           float x = S[kb][r] * p.scale_log2;
-          if (key >= N || (CAUSAL && key > my_q)) x = -INFINITY;
+          if (key >= Nk || (CAUSAL && key > my_q)) x = -INFINITY;
           S[kb][r] = x;
           smax = fmaxf(smax, x);
         }
@@ -164,9 +165,10 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
     }
   }
 
-  // Epilogue: combine the two lane halves' partial row sums, normalise, store.
+  // Epilogue: combine the two lane halves' partial row sums, normalise, store (a row with no
+  // key, kv_len = 0, stores O = 0, m = -inf, l = 0).
   const float l_tot = l_run + __shfl_xor(l_run, 32);
-  const float inv_l = 1.f / l_tot;
+  const float inv_l = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (my_q < N) {
     T* Og = (T*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
 #pragma unroll
@@ -233,6 +235,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
   const int q0 = (pass == 0 ? u : nqb - 1 - u) * BQ;
   const int my_q = q0 + wave * 32 + c32;
   const int wave_qmax = q0 + wave * 32 + 31;
+  const int Nk = kv_keys(p, b);  // keys >= Nk are padding
 
   // Q row my_q (clamped; rows past N are computed but not stored), k-step ks: elements
   // 16 ks + 8 hf .. +7, zero past d (d is a multiple of 16 B here)
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
 #pragma unroll
   for (int i = 0; i < DT / 32; ++i) O[i] = f32x16{};
 
-  const int kend = CAUSAL ? min(N, q0 + BQ) : N;
+  const int kend = CAUSAL ? min(Nk, q0 + BQ) : Nk;
   const int ntiles = (kend + BK - 1) / BK;
 
   uint4 pk[NCK], pv[NCK];
@@ -311,13 +314,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
       // query (causal); the row max is taken on the raw scores (the scale c2 > 0), and
       // exp2(c2·s − m) is one fma into one v_exp_f32
       const float c2 = p.scale_log2;
-      if (k0 + BK > N || (CAUSAL && k0 + BK - 1 > q0 + wave * 32)) {
+      if (k0 + BK > Nk || (CAUSAL && k0 + BK - 1 > q0 + wave * 32)) {
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kb * 32 + acc_row(r, hf);
-            if (key >= N || (CAUSAL && key > my_q)) S[kb][r] = -INFINITY;
+            if (key >= Nk || (CAUSAL && key > my_q)) S[kb][r] = -INFINITY;
           }
       }
       float smax = -INFINITY;
@@ -362,7 +365,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
   }
 
   const float l_tot = l_run + __shfl_xor(l_run, 32);
-  const float inv_l = 1.f / l_tot;
+  const float inv_l = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (my_q < N) {
     T* Og = (T*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
 #pragma unroll
@@ -431,7 +434,7 @@ hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
   // workgroups per CU (0: fa_fwd_generic)
   // bf16 reaches this function only for head dims the MFMA fast paths do not take (d != 64,
   // 128) or strided rows; d < 64 with 16-B rows takes the same ring kernel
-  if (ring && vec && bf16_io && a.d < 64) {
+  if (ring && vec && bf16_io && (a.d < 64 || (a.kv_len && a.d == 64))) {
     const bool pair = ring == 2 || (ring == 3 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
     if (a.d <= 32)
       return causal ? (pair ? launch_fwd_ring_t<bf16, 32, 2, true, true>(a, st)

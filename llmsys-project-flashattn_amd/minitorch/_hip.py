@@ -37,9 +37,13 @@ _PROTOS = {
     "mt_flash_get_kernel_policy": (_int, []),
     "mt_flash_attn_fwd": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,
                                  _i64p, _i64p, _i64p, _i64p, _vp]),
+    "mt_flash_attn_fwd_varlen": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
+                                        _i64, _i64p, _i64p, _i64p, _i64p, _vp, _vp]),
     "mt_flash_attn_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "mt_flash_attn_bwd": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _i64, _i64, _i64, _i64, _i64p, _vp, _vp]),
+    "mt_flash_attn_bwd_varlen": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                        _i64, _i64, _i64, _i64, _i64p, _vp, _vp, _vp]),
     "mt_attn_softmax_fw": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _int, _vp]),
     "mt_attn_softmax_bw": (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_layernorm_fw": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
@@ -175,9 +179,23 @@ def _check_dev(*ts) -> None:
             raise ValueError("HIP flash attention needs device (cuda) tensors")
 
 
-def flash_fwd(q, k, v, causal: bool = False, out=None, m=None, l=None, stream: Optional[int] = None):
+def _kv_arg(kv_len, B, device):
+    """kv_len as the C ABI takes it: a device int32 [B] (None stays None)."""
+    if kv_len is None:
+        return None
+    torch = _torch()
+    kv = torch.as_tensor(kv_len, device=device).to(torch.int32).contiguous()
+    if kv.shape != (B,):
+        raise ValueError(f"kv_len must have shape ({B},), got {tuple(kv.shape)}")
+    return kv
+
+
+def flash_fwd(q, k, v, causal: bool = False, out=None, m=None, l=None, stream: Optional[int] = None,
+              kv_len=None):
     """Device-pointer forward on torch tensors [B,H,N,d] (fp32 or bf16, any strides
-    with unit-stride d). Returns (O, m, l); O has q's dtype, m/l are fp32 [B,H,N]."""
+    with unit-stride d). Returns (O, m, l); O has q's dtype, m/l are fp32 [B,H,N].
+    kv_len: optional [B] valid-key counts (key padding: keys >= kv_len[b] are masked,
+    mt_flash_attn_fwd_varlen)."""
     torch = _torch()
     _check_dev(q, k, v)
     B, H, N, d = q.shape
@@ -192,16 +210,24 @@ def flash_fwd(q, k, v, causal: bool = False, out=None, m=None, l=None, stream: O
     if l is None:
         l = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
     st = stream_ptr(q.device) if stream is None else stream
-    check(lib().mt_flash_attn_fwd(dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(), v.data_ptr(),
-                                  out.data_ptr(), m.data_ptr(), l.data_ptr(), B, H, N, d,
-                                  strides3(q), strides3(k), strides3(v), strides3(out), st),
-          "mt_flash_attn_fwd")
+    kv = _kv_arg(kv_len, B, q.device)
+    if kv is None:
+        check(lib().mt_flash_attn_fwd(dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(),
+                                      v.data_ptr(), out.data_ptr(), m.data_ptr(), l.data_ptr(),
+                                      B, H, N, d, strides3(q), strides3(k), strides3(v),
+                                      strides3(out), st), "mt_flash_attn_fwd")
+    else:
+        check(lib().mt_flash_attn_fwd_varlen(dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(),
+                                             v.data_ptr(), out.data_ptr(), m.data_ptr(), l.data_ptr(),
+                                             B, H, N, d, strides3(q), strides3(k), strides3(v),
+                                             strides3(out), kv.data_ptr(), st),
+              "mt_flash_attn_fwd_varlen")
     return out, m, l
 
 
 def flash_bwd(q, k, v, o, do, m, l, causal: bool = False, dq=None, dk=None, dv=None,
-              workspace=None, stream: Optional[int] = None):
-    """Device-pointer backward. Returns (dQ, dK, dV) in q's dtype."""
+              workspace=None, stream: Optional[int] = None, kv_len=None):
+    """Device-pointer backward. Returns (dQ, dK, dV) in q's dtype. kv_len: as flash_fwd."""
     torch = _torch()
     _check_dev(q, k, v, o, do, m, l)
     B, H, N, d = q.shape
@@ -218,11 +244,15 @@ def flash_bwd(q, k, v, o, do, m, l, causal: bool = False, dq=None, dk=None, dv=N
         s = strides3(t)
         strides[3 * i:3 * i + 3] = list(s)
     st = stream_ptr(q.device) if stream is None else stream
-    check(lib().mt_flash_attn_bwd(dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(), v.data_ptr(),
-                                  o.data_ptr(), do.data_ptr(), m.data_ptr(), l.data_ptr(),
-                                  dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, N, d,
-                                  strides, workspace.data_ptr(), st),
-          "mt_flash_attn_bwd")
+    kv = _kv_arg(kv_len, B, q.device)
+    args = (dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+            do.data_ptr(), m.data_ptr(), l.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+            B, H, N, d, strides)
+    if kv is None:
+        check(lib().mt_flash_attn_bwd(*args, workspace.data_ptr(), st), "mt_flash_attn_bwd")
+    else:
+        check(lib().mt_flash_attn_bwd_varlen(*args, kv.data_ptr(), workspace.data_ptr(), st),
+              "mt_flash_attn_bwd_varlen")
     return dq, dk, dv
 
 

@@ -264,7 +264,16 @@ class HipKernelOps(TensorOps):
         return dx, dgamma, dbeta
 
     @staticmethod
-    def _flash_fw(Q: Tensor, K: Tensor, V: Tensor, causal: bool):
+    def _kv(kv_len):
+        """A [B] key-padding length tensor (minitorch Tensor, device storage) as the int32
+        device vector the C ABI takes, or None."""
+        if kv_len is None:
+            return None
+        import torch
+        return _torch_view(kv_len).reshape(-1).to(torch.int32)
+
+    @staticmethod
+    def _flash_fw(Q: Tensor, K: Tensor, V: Tensor, causal: bool, kv_len=None):
         import torch
         B, H, N, d = Q.shape
         backend = Q.backend
@@ -272,12 +281,13 @@ class HipKernelOps(TensorOps):
         m = torch.empty(B * H * N, dtype=torch.float32, device="cuda")
         l = torch.empty(B * H * N, dtype=torch.float32, device="cuda")
         _hip.flash_fwd(_torch_view(Q), _torch_view(K), _torch_view(V), causal,
-                       out=o.view(B, H, N, d), m=m.view(B, H, N), l=l.view(B, H, N))
+                       out=o.view(B, H, N, d), m=m.view(B, H, N), l=l.view(B, H, N),
+                       kv_len=HipKernelOps._kv(kv_len))
         return (_wrap(o, (B, H, N, d), backend), _wrap(m, (B, H, N), backend),
                 _wrap(l, (B, H, N), backend))
 
     @staticmethod
-    def _flash_bw(Q, K, V, O, dO, m, l, causal: bool):
+    def _flash_bw(Q, K, V, O, dO, m, l, causal: bool, kv_len=None):
         import torch
         B, H, N, d = Q.shape
         backend = Q.backend
@@ -285,21 +295,23 @@ class HipKernelOps(TensorOps):
         _hip.flash_bwd(_torch_view(Q), _torch_view(K), _torch_view(V), _torch_view(O),
                        _torch_view(dO), _torch_view(m), _torch_view(l), causal,
                        dq=bufs[0].view(B, H, N, d), dk=bufs[1].view(B, H, N, d),
-                       dv=bufs[2].view(B, H, N, d))
+                       dv=bufs[2].view(B, H, N, d), kv_len=HipKernelOps._kv(kv_len))
         return tuple(_wrap(b, (B, H, N, d), backend) for b in bufs)
 
+    # reference cuda_kernel_ops.py:605-892; kv_len (optional keyword, [B] valid key counts):
+    # key padding through mt_flash_attn_*_varlen
     @staticmethod
-    def flash_attention_fw(Q: Tensor, K: Tensor, V: Tensor):
-        return HipKernelOps._flash_fw(Q, K, V, False)
+    def flash_attention_fw(Q: Tensor, K: Tensor, V: Tensor, kv_len=None):
+        return HipKernelOps._flash_fw(Q, K, V, False, kv_len)
 
     @staticmethod
-    def flash_attention_bw(Q, K, V, O, dO, m, l):
-        return HipKernelOps._flash_bw(Q, K, V, O, dO, m, l, False)
+    def flash_attention_bw(Q, K, V, O, dO, m, l, kv_len=None):
+        return HipKernelOps._flash_bw(Q, K, V, O, dO, m, l, False, kv_len)
 
     @staticmethod
-    def flash_attention_causal_fw(Q: Tensor, K: Tensor, V: Tensor):
-        return HipKernelOps._flash_fw(Q, K, V, True)
+    def flash_attention_causal_fw(Q: Tensor, K: Tensor, V: Tensor, kv_len=None):
+        return HipKernelOps._flash_fw(Q, K, V, True, kv_len)
 
     @staticmethod
-    def flash_attention_causal_bw(Q, K, V, O, dO, m, l):
-        return HipKernelOps._flash_bw(Q, K, V, O, dO, m, l, True)
+    def flash_attention_causal_bw(Q, K, V, O, dO, m, l, kv_len=None):
+        return HipKernelOps._flash_bw(Q, K, V, O, dO, m, l, True, kv_len)

@@ -57,28 +57,51 @@ class MultiHeadAttention(Module):
         v = self.v_projection(flat).view(*shp).permute(0, 2, 1, 3)
         return q, k, kT, v
 
-    def self_attention(self, q, kT, v):
-        """``kT`` is the [B,H,d,N] transpose, or the [B,H,N,d] keys on the flash path."""
+    def create_padding_mask(self, kv_len, seq_len):
+        """The reference's key-padding contract (src/softmax_kernel.cu:26-33: attn_mask
+        [B, to_len], 0 for tokens, -inf for padding) as an additive [B, 1, 1, T] mask."""
+        kv = np.asarray(kv_len).reshape(-1, 1, 1, 1)
+        mask = np.where(np.arange(seq_len)[None, None, None, :] < kv, 0.0, -np.inf).astype(datatype)
+        return tensor_from_numpy(mask, backend=self.backend)
+
+    def self_attention(self, q, kT, v, kv_len=None):
+        """``kT`` is the [B,H,d,N] transpose, or the [B,H,N,d] keys on the flash path.
+        ``kv_len``: optional per-batch-row count of valid (non-padding) keys: the flash path
+        masks keys >= kv_len[b] in the kernel (mt_flash_attn_*_varlen); the other branches add
+        the equivalent [B, to_len] padding mask."""
         batch_size, num_head, queries_len, q_dim = q.shape
         scale = self.attn_hidden_dim ** 0.5
         if self.use_flash_attention:
-            result = q.flash_attention_causal(kT, v) if self.causal else q.flash_attention(kT, v)
+            kv = None
+            if kv_len is not None:
+                kv = tensor_from_numpy(np.asarray(kv_len, dtype=datatype).reshape(batch_size),
+                                       backend=self.backend)
+            result = (q.flash_attention_causal(kT, v, kv_len=kv) if self.causal
+                      else q.flash_attention(kT, v, kv_len=kv))
         elif self.use_fused_kernel:
             scores = (q @ kT) / scale
-            result = (scores.attn_softmax(None, mask_future=True) if self.causal
-                      else scores.attn_softmax(None)) @ v
+            if kv_len is None:
+                result = (scores.attn_softmax(None, mask_future=True) if self.causal
+                          else scores.attn_softmax(None)) @ v
+            else:
+                mask = self.create_padding_mask(kv_len, queries_len)
+                if self.causal:
+                    mask = mask + self.create_causal_mask(batch_size, num_head, queries_len)
+                result = scores.attn_softmax(mask) @ v
         else:
             scores = (q @ kT) / scale
             if self.causal:
                 scores = scores + self.create_causal_mask(batch_size, num_head, queries_len)
+            if kv_len is not None:
+                scores = scores + self.create_padding_mask(kv_len, queries_len)
             result = softmax(scores, dim=3) @ v
         result = result.permute(0, 2, 1, 3).contiguous()
         return result.view(batch_size, queries_len, self.n_embd)
 
-    def forward(self, x):
+    def forward(self, x, kv_len=None):
         batch_size, seq_len, n_embd = x.shape
         q, k, kT, v = self.project_to_query_key_value(x)
-        attn = self.self_attention(q, k if self.use_flash_attention else kT, v)
+        attn = self.self_attention(q, k if self.use_flash_attention else kT, v, kv_len)
         return self.out_projection(attn.view(batch_size * seq_len, n_embd)).view(batch_size, seq_len, n_embd)
 
 
@@ -116,10 +139,10 @@ class TransformerLayer(Module):
             self.ln_1 = LayerNorm1d(n_embd, ln_eps, backend)
             self.ln_2 = LayerNorm1d(n_embd, ln_eps, backend)
 
-    def forward(self, x):
+    def forward(self, x, kv_len=None):
         batch_size, seq_len, x_dim = x.shape
         a = self.ln_1(x.view(batch_size * seq_len, x_dim)).view(batch_size, seq_len, x_dim)
-        a = self.attention(a) + x
+        a = self.attention(a, kv_len) + x
         h = self.ln_2(a.view(batch_size * seq_len, x_dim)).view(batch_size, seq_len, x_dim)
         return self.ff(h) + a
 
@@ -146,12 +169,15 @@ class DecoderLM(Module):
         self.use_fused_kernel = use_fused_kernel
         self.ln = FusedLayerNorm(n_embd, backend) if use_fused_kernel else LayerNorm1d(n_embd, ln_eps, backend)
 
-    def forward(self, idx):
+    def forward(self, idx, kv_len=None):
+        """kv_len: optional valid-token count per batch row of a right-padded batch (keys past
+        it are masked in every layer's self-attention; with the causal mask and right padding
+        this changes only the outputs at padding positions)."""
         batch_size, seq_len = idx.shape
         pos = tensor([[float(i) for i in range(seq_len)]], backend=self.backend)
         h = self.token_embeddings(idx) + self.position_embeddings(pos).view(1, seq_len, self.n_embd)
         h = self.dropout(h)
         for i in range(self.n_layer):
-            h = getattr(self, f"t_layer_{i + 1}")(h)
+            h = getattr(self, f"t_layer_{i + 1}")(h, kv_len)
         h = self.ln(h.view(batch_size * seq_len, self.n_embd))
         return self.lm_head(h).view(batch_size, seq_len, self.n_vocab)

@@ -290,8 +290,13 @@ class Tensor:
     def layernorm(self, gamma: "Tensor", beta: "Tensor") -> "Tensor":
         return LayerNorm.apply(self, gamma, beta)
 
-    def flash_attention(self, K: "Tensor", V: "Tensor") -> "Tensor":  # noqa: N803
-        return FlashAttention.apply(self, K, V)
+    def flash_attention(self, K: "Tensor", V: "Tensor", kv_len: Optional["Tensor"] = None) -> "Tensor":  # noqa: N803
+        """kv_len: optional constant [B] tensor of valid key counts (key padding)."""
+        if kv_len is None:
+            return FlashAttention.apply(self, K, V)
+        return FlashAttention.apply(self, K, V, kv_len)
 
-    def flash_attention_causal(self, K: "Tensor", V: "Tensor") -> "Tensor":  # noqa: N803
-        return FlashAttentionCausal.apply(self, K, V)
+    def flash_attention_causal(self, K: "Tensor", V: "Tensor", kv_len: Optional["Tensor"] = None) -> "Tensor":  # noqa: N803
+        if kv_len is None:
+            return FlashAttentionCausal.apply(self, K, V)
+        return FlashAttentionCausal.apply(self, K, V, kv_len)

@@ -329,30 +329,42 @@ class LayerNorm(Function):
         return out_grad.f.layernorm_bw(out_grad, inp, gamma, beta, var, means)
 
 
+def _kv_kw(kv):
+    """The optional key-padding lengths (a [B] constant tensor) as the ops' keyword."""
+    return {} if kv is None else {"kv_len": kv}
+
+
 class FlashAttention(Function):
+    """Reference tensor_functions.py:472-497. An optional 4th input is a constant [B]
+    tensor of valid key counts (key padding, mt_flash_attn_*_varlen); it gets no gradient."""
+
     @staticmethod
-    def forward(ctx, Q, K, V):  # noqa: N803 - reference names
-        O, m, l = Q.f.flash_attention_fw(Q, K, V)
-        ctx.save_for_backward(Q, K, V, O, m, l)
+    def forward(ctx, Q, K, V, kv=None):  # noqa: N803 - reference names
+        O, m, l = Q.f.flash_attention_fw(Q, K, V, **_kv_kw(kv))
+        ctx.save_for_backward(Q, K, V, O, m, l, kv)
         return O
 
     @staticmethod
     def backward(ctx, out_grad):
-        Q, K, V, O, m, l = ctx.saved_values
-        return out_grad.f.flash_attention_bw(Q, K, V, O, out_grad, m, l)
+        Q, K, V, O, m, l, kv = ctx.saved_values
+        g = out_grad.f.flash_attention_bw(Q, K, V, O, out_grad, m, l, **_kv_kw(kv))
+        return g if kv is None else tuple(g) + (0.0,)
 
 
 class FlashAttentionCausal(Function):
+    """Reference tensor_functions.py:501-516; kv as in FlashAttention."""
+
     @staticmethod
-    def forward(ctx, Q, K, V):  # noqa: N803
-        O, m, l = Q.f.flash_attention_causal_fw(Q, K, V)
-        ctx.save_for_backward(Q, K, V, O, m, l)
+    def forward(ctx, Q, K, V, kv=None):  # noqa: N803
+        O, m, l = Q.f.flash_attention_causal_fw(Q, K, V, **_kv_kw(kv))
+        ctx.save_for_backward(Q, K, V, O, m, l, kv)
         return O
 
     @staticmethod
     def backward(ctx, out_grad):
-        Q, K, V, O, m, l = ctx.saved_values
-        return out_grad.f.flash_attention_causal_bw(Q, K, V, O, out_grad, m, l)
+        Q, K, V, O, m, l, kv = ctx.saved_values
+        g = out_grad.f.flash_attention_causal_bw(Q, K, V, O, out_grad, m, l, **_kv_kw(kv))
+        return g if kv is None else tuple(g) + (0.0,)
 
 
 # ---- constructors --------------------------------------------------------------------

@@ -59,8 +59,17 @@ def bf16_from_bits(b: np.ndarray) -> np.ndarray:
     return (b.astype(np.uint32) << 16).view(np.float32)
 
 
-def _scores(q: np.ndarray, k: np.ndarray, causal: bool) -> np.ndarray:
-    """Scaled (and masked) fp32 logits of one (..., N, d) batch, reference op order."""
+def pad_mask(kv_len, B: int, n_k: int) -> np.ndarray:
+    """The key-padding mask of a [B] valid-key-count vector as the reference's fused softmax
+    takes it (``src/softmax_kernel.cu:26-33``: ``attn_mask[B, to_len]``, 0 for tokens,
+    -inf for padding), shaped (B, 1, 1, n_k) to add to (B, H, N, n_k) logits."""
+    kv = np.asarray(kv_len).reshape(B, 1, 1, 1)
+    return np.where(np.arange(n_k)[None, None, None, :] < kv, np.float32(0), -np.inf).astype(np.float32)
+
+
+def _scores(q: np.ndarray, k: np.ndarray, causal: bool, kv_len=None) -> np.ndarray:
+    """Scaled (and masked) fp32 logits of one (..., N, d) batch, reference op order.
+    kv_len: optional [B] valid keys per batch row of a (B, H, N, d) batch (padding mask)."""
     d = q.shape[-1]
     n_q, n_k = q.shape[-2], k.shape[-2]
     s = (q.astype(np.float64) @ np.swapaxes(k, -1, -2).astype(np.float64)).astype(np.float32)
@@ -69,29 +78,38 @@ def _scores(q: np.ndarray, k: np.ndarray, causal: bool) -> np.ndarray:
     if causal:
         mask = np.triu(np.ones((n_q, n_k), dtype=np.float32), 1) * -F32_MAX
         s = (s + mask).astype(np.float32)
+    if kv_len is not None:
+        s = (s + pad_mask(kv_len, q.shape[0], n_k)).astype(np.float32)
     return s
 
 
-def attention_fwd(q, k, v, causal=False):
-    """(B,H,N,d) fp32 -> (O, m, l), see module docstring."""
+def attention_fwd(q, k, v, causal=False, kv_len=None):
+    """(B,H,N,d) fp32 -> (O, m, l), see module docstring. kv_len: optional [B] key-padding
+    lengths (keys >= kv_len[b] masked with -inf, as the reference's [B, to_len] softmax
+    mask); a row with no valid key returns O = 0, m = -inf, l = 0 (the reference's softmax
+    is NaN there)."""
     q = np.asarray(q, np.float32)
     k = np.asarray(k, np.float32)
     v = np.asarray(v, np.float32)
-    s = _scores(q, k, causal)
+    s = _scores(q, k, causal, kv_len)
     m = s.max(axis=-1, keepdims=True)
-    e = np.exp((s - m).astype(np.float32).astype(np.float64)).astype(np.float32)
-    l = e.sum(axis=-1, keepdims=True, dtype=np.float32)
-    p = (e * np.float32(1.0) / l).astype(np.float32)
+    empty = np.isneginf(m)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        e = np.exp((s - np.where(empty, 0, m)).astype(np.float32).astype(np.float64)).astype(np.float32)
+        l = e.sum(axis=-1, keepdims=True, dtype=np.float32)
+        p = np.where(empty, 0, (e * np.float32(1.0) / l)).astype(np.float32)
     o = (p.astype(np.float64) @ v.astype(np.float64)).astype(np.float32)
     return o, m[..., 0].astype(np.float32), l[..., 0].astype(np.float32)
 
 
-def attention_bwd(q, k, v, o, do, m, l, causal=False):
+def attention_bwd(q, k, v, o, do, m, l, causal=False, kv_len=None):
     """Exact gradients (dQ, dK, dV) of the composition above, fp64 internally."""
     q64, k64, v64, do64 = (np.asarray(a, np.float64) for a in (q, k, v, do))
     d = q.shape[-1]
-    s = _scores(np.asarray(q, np.float32), np.asarray(k, np.float32), causal).astype(np.float64)
-    p = np.exp(s - np.asarray(m, np.float64)[..., None]) / np.asarray(l, np.float64)[..., None]
+    s = _scores(np.asarray(q, np.float32), np.asarray(k, np.float32), causal, kv_len).astype(np.float64)
+    m64, l64 = np.asarray(m, np.float64)[..., None], np.asarray(l, np.float64)[..., None]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        p = np.where(l64 > 0, np.exp(s - m64) / l64, 0.0)
     dv = np.swapaxes(p, -1, -2) @ do64
     dp = do64 @ np.swapaxes(v64, -1, -2)
     delta = (dp * p).sum(axis=-1, keepdims=True)

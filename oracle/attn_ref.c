@@ -15,6 +15,10 @@
  * m = mx and l = sum are returned with the reference flash contract's meaning
  * (P = exp(S - m) / l, src/flashattention_kernel.cu:194).
  *
+ * Key padding (the *_kv entry points): keys j >= kv[bh] get the reference's additive -inf
+ * padding mask (src/softmax_kernel.cu:26-33, attn_mask[B, to_len]); a row with no valid key
+ * returns O = 0, m = -inf, l = 0 (the reference's softmax is NaN there).
+ *
  * One N-float score row per (bh, i), OpenMP over (bh, i) like numba's prange.
  * The backward is the exact gradient, fp64 accumulation, one N x N fp32 P slice
  * per (bh) and thread; OpenMP over bh.
@@ -29,7 +33,7 @@
 #endif
 
 static void score_row(const float* q, const float* k, int64_t N, int64_t d, int64_t i,
-                      int causal, float inv_sqrt_d, float* s) {
+                      int causal, float inv_sqrt_d, int64_t nk, float* s) {
   for (int64_t j = 0; j < N; ++j) {
     double acc = 0.0;
     const float* kj = k + j * d;
@@ -37,8 +41,15 @@ static void score_row(const float* q, const float* k, int64_t N, int64_t d, int6
     float v = (float)acc;
     v = v * inv_sqrt_d;
     if (causal && j > i) v = v + (-FLT_MAX);
+    if (j >= nk) v = v + (-INFINITY);
     s[j] = v;
   }
+}
+
+static int64_t keys_of(const int* kv, int64_t bh, int64_t N) {
+  if (!kv) return N;
+  const int64_t n = kv[bh];
+  return n < 0 ? 0 : n > N ? N : n;
 }
 
 int oracle_num_threads(void) {
@@ -49,9 +60,10 @@ int oracle_num_threads(void) {
 #endif
 }
 
-/* q,k,v,o: [BH, N, d] contiguous fp32; m,l: [BH, N] (may be NULL). */
-void oracle_attn_fwd(const float* q, const float* k, const float* v, float* o, float* m,
-                     float* l, int64_t BH, int64_t N, int64_t d, int causal, int nthreads) {
+/* q,k,v,o: [BH, N, d] contiguous fp32; m,l: [BH, N] (may be NULL); kv: [BH] valid keys or NULL. */
+void oracle_attn_fwd_kv(const float* q, const float* k, const float* v, float* o, float* m,
+                        float* l, int64_t BH, int64_t N, int64_t d, int causal, const int* kv,
+                        int nthreads) {
   const float inv_sqrt_d = (float)(1.0 / (double)(float)sqrt((double)d));
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -64,15 +76,15 @@ void oracle_attn_fwd(const float* q, const float* k, const float* v, float* o, f
     for (int64_t bh = 0; bh < BH; ++bh) {
       for (int64_t i = 0; i < N; ++i) {
         const int64_t base = bh * N * d;
-        score_row(q + base + i * d, k + base, N, d, i, causal, inv_sqrt_d, s);
+        score_row(q + base + i * d, k + base, N, d, i, causal, inv_sqrt_d, keys_of(kv, bh, N), s);
         float mx = -INFINITY;
         for (int64_t j = 0; j < N; ++j) mx = s[j] > mx ? s[j] : mx;
         float sum = 0.0f;
         for (int64_t j = 0; j < N; ++j) {
-          s[j] = (float)exp((double)(s[j] - mx));
+          s[j] = mx == -INFINITY ? 0.0f : (float)exp((double)(s[j] - mx));
           sum += s[j];
         }
-        const float inv = (float)(1.0 / (double)sum);
+        const float inv = sum > 0.0f ? (float)(1.0 / (double)sum) : 0.0f;
         for (int64_t t = 0; t < d; ++t) acc[t] = 0.0;
         for (int64_t j = 0; j < N; ++j) {
           const float p = s[j] * inv;
@@ -90,10 +102,16 @@ void oracle_attn_fwd(const float* q, const float* k, const float* v, float* o, f
   }
 }
 
+void oracle_attn_fwd(const float* q, const float* k, const float* v, float* o, float* m,
+                     float* l, int64_t BH, int64_t N, int64_t d, int causal, int nthreads) {
+  oracle_attn_fwd_kv(q, k, v, o, m, l, BH, N, d, causal, NULL, nthreads);
+}
+
 /* Exact gradients. dq, dk, dv: [BH, N, d] outputs (overwritten). */
-void oracle_attn_bwd(const float* q, const float* k, const float* v, const float* dout,
-                     const float* m, const float* l, float* dq, float* dk, float* dv,
-                     int64_t BH, int64_t N, int64_t d, int causal, int nthreads) {
+void oracle_attn_bwd_kv(const float* q, const float* k, const float* v, const float* dout,
+                        const float* m, const float* l, float* dq, float* dk, float* dv,
+                        int64_t BH, int64_t N, int64_t d, int causal, const int* kv,
+                        int nthreads) {
   const float inv_sqrt_d = (float)(1.0 / (double)(float)sqrt((double)d));
   const double scale = 1.0 / sqrt((double)d);
 #ifdef _OPENMP
@@ -109,11 +127,11 @@ void oracle_attn_bwd(const float* q, const float* k, const float* v, const float
       const int64_t base = bh * N * d;
       const float *Q = q + base, *K = k + base, *V = v + base, *dO = dout + base;
       for (int64_t i = 0; i < N; ++i) {
-        score_row(Q + i * d, K, N, d, i, causal, inv_sqrt_d, s);
+        score_row(Q + i * d, K, N, d, i, causal, inv_sqrt_d, keys_of(kv, bh, N), s);
         const double mi = m[bh * N + i], li = l[bh * N + i];
         double delta = 0.0;
         for (int64_t j = 0; j < N; ++j) {
-          const double pij = exp((double)s[j] - mi) / li;
+          const double pij = li > 0.0 ? exp((double)s[j] - mi) / li : 0.0;
           double dp = 0.0;
           for (int64_t t = 0; t < d; ++t) dp += (double)dO[i * d + t] * (double)V[j * d + t];
           p[i * N + j] = pij;
@@ -143,4 +161,10 @@ void oracle_attn_bwd(const float* q, const float* k, const float* v, const float
     free(ds);
     free(s);
   }
+}
+
+void oracle_attn_bwd(const float* q, const float* k, const float* v, const float* dout,
+                     const float* m, const float* l, float* dq, float* dk, float* dv,
+                     int64_t BH, int64_t N, int64_t d, int causal, int nthreads) {
+  oracle_attn_bwd_kv(q, k, v, dout, m, l, dq, dk, dv, BH, N, d, causal, NULL, nthreads);
 }

@@ -34,6 +34,12 @@ def lib():
         _lib.oracle_attn_bwd.argtypes = [f, f, f, f, f, f, f, f, f, i64, i64, i64,
                                          ctypes.c_int, ctypes.c_int]
         _lib.oracle_attn_bwd.restype = None
+        ip = ctypes.POINTER(ctypes.c_int)
+        _lib.oracle_attn_fwd_kv.argtypes = [f, f, f, f, f, f, i64, i64, i64, ctypes.c_int, ip, ctypes.c_int]
+        _lib.oracle_attn_fwd_kv.restype = None
+        _lib.oracle_attn_bwd_kv.argtypes = [f, f, f, f, f, f, f, f, f, i64, i64, i64,
+                                            ctypes.c_int, ip, ctypes.c_int]
+        _lib.oracle_attn_bwd_kv.restype = None
         _lib.oracle_num_threads.restype = ctypes.c_int
     return _lib
 
@@ -46,23 +52,40 @@ def num_threads() -> int:
     return lib().oracle_num_threads()
 
 
-def attn_fwd(q, k, v, causal=False, nthreads=0):
-    """q,k,v: (..., N, d) fp32 -> (o, m, l) through the C restatement."""
+def _kv_rows(kv_len, lead):
+    """[B] key-padding lengths of a (B, H, ...) batch -> one int32 per (b, h) row (or None)."""
+    if kv_len is None:
+        return None
+    kv = np.asarray(kv_len, np.int32).reshape(-1)
+    reps = int(np.prod(lead[1:])) if len(lead) > 1 else 1
+    return np.ascontiguousarray(np.repeat(kv, reps), np.int32)
+
+
+def _ip(a):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def attn_fwd(q, k, v, causal=False, nthreads=0, kv_len=None):
+    """q,k,v: (..., N, d) fp32 -> (o, m, l) through the C restatement. kv_len: optional [B]
+    key-padding lengths of a (B, H, N, d) batch."""
     q, k, v = (np.ascontiguousarray(a, dtype=np.float32) for a in (q, k, v))
     *lead, N, d = q.shape
     BH = int(np.prod(lead)) if lead else 1
     o = np.empty_like(q)
     m = np.empty(tuple(lead) + (N,), np.float32)
     l = np.empty_like(m)
-    lib().oracle_attn_fwd(_p(q), _p(k), _p(v), _p(o), _p(m), _p(l), BH, N, d, int(causal), nthreads)
+    kv = _kv_rows(kv_len, lead)
+    lib().oracle_attn_fwd_kv(_p(q), _p(k), _p(v), _p(o), _p(m), _p(l), BH, N, d, int(causal),
+                             _ip(kv), nthreads)
     return o, m, l
 
 
-def attn_bwd(q, k, v, do, m, l, causal=False, nthreads=0):
+def attn_bwd(q, k, v, do, m, l, causal=False, nthreads=0, kv_len=None):
     q, k, v, do, m, l = (np.ascontiguousarray(a, dtype=np.float32) for a in (q, k, v, do, m, l))
     *lead, N, d = q.shape
     BH = int(np.prod(lead)) if lead else 1
     dq, dk, dv = np.empty_like(q), np.empty_like(q), np.empty_like(q)
-    lib().oracle_attn_bwd(_p(q), _p(k), _p(v), _p(do), _p(m), _p(l), _p(dq), _p(dk), _p(dv),
-                          BH, N, d, int(causal), nthreads)
+    kv = _kv_rows(kv_len, lead)
+    lib().oracle_attn_bwd_kv(_p(q), _p(k), _p(v), _p(do), _p(m), _p(l), _p(dq), _p(dk), _p(dv),
+                             BH, N, d, int(causal), _ip(kv), nthreads)
     return dq, dk, dv

@@ -23,7 +23,7 @@ Caveats that shape the recipe (verified in this container):
 
 Usage (from the repo root, in the build container only)::
 
-    python oracle/gen_golden.py          # writes tests/golden/attn_*.npz
+    python oracle/gen_golden.py [case ...]   # writes tests/golden/attn_*.npz
 """
 from __future__ import annotations
 
@@ -76,6 +76,12 @@ CASES = [
     ("ragged_causal", 1, 2, 100, 32, True, 3),
     ("odd_d_causal", 2, 1, 67, 20, True, 4),
 ]
+# key padding: the reference's [B, to_len] additive mask (src/softmax_kernel.cu:26-33: 0 for
+# tokens, -inf for padding) on the same composition; (name, B, H, N, d, causal, seed, kv_len)
+VARLEN_CASES = [
+    ("varlen", 2, 2, 96, 32, False, 5, (60, 96)),
+    ("varlen_causal", 3, 1, 80, 32, True, 6, (33, 80, 1)),
+]
 
 
 def _import_reference():
@@ -98,7 +104,7 @@ def _import_reference():
     return minitorch, minitorch.TensorBackend(CPUOps)
 
 
-def run_case(mt, backend, B, H, N, d, causal, seed):
+def run_case(mt, backend, B, H, N, d, causal, seed, kv_len=None):
     rng = np.random.default_rng(seed)
     q = rng.standard_normal((B, H, N, d)).astype(np.float32)
     k = rng.standard_normal((B, H, N, d)).astype(np.float32)
@@ -113,6 +119,10 @@ def run_case(mt, backend, B, H, N, d, causal, seed):
     if causal:
         mask = -np.finfo(np.float32).max * np.triu(np.ones((BH, N, N), dtype=np.float32), 1)
         scores = scores + mt.tensor_from_numpy(mask, backend, True)
+    if kv_len is not None:  # [B, to_len] padding mask broadcast over heads and queries
+        pad = np.where(np.arange(N)[None, :] < np.asarray(kv_len)[:, None], 0.0, -np.inf)
+        pad = np.broadcast_to(pad[:, None, None, :], (B, H, N, N)).reshape(BH, N, N)
+        scores = scores + mt.tensor_from_numpy(np.ascontiguousarray(pad, dtype=np.float32), backend, False)
     O = mt.softmax(scores, dim=2) @ V
     O.backward(mt.tensor_from_numpy(do.reshape(BH, N, d), backend, False))
     shp = (B, H, N, d)
@@ -123,6 +133,7 @@ def run_case(mt, backend, B, H, N, d, causal, seed):
         dk=K.grad.to_numpy().reshape(shp).astype(np.float32),
         dv=V.grad.to_numpy().reshape(shp).astype(np.float32),
         causal=np.array(causal), B=np.array(B), H=np.array(H), N=np.array(N), d=np.array(d),
+        **({} if kv_len is None else {"kv_len": np.asarray(kv_len, np.int32)}),
         source=np.array("reference minitorch FastOps+nn.softmax+autodiff (numba stand-in)"),
     )
 
@@ -130,9 +141,13 @@ def run_case(mt, backend, B, H, N, d, causal, seed):
 def main():
     os.makedirs(OUT, exist_ok=True)
     mt, backend = _import_reference()
-    for name, B, H, N, d, causal, seed in CASES:
+    only = set(sys.argv[1:])  # optional case names
+    cases = [c + (None,) for c in CASES] + list(VARLEN_CASES)
+    for name, B, H, N, d, causal, seed, kv_len in cases:
+        if only and name not in only:
+            continue
         t0 = time.time()
-        arrays = run_case(mt, backend, B, H, N, d, causal, seed)
+        arrays = run_case(mt, backend, B, H, N, d, causal, seed, kv_len)
         path = os.path.join(OUT, f"attn_{name}.npz")
         np.savez_compressed(path, **arrays)
         print(f"{name}: (B,H,N,d)=({B},{H},{N},{d}) causal={causal} -> {path} "

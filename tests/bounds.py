@@ -19,17 +19,22 @@ import numpy as np
 R_BF16 = 2.0 ** -7
 
 
-def head_terms(q, k, v, do, causal):
-    """fp64 P, |dS| pieces for one head (N, d)."""
+def head_terms(q, k, v, do, causal, kv=None):
+    """fp64 P, |dS| pieces for one head (N, d); kv: valid keys of the head's batch row
+    (key padding; a row with none gets P = 0)."""
     q, k, v, do = (np.asarray(a, np.float64) for a in (q, k, v, do))
     N, d = q.shape
     sc = 1.0 / np.sqrt(d)
     S = (q @ k.T) * sc
     if causal:
         S[np.triu_indices(N, 1)] = -np.inf
-    S -= S.max(axis=1, keepdims=True)
+    if kv is not None:
+        S[:, int(kv):] = -np.inf
+    mx = S.max(axis=1, keepdims=True)
+    S -= np.where(np.isneginf(mx), 0.0, mx)
     P = np.exp(S)
-    P /= P.sum(axis=1, keepdims=True)
+    tot = P.sum(axis=1, keepdims=True)
+    P = np.where(tot > 0, P / np.where(tot > 0, tot, 1.0), 0.0)
     O = P @ v
     dP = do @ v.T
     delta = (do * O).sum(axis=1, keepdims=True)
@@ -38,8 +43,8 @@ def head_terms(q, k, v, do, causal):
     return P, absdS, sc
 
 
-def grad_bounds(q, k, v, do, causal, atol=1e-3, r=R_BF16):
-    P, absdS, sc = head_terms(q, k, v, do, causal)
+def grad_bounds(q, k, v, do, causal, atol=1e-3, r=R_BF16, kv=None):
+    P, absdS, sc = head_terms(q, k, v, do, causal, kv)
     q, k, do = (np.abs(np.asarray(a, np.float64)) for a in (q, k, do))
     return (atol + r * sc * (absdS @ k),      # dQ
             atol + r * sc * (absdS.T @ q),    # dK

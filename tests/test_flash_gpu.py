@@ -59,14 +59,15 @@ def test_golden_fp32(torch_dev, path):
     torch = torch_dev
     z = np.load(path)
     causal = bool(z["causal"])
+    kv = z["kv_len"] if "kv_len" in z.files else None  # key-padding fixtures (attn_varlen*)
     q, k, v, do = (_dev(torch, z[n]) for n in ("q", "k", "v", "do"))
-    o, m, l = _hip.flash_fwd(q, k, v, causal)
+    o, m, l = _hip.flash_fwd(q, k, v, causal, kv_len=kv)
     torch.cuda.synchronize()
     np.testing.assert_allclose(_np(o), z["o"], atol=1e-5, rtol=0)
-    _, m_ref, l_ref = A.attention_fwd(z["q"], z["k"], z["v"], causal)
+    _, m_ref, l_ref = A.attention_fwd(z["q"], z["k"], z["v"], causal, kv)
     np.testing.assert_allclose(_np(m), m_ref, atol=1e-5, rtol=1e-5)
     np.testing.assert_allclose(_np(l), l_ref, rtol=1e-5)
-    dq, dk, dv = _hip.flash_bwd(q, k, v, o, do, m, l, causal)
+    dq, dk, dv = _hip.flash_bwd(q, k, v, o, do, m, l, causal, kv_len=kv)
     torch.cuda.synchronize()
     for got, name in ((dq, "dq"), (dk, "dk"), (dv, "dv")):
         np.testing.assert_allclose(_np(got), z[name], atol=1e-5, rtol=0, err_msg=name)
