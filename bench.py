@@ -457,12 +457,31 @@ def extra_legs(torch, _hip, time_fn):
     return extra
 
 
+def synthetic_mt_batch(rng, B, T, V, pad_id=0):
+    """A right-padded token batch shaped like the reference's collate_fn output
+    (reference project/run_machine_translation.py:119-141): each row is source tokens + target tokens
+    + padding, input_ids = tokens[:, :-1], labels = tokens[:, 1:], label_token_weights = the
+    target mask shifted by one; kv_len = the valid input tokens per row."""
+    import numpy as np
+    total = rng.integers(T // 2, T + 2, B)  # row length in tokens of T + 1 columns
+    src = np.maximum(1, total // 2)
+    tok = rng.integers(1, V, (B, T + 1))
+    tgt_mask = np.zeros((B, T + 1), np.float32)
+    for b in range(B):
+        tok[b, total[b]:] = pad_id
+        tgt_mask[b, src[b]:total[b]] = 1.0
+    return {"input_ids": tok[:, :-1].astype(np.float32), "labels": tok[:, 1:].astype(np.float32),
+            "label_token_weights": tgt_mask[:, 1:], "kv_len": np.minimum(total, T).astype(np.int64)}
+
+
 def c5_step_leg(torch, steps: int = 10) -> dict:
     """Config 5: one DecoderLM training step (forward, backward, Adam) of the reference's
     machine-translation setup (project/run_machine_translation.py:397-407: vocab 10000,
     n_embd 256, 8 heads, batch 128, seq 39) on the HIP backend with fused LayerNorm + softmax
-    and flash attention, synthetic tokens, random init (scripts/mt_step_bench.py, same setup).
-    Host-bound in minitorch's Python autodiff; reported beside the kernels, not the headline."""
+    and flash attention, random init, on a synthetic right-padded batch with the reference's
+    weighted loss (loss_fn, :164-192: softmax_loss · label_token_weights, summed, over the
+    weight sum); the flash path masks the padding keys (kv_len). Host-bound in minitorch's
+    Python autodiff; reported beside the kernels, not the headline."""
     import numpy as np
     import minitorch
     B, T, V, E, H = 128, 39, 10000, 256, 8
@@ -471,12 +490,15 @@ def c5_step_leg(torch, steps: int = 10) -> dict:
     lm = minitorch.DecoderLM(n_vocab=V, n_embd=E, n_head=H, n_positions=40, p_dropout=0.1,
                              backend=backend, use_fused_kernel=True, use_flash_attention=True)
     opt = minitorch.Adam(lm.parameters(), lr=1e-4)
-    x = minitorch.tensor_from_numpy(rng.integers(0, V, (B, T)).astype(np.float32), backend)
-    y = minitorch.tensor_from_numpy(rng.integers(0, V, (B * T,)).astype(np.float32), backend)
+    batch = synthetic_mt_batch(rng, B, T, V)
+    x = minitorch.tensor_from_numpy(batch["input_ids"], backend)
+    y = minitorch.tensor_from_numpy(batch["labels"].reshape(-1), backend)
+    w = minitorch.tensor_from_numpy(batch["label_token_weights"].reshape(-1), backend)
+    kv = batch["kv_len"]
 
     def step():
         opt.zero_grad()
-        loss = minitorch.softmax_loss(lm(x).view(B * T, V), y).sum() / (B * T)
+        loss = (minitorch.softmax_loss(lm(x, kv_len=kv).view(B * T, V), y) * w).sum() / w.sum()
         loss.backward()
         opt.step()
         return loss
@@ -490,7 +512,8 @@ def c5_step_leg(torch, steps: int = 10) -> dict:
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
     return {"c5_step_ms": round(ms, 2), "c5_tokens_per_s": round(B * T / ms * 1e3, 1),
-            "c5_loss": round(float(loss.item()), 4)}
+            "c5_loss": round(float(loss.item()), 4),
+            "c5_batch": "right-padded synthetic tokens, weighted loss, kv_len key padding"}
 
 
 def parse_args(argv=None):

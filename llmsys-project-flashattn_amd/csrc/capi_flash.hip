@@ -20,7 +20,6 @@ hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStrea
                            bool* handled);
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
                          bool* handled, int pair = 0);
-hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hipStream_t st,
                          bool* handled);
 hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled);
@@ -31,18 +30,23 @@ hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
                               hipStream_t st, int pair, bool ring);
 int64_t bwd_fused_slab_bytes(int64_t B, int64_t H, int64_t N);
 #ifdef MT_DIAGNOSTICS
+hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
 #endif
 
 static thread_local char g_err[512] = "";
 
 // ---- kernel policies (A/B selection) ------------------------------------------------
-// Every id below computes the same attention as the default; each has its own parity
-// tests (tests/test_flash_gpu.py FAST_POLICIES / test_bf16_bwd_policies_vs_oracle). The
-// ids are the ones the round-1 A/B records under profiles/ cite. mt_flash_set_kernel_policy
-// rejects anything else with a status. Timing-only ablations that compute WRONG results
-// exist only in a diagnostics build (make DIAG=1 -> libminitorch_hip_diag.so, compiled with
-// -DMT_DIAGNOSTICS), never in the product library.
+// The product library selects: 0 the defaults, 1 the generic tiled kernels, 120 / 121 the
+// fused / split bf16 backward (A/B of the two backward forms). Every other id below is an
+// alternative schedule kept for the A/B records under profiles/ (each computes the same
+// attention and has its own parity tests, tests/test_flash_gpu.py, which skip an id the
+// loaded library rejects); those, and the timing-only ablations that compute WRONG results,
+// exist only in the diagnostics build (make DIAG=1 -> libminitorch_hip_diag.so, compiled with
+// -DMT_DIAGNOSTICS; MT_HIP_LIB selects it for the tests and scripts), so the product library
+// carries only the kernels some default selects. Note: ids 23 / 24 were swapped in round 2
+// (23 now the 8-wave, 24 the 4-wave packed v4); profiles/r1_ab_v4b.txt measured the old
+// meaning.
 enum : int {
   kPolDefault = 0,
   kPolGeneric = 1,  // generic tiled kernels only (fa_fwd.hip / fa_bwd.hip)
@@ -107,7 +111,10 @@ enum : int {
   kPolBwdGenNoPair = 112, kPolBwdGenPair = 113,
   kPolBwdF32Lds = 114,  // fp32 backward: fa_bwd.hip's LDS-row kernels instead of the register-row ring
   kPolBwdFused = 120,   // bf16 d = 64: dQ folded into the dK/dV pass (fa_bwd_fused.hip)
+  kPolBwdSplit = 121,   // bf16 d = 64: the split backward's defaults (dK/dV pass + dQ pass)
 };
+static const int kProductPolicies[] = {kPolDefault, kPolGeneric, kPolBwdFused, kPolBwdSplit};
+#ifdef MT_DIAGNOSTICS
 static const int kValidPolicies[] = {
     kPolDefault, kPolGeneric, kPolFast8, kPolFast4, kPolFastSp8, kPolFastSp4, kPolFastPp,
     kPolV4w4, kPolV4w8, kPolV4Pk8, kPolV4Pk4, kPolV4DeepPk, kPolV4Deep, kPolV4Pair4,
@@ -116,13 +123,16 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit};
+#endif
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
 static bool policy_valid(int p) {
-  for (int v : kValidPolicies)
+  for (int v : kProductPolicies)
     if (v == p) return true;
 #ifdef MT_DIAGNOSTICS
+  for (int v : kValidPolicies)
+    if (v == p) return true;
   // wrong-result ablations (timing only): v5 80-86 / 97 / 98, v4 91-96, fast 10-15, bwd 87-90;
   // 101 v6 with Q pre-scaled (reduced precision)
   if ((p >= 80 && p <= 98) || p == 101 || (p >= 10 && p <= 15)) return true;
@@ -134,7 +144,7 @@ static bool policy_valid(int p) {
 // 8 waves (launcher only), static priority for waves 4-7, single-issue softmax VALU,
 // staggered waves, Vᵀ fragment reuse, exp-to-use distance, DMA from inline asm.
 namespace v5 {
-constexpr int kUnroll = 4, kDma = 1024, kW8 = 2048, kPrio = 4096, kScalar = 8192,
+[[maybe_unused]] constexpr int kUnroll = 4, kDma = 1024, kW8 = 2048, kPrio = 4096, kScalar = 8192,
               kStagger = 16384, kVKeep = 32768, kDefer = 65536, kSplit = 131072, kRowSumMfma = 262144,
               kAsmDma = 524288;
 constexpr int kDefault = kW8 | kDefer | kVKeep | kDma | kUnroll;
@@ -185,11 +195,12 @@ static int check_sizes(int dtype, int64_t B, int64_t H, int64_t N, int64_t d) {
   return 0;
 }
 
-// bf16 forward with 16-B rows: pick the MFMA kernel for policy `pol`. Returns with
-// *handled = false when no bf16 MFMA kernel takes the shape (the caller then runs the
-// generic kernel).
-static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hipStream_t st,
-                                    bool* handled) {
+#ifdef MT_DIAGNOSTICS
+// bf16 forward with 16-B rows under an A/B policy `pol` (diagnostics build): the MFMA kernel
+// that policy names, else the defaults. Returns with *handled = false when no bf16 MFMA kernel
+// takes the shape (the caller then runs the generic kernel).
+static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, hipStream_t st,
+                                       bool* handled) {
   *handled = false;
   hipError_t e = hipSuccess;
   const int N = a.N;
@@ -354,6 +365,57 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
   }
   return e;
 }
+#endif  // MT_DIAGNOSTICS
+
+// bf16 forward with 16-B rows, the defaults (A/B measurements: DESIGN.md §3, profiles/).
+// Returns with *handled = false when no bf16 MFMA kernel takes the shape (the caller then
+// runs the generic kernel).
+static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hipStream_t st,
+                                    bool* handled) {
+#ifdef MT_DIAGNOSTICS
+  if (pol != kPolDefault && pol != kPolBwdFused && pol != kPolBwdSplit)
+    return fwd_bf16_dispatch_ab(a, causal, pol, st, handled);
+#endif
+  (void)pol;
+  *handled = false;
+  hipError_t e = hipSuccess;
+  const int N = a.N;
+  const int64_t bh = (int64_t)a.B * a.H;
+  if (a.d == 64) {
+    if (!causal) {
+      // v6 (v5's schedule on the 16x16x32 MFMA, row sums on the MFMA pipe, policy 102) with
+      // at least one 8-wave workgroup per CU; with the keys split between the workgroup
+      // halves (policy 105) at one 256-query workgroup per CU (the 8-GPU C3 shard)
+      if ((int64_t)((N + 511) / 512) * bh >= 256)
+        e = launch_fwd_v6(a, false, 2, st, handled);
+      else if ((int64_t)((N + 255) / 256) * bh >= 256)
+        e = launch_fwd_v6(a, false, 18, st, handled);
+      if (!*handled) {
+        // v5: the 8-wave default (policy 56); on smaller grids its split-keys form (76), or the
+        // 4-wave form where the split does not apply (profiles/r2_ab_split.txt,
+        // r2_ab_small_grids.txt); it declines N % 64 != 0
+        const int var = (int64_t)((N + 511) / 512) * bh >= 256 ? v5::kDefault
+                        : (N % 128 == 0 && N >= 256)          ? (v5::kDefault | v5::kSplit)
+                                                              : (v5::kDma | v5::kUnroll);
+        e = launch_fwd_v5(a, false, 2, var, st, handled);
+      }
+    } else if ((int64_t)((N + 511) / 512 + 1) / 2 * bh >= 256) {
+      // causal with at least one 8-wave workgroup per CU: paired light / heavy query blocks
+      // with each wave's diagonal inside the pipeline, v6 (policy 106), else v5 (67)
+      e = launch_fwd_v6(a, true, 34, st, handled);
+      if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
+    }
+    // ragged N, short N, small causal grids: v4 (causal: paired, light block first, 8 waves
+    // from N = 8192; profiles/r1_ab_causal_pair.txt)
+    if (!*handled)
+      e = launch_fwd_v4(a, causal, causal && N >= 8192 ? 8 : 4, !causal, st, handled, causal ? 2 : 0);
+  }
+  // d = 128: 8 waves, causal with paired query blocks (profiles/r1_ab_d128_warm.txt)
+  if (!*handled && a.d == 128) e = launch_fwd_d128(a, causal, 8, false, st, handled, causal ? 2 : 0);
+  // anything else those decline (buffer range): the single-phase 8-wave kernel
+  if (!*handled) e = launch_fwd_fast(a, causal, 2, st, handled);
+  return e;
+}
 
 }  // namespace mt
 
@@ -409,7 +471,7 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
     if (handled) return check_hip(e, "mt_flash_attn_fwd(bf16)");
   }
   return check_hip(launch_fwd_generic(a, dtype == MT_BF16, vec, causal != 0, st,
-                                      pol == kPolFwdF32TwoBarrier ? 0
+                                      pol == kPolFwdF32TwoBarrier || pol == kPolGeneric ? 0
                                       : pol == kPolFwdF32Ring     ? 1
                                       : pol == kPolFwdF32RingPair ? 2
                                       // default: the ring, paired on large grids (C2 0.3209 ->
@@ -422,6 +484,9 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
 // The fused bf16 d = 64 backward keeps its dQ partial sums (bf16, N/256 per element) in the
 // workspace; their size grows as N^2, so it runs only up to N = 8192 (C3: 1 GiB).
 static bool fused_bwd_applies(int64_t N, int64_t d) { return d == 64 && N <= 8192; }
+// whether the fused backward is the bf16 d = 64 default (the split forms stay selectable,
+// policy 121)
+static constexpr bool kFusedBwdDefault = false;
 static int64_t bwd_rows_bytes(int64_t B, int64_t H, int64_t N) {
   return (2 * B * H * N * (int64_t)sizeof(float) + 255) / 256 * 256;
 }
@@ -468,42 +533,44 @@ int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k
   // mask keys >= kv_len[b]
   if (dtype == MT_BF16 && vec && pol != kPolGeneric && (!kv_len || a.slab)) {
     bool handled = false;
-    // dK/dV forms: 0 32-query steps, 1 software-pipelined, 3 64-query steps at one wave
-    // per SIMD, 4 64-query steps with LDS-DMA Q/dO, 5 the same with 8 waves (256 keys per
-    // dK/dV workgroup, 256 queries per dQ workgroup). Default: 5 non-causal (1.868 vs
-    // 1.937 ms for 4 at C3, profiles/r2_ab_bwd.txt), 0 causal (1.12 vs 1.31 ms: the masked
-    // diagonal steps spill in the 64-query form), paired (18) on large causal grids. An in-wave interleaved dQ tile measured
-    // 1.7 % slower than the plain tile and was removed (profiles/r1_ab_bwd_dq.txt).
-    const int variant = kv_len                    ? 20  // the fused kernel masks padding keys
-                        : pol == kPolBwdPipe        ? 1
-                        : pol == kPolBwdQ64OneWave ? 3
-                        : pol == kPolBwdQ64Dma     ? 4
-                        : pol == kPolBwdQ64Dma8    ? 5
-                        : pol == kPolBwdStagger    ? 11
-                        : pol == kPolBwdDqPf       ? 12
-                        : pol == kPolBwdW64        ? 13
-                        : pol == kPolBwdDqPipe     ? 14
-                        : pol == kPolBwdMix0       ? 15
-                        : pol == kPolBwdMix4       ? 16
-                        : pol == kPolBwdQ128       ? 17
-                        : pol == kPolBwdPair       ? 18
-                        : pol == kPolBwdPair8      ? 19
-                        : pol == kPolBwdFused && a.slab ? 20
+    // 20: the fused backward (dQ in the dK/dV pass, fa_bwd_fused.hip), wherever its dQ partial
+    // slab fits the workspace (N <= 8192) and kFusedBwdDefault says so; else the split forms.
+    // the split backward's defaults: dK/dV with 8 waves and LDS-DMA (variant 5, policy 69)
+    // non-causal; causal paired light / heavy blocks (18, policy 107: 1.065 vs 1.172 ms at C3
+    // causal, profiles/r2m_ab_bwd_pair.txt) once the paired dK/dV grid fills two workgroups
+    // per CU, else the 32-query form (0)
+    const int split = !causal ? 5 : (int64_t)((N + 255) / 256) * a.B * a.H >= 512 ? 18 : 0;
+    int variant = kv_len ? 20  // the fused kernel masks padding keys
+                  : pol == kPolBwdSplit ? split
+                  : pol == kPolBwdFused && a.slab ? 20
+                  : a.slab && kFusedBwdDefault ? 20
+                  : split;
 #ifdef MT_DIAGNOSTICS
-                        : (pol >= 87 && pol <= 90)  ? pol - 81  // dK/dV ablations (wrong results)
+    // A/B forms (the split kernels' dK/dV and dQ variants, fa_bwd_bf16.hip)
+    if (!kv_len && pol != kPolDefault && pol != kPolBwdFused && pol != kPolBwdSplit)
+      variant = pol == kPolBwdPipe        ? 1
+                : pol == kPolBwdQ64OneWave ? 3
+                : pol == kPolBwdQ64Dma     ? 4
+                : pol == kPolBwdQ64Dma8    ? 5
+                : pol == kPolBwdStagger    ? 11
+                : pol == kPolBwdDqPf       ? 12
+                : pol == kPolBwdW64        ? 13
+                : pol == kPolBwdDqPipe     ? 14
+                : pol == kPolBwdMix0       ? 15
+                : pol == kPolBwdMix4       ? 16
+                : pol == kPolBwdQ128       ? 17
+                : pol == kPolBwdPair       ? 18
+                : pol == kPolBwdPair8      ? 19
+                : (pol >= 87 && pol <= 90)  ? pol - 81  // dK/dV ablations (wrong results)
+                : pol == kPolBwdQ32        ? 0
+                                           : split;
 #endif
-                        : pol == kPolBwdQ32        ? 0
-                        : !causal                  ? 5
-                        // causal: paired light/heavy blocks (policy 107: 1.065 vs 1.172 ms at C3
-                        // causal, profiles/r2m_ab_bwd_pair.txt) once the paired dK/dV grid fills
-                        // two workgroups per CU; below that pairing would idle half the CUs
-                        : (int64_t)((N + 255) / 256) * a.B * a.H >= 512 ? 18 : 0;
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }
   return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream,
                                       pol == kPolBwdGenNoPair ? 0 : pol == kPolBwdGenPair ? 1 : 2,
-                                      pol != kPolBwdF32Lds),
+                                      pol != kPolBwdF32Lds && pol != kPolGeneric),
                    "mt_flash_attn_bwd");
 }
 

@@ -730,6 +730,7 @@ __global__ __launch_bounds__(64 * NW, MINB) void fa_bwd_dkv_bf16_q64(AttnArgs p,
 // the loop, so the partner of a wave in its first sub-tile is in its second. Non-causal,
 // N % 64 == 0 (every step mask-free); the launcher sends other shapes to the 64-query
 // kernel.
+#ifdef MT_DIAGNOSTICS  // an A/B form (policy 70): diagnostics build only
 __global__ __launch_bounds__(512, 2) void fa_bwd_dkv_bf16_st(AttnArgs p, int nkb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kStepB = 2 * kBufQ;  // bytes per ring step (2 sub-tiles)
@@ -843,6 +844,8 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_dkv_bf16_st(AttnArgs p, int nkb
       }
   }
 }
+
+#endif  // MT_DIAGNOSTICS
 
 // ---------------------------------------------------------------------------------------
 // ---------------------------------------------------------------------------------------
@@ -1053,9 +1056,11 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb
 }
 
 // ---------------------------------------------------------------------------------------
-hipError_t launch_dkv_w64(const AttnArgs& a, int nkb, unsigned nblk, size_t smem, hipStream_t st);
 hipError_t launch_bwd_fused(const AttnArgs& a, bool causal, bf16* slab, hipStream_t st);
+#ifdef MT_DIAGNOSTICS
+hipError_t launch_dkv_w64(const AttnArgs& a, int nkb, unsigned nblk, size_t smem, hipStream_t st);
 hipError_t launch_dq_pipe(const AttnArgs& a, int nqb, unsigned nblk, hipStream_t st);
+#endif
 
 template <bool CAUSAL>
 static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t st) {
@@ -1066,6 +1071,11 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   if (e != hipSuccess) return e;
   // 20: dQ folded into the dK/dV pass (fa_bwd_fused.hip: 5 products instead of 7)
   if (variant == 20) return launch_bwd_fused(a, CAUSAL, (bf16*)a.slab, st);
+#ifndef MT_DIAGNOSTICS
+  // product build: the split defaults 5 (non-causal), 18 / 0 (causal paired / not); the
+  // other forms are A/B policies of the diagnostics build
+  if (variant != 0 && variant != 5 && variant != 18) variant = CAUSAL ? 0 : 5;
+#endif
   // variant -> (dK/dV form, dQ form). dK/dV: 0 32-query steps (128 keys), 1 software-
   // pipelined, 3 / 4 64-query steps (one wave per SIMD / LDS-DMA), 5 the 8-wave LDS-DMA form
   // (256 keys), 11 staggered SIMD partners, 13 one wave per SIMD with 64 keys per wave.
@@ -1091,22 +1101,27 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     const int64_t nblk = (int64_t)(pair ? (nkb + 1) / 2 : nkb) * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
     const size_t smem = (dkv == 11 || dkv == 17 ? 8 : (dkv == 1 || dkv == 13) ? 3 : dkv >= 2 ? 4 : 2) * (size_t)kBufQ;
+#ifndef MT_DIAGNOSTICS
+    auto kfn = dkv == 5 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
+               : pair   ? fa_bwd_dkv_bf16<CAUSAL, true>
+                        : fa_bwd_dkv_bf16<CAUSAL>;
+#else
     auto kfn = dkv == 1   ? fa_bwd_dkv_bf16_p<CAUSAL>
                : dkv == 3 ? fa_bwd_dkv_bf16_q64<CAUSAL, 1>
                : dkv == 4 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true>
                : dkv == 5 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
                : dkv == 11 ? fa_bwd_dkv_bf16_st
                : dkv == 17 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 0, 4>
-#ifdef MT_DIAGNOSTICS
                : dkv == 6 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 1>
                : dkv == 7 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 2>
                : dkv == 8 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 6>
                : dkv == 9 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 7>
-#endif
                           : pair ? fa_bwd_dkv_bf16<CAUSAL, true> : fa_bwd_dkv_bf16<CAUSAL>;
     if (dkv == 13) {
       e = launch_dkv_w64(a, nkb, (unsigned)nblk, smem, st);
-    } else {
+    } else
+#endif
+    {
       e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(nthr), smem, st, a, nkb);
@@ -1119,10 +1134,15 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     const int nqb = (a.N + kqb - 1) / kqb;
     const int64_t nblk = (int64_t)(pair ? (nqb + 1) / 2 : nqb) * a.B * a.H;
     const size_t smem = 2 * (size_t)kBufK;
+#ifndef MT_DIAGNOSTICS
+    auto kfn = pair ? fa_bwd_dq_bf16<CAUSAL, 4, false, true>
+               : dq == 8 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
+#else
     if (dq == 14) return launch_dq_pipe(a, nqb, (unsigned)nblk, st);
     auto kfn = dq == 12 ? fa_bwd_dq_bf16<CAUSAL, 8, true>
                : pair ? (dq == 8 ? fa_bwd_dq_bf16<CAUSAL, 8, false, true> : fa_bwd_dq_bf16<CAUSAL, 4, false, true>)
                : dq == 8 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
+#endif
     e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(kqb * 2), smem, st, a, nqb);

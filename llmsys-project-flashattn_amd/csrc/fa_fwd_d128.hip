@@ -433,6 +433,13 @@ hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hip
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
+#ifndef MT_DIAGNOSTICS
+  // product build: 8 waves, causal paired light-first (the defaults); the rest are A/B policies
+  (void)nw;
+  (void)dma;
+  (void)pair;
+  return causal ? launch_d128_t<true, 8, false, 2>(a, st) : launch_d128_t<false, 8>(a, st);
+#else
   if (causal && pair == 2)
     return nw == 8 ? launch_d128_t<true, 8, false, 2>(a, st) : launch_d128_t<true, 4, false, 2>(a, st);
   if (causal && pair)
@@ -443,6 +450,7 @@ hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hip
   }
   if (nw == 8) return causal ? launch_d128_t<true, 8>(a, st) : launch_d128_t<false, 8>(a, st);
   return causal ? launch_d128_t<true, 4>(a, st) : launch_d128_t<false, 4>(a, st);
+#endif
 }
 
 }  // namespace mt

@@ -799,6 +799,11 @@ hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStrea
                            : LAUNCH<64, false, ##__VA_ARGS__>(a, st))                    \
                  : (causal ? LAUNCH<128, true, ##__VA_ARGS__>(a, st)                     \
                            : LAUNCH<128, false, ##__VA_ARGS__>(a, st));
+#ifndef MT_DIAGNOSTICS
+  // product build: the single-phase 8-wave kernel (the default fallback); the others are A/B
+  (void)variant;
+  MT_DISPATCH(launch_fast_t, 8)
+#else
   switch (variant) {
     case 2: MT_DISPATCH(launch_fast_t, 8)
     case 4: MT_DISPATCH(launch_sp2_t, 8)
@@ -806,7 +811,6 @@ hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStrea
     case 6: MT_DISPATCH(launch_pp_t)
     default: break;
   }
-#ifdef MT_DIAGNOSTICS
   if (variant >= 10 && variant <= 15 && d == 64 && !causal) {  // diagnostics
     switch (variant) {
       case 10: return launch_fast_t<64, false, 8, 0>(a, st);
@@ -817,8 +821,8 @@ hipError_t launch_fwd_fast(const AttnArgs& a, bool causal, int variant, hipStrea
       default: return launch_fast_t<64, false, 8, 5>(a, st);
     }
   }
-#endif
   MT_DISPATCH(launch_fast_t, 4)
+#endif
 #undef MT_DISPATCH
 }
 

@@ -467,12 +467,12 @@ hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st) {
     default: return launch_v4_t<false, 4, true, 6>(a, st);
   }
 }
-#endif
 
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st) {
   if (pk) return causal ? launch_v4_t<true, 4, true, 0, true>(a, st) : launch_v4_t<false, 4, true, 0, true>(a, st);
   return causal ? launch_v4_t<true, 4, false, 0, true>(a, st) : launch_v4_t<false, 4, false, 0, true>(a, st);
 }
+#endif  // MT_DIAGNOSTICS
 
 hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStream_t st,
                          bool* handled, int pair) {
@@ -482,6 +482,16 @@ hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStr
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
+#ifndef MT_DIAGNOSTICS
+  // product build: the default forms only (causal: paired blocks, light first; non-causal:
+  // 4 waves with the packed softmax); the others are A/B policies of the diagnostics build
+  (void)pk;
+  (void)pair;
+  if (causal)
+    return nw == 8 ? launch_v4_t<true, 8, false, 0, false, 2>(a, st)
+                   : launch_v4_t<true, 4, false, 0, false, 2>(a, st);
+  return launch_v4_t<false, 4, true>(a, st);
+#else
   if (causal && pair == 2)
     return nw == 8 ? launch_v4_t<true, 8, false, 0, false, 2>(a, st)
                    : launch_v4_t<true, 4, false, 0, false, 2>(a, st);
@@ -494,6 +504,7 @@ hipError_t launch_fwd_v4(const AttnArgs& a, bool causal, int nw, bool pk, hipStr
   }
   if (nw == 8) return causal ? launch_v4_t<true, 8, false>(a, st) : launch_v4_t<false, 8, false>(a, st);
   return causal ? launch_v4_t<true, 4, false>(a, st) : launch_v4_t<false, 4, false>(a, st);
+#endif
 }
 
 }  // namespace mt

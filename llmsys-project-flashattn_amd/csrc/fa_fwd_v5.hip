@@ -730,6 +730,17 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
   void (*kfn)(AttnArgs, int);
   const int nw = (var & 2048) ? 8 : 4;  // VAR bit 2048 (launcher only): 8 waves per workgroup
   var &= ~2048;
+#ifndef MT_DIAGNOSTICS
+  // product build: the default forms only (causal paired 8-wave; non-causal 8-wave, its
+  // split-keys form, the 4-wave LDS-DMA form of small grids); the rest are A/B policies
+  (void)ahead;
+  if (causal)
+    kfn = fa_fwd_bf16_v5<2, 99332, true, 8>;
+  else if (nw == 8)
+    kfn = split ? fa_fwd_bf16_v5<2, 230404, false, 8> : fa_fwd_bf16_v5<2, 99332, false, 8>;
+  else
+    kfn = fa_fwd_bf16_v5<2, 1028, false>;
+#else
   if (causal)  // paired query blocks, pipelined diagonal (8 or 4 waves), or the 4-wave forms
     kfn = var == 99332 ? (nw == 8 ? fa_fwd_bf16_v5<2, 99332, true, 8> : fa_fwd_bf16_v5<2, 99332, true, 4>)
           : var == 4   ? fa_fwd_bf16_v5<2, 4, true>
@@ -773,6 +784,7 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
           : ahead >= 6 ? fa_fwd_bf16_v5<6, 0, false>
           : ahead >= 4 ? fa_fwd_bf16_v5<4, 0, false>
                        : fa_fwd_bf16_v5<2, 0, false>;
+#endif
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
   const int kBQ = split ? 256 : 64 * nw;

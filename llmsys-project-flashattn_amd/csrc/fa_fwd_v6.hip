@@ -596,14 +596,14 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   *handled = true;
   const size_t smem = (size_t)(split ? 2 : 1) * (kKSlots + kVSlots) * TILE * sizeof(bf16);
   void (*kern)(AttnArgs, int) = nullptr;
-  switch (var) {
-    case 0: kern = fa_fwd_bf16_v6<0>; break;
+  switch (var) {  // product build: the defaults 2 / 18 / 34; the rest are A/B policies
     case 2: kern = fa_fwd_bf16_v6<2>; break;
-    case 6: kern = fa_fwd_bf16_v6<6>; break;
-    case 10: kern = fa_fwd_bf16_v6<10>; break;
     case 18: kern = fa_fwd_bf16_v6<18>; break;
     case 34: kern = fa_fwd_bf16_v6<34>; break;
 #ifdef MT_DIAGNOSTICS
+    case 0: kern = fa_fwd_bf16_v6<0>; break;
+    case 6: kern = fa_fwd_bf16_v6<6>; break;
+    case 10: kern = fa_fwd_bf16_v6<10>; break;
     case 1: kern = fa_fwd_bf16_v6<1>; break;
 #endif
     default: return hipErrorInvalidValue;

@@ -15,7 +15,10 @@ import os
 from typing import Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libminitorch_hip.so")
+# MT_HIP_LIB: another build of the library (diagnostics: _lib/diag/libminitorch_hip_diag.so,
+# `make DIAG=1`, which adds the A/B kernel policies) for tests and scripts; the package
+# default is the product library
+LIB_PATH = os.environ.get("MT_HIP_LIB") or os.path.join(_HERE, "_lib", "libminitorch_hip.so")
 
 MT_F32 = 0
 MT_BF16 = 1

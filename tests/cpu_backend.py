@@ -120,28 +120,33 @@ class NumpyOps(TensorOps):
         return _new(dx, b), _new((dy * xh).sum(0)[None], b), _new(dy.sum(0)[None], b)
 
     @staticmethod
-    def _fw(Q, K, V, causal):
-        o, m, l = A.attention_fwd(_arr(Q), _arr(K), _arr(V), causal)
+    def _kv(kv_len):
+        return None if kv_len is None else _arr(kv_len).reshape(-1).astype(np.int64)
+
+    @staticmethod
+    def _fw(Q, K, V, causal, kv_len=None):
+        o, m, l = A.attention_fwd(_arr(Q), _arr(K), _arr(V), causal, NumpyOps._kv(kv_len))
         b = Q.backend
         return _new(o, b), _new(m, b), _new(l, b)
 
     @staticmethod
-    def _bw(Q, K, V, O, dO, m, l, causal):
-        g = A.attention_bwd(_arr(Q), _arr(K), _arr(V), _arr(O), _arr(dO), _arr(m), _arr(l), causal)
+    def _bw(Q, K, V, O, dO, m, l, causal, kv_len=None):
+        g = A.attention_bwd(_arr(Q), _arr(K), _arr(V), _arr(O), _arr(dO), _arr(m), _arr(l), causal,
+                            NumpyOps._kv(kv_len))
         return tuple(_new(x, Q.backend) for x in g)
 
     @staticmethod
-    def flash_attention_fw(Q, K, V):
-        return NumpyOps._fw(Q, K, V, False)
+    def flash_attention_fw(Q, K, V, kv_len=None):
+        return NumpyOps._fw(Q, K, V, False, kv_len)
 
     @staticmethod
-    def flash_attention_bw(Q, K, V, O, dO, m, l):
-        return NumpyOps._bw(Q, K, V, O, dO, m, l, False)
+    def flash_attention_bw(Q, K, V, O, dO, m, l, kv_len=None):
+        return NumpyOps._bw(Q, K, V, O, dO, m, l, False, kv_len)
 
     @staticmethod
-    def flash_attention_causal_fw(Q, K, V):
-        return NumpyOps._fw(Q, K, V, True)
+    def flash_attention_causal_fw(Q, K, V, kv_len=None):
+        return NumpyOps._fw(Q, K, V, True, kv_len)
 
     @staticmethod
-    def flash_attention_causal_bw(Q, K, V, O, dO, m, l):
-        return NumpyOps._bw(Q, K, V, O, dO, m, l, True)
+    def flash_attention_causal_bw(Q, K, V, O, dO, m, l, kv_len=None):
+        return NumpyOps._bw(Q, K, V, O, dO, m, l, True, kv_len)

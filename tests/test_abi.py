@@ -70,11 +70,30 @@ def test_kernel_policy_switch_rejects_unknown_ids():
         assert lib.mt_flash_set_kernel_policy(bad) != 0, bad
         assert b"unknown policy" in lib.mt_last_error()
         assert lib.mt_flash_get_kernel_policy() == 0
-    with _hip.policy(56):
-        assert lib.mt_flash_get_kernel_policy() == 56
+    with _hip.policy(120):
+        assert lib.mt_flash_get_kernel_policy() == 120
     assert lib.mt_flash_get_kernel_policy() == 0
     with pytest.raises(RuntimeError):
         _hip.set_policy(97)
+
+
+def test_product_library_policy_list():
+    """The product library ships the kernels some default selects, and its policy switch takes
+    exactly 0 (defaults), 1 (generic kernels), 120 / 121 (fused / split bf16 backward); the
+    A/B schedules are in the diagnostics build (make DIAG=1)."""
+    from minitorch import _hip
+    if os.environ.get("MT_HIP_LIB"):
+        pytest.skip("a non-product library is loaded")
+    lib = _hip.lib()
+    accepted = [p for p in range(0, 200) if lib.mt_flash_set_kernel_policy(p) == 0]
+    lib.mt_flash_set_kernel_policy(0)
+    assert accepted == [0, 1, 120, 121]
+    import subprocess
+    syms = subprocess.run(["nm", "-C", "--defined-only", _hip.LIB_PATH], capture_output=True,
+                          text=True).stdout
+    for absent in ("fa_bwd_dkv_bf16_w64", "fa_bwd_dq_pipe", "fa_bwd_dkv_bf16_st", "fa_fwd_bf16_sp2",
+                   "fa_fwd_bf16_pp", "launch_fwd_v4_deep"):
+        assert absent not in syms, absent
 
 
 def test_product_library_has_no_ablation_kernels():

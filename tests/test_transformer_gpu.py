@@ -81,7 +81,7 @@ def test_decoder_lm_step_hip_vs_cpu(mt, parity_record):
     from cpu_backend import NumpyOps
     _, hip = mt
     cpu = minitorch.TensorBackend(NumpyOps)
-    V, E, H, B, T = 10000, 256, 8, 2, 39
+    V, E, H, B, T = 10000, 256, 8, 4, 39
     kw = dict(n_vocab=V, n_embd=E, n_head=H, n_positions=40, p_dropout=0.0,
               use_fused_kernel=True, use_flash_attention=True)
     lm_h = minitorch.DecoderLM(backend=hip, **kw)
@@ -91,13 +91,19 @@ def test_decoder_lm_step_hip_vs_cpu(mt, parity_record):
     for name, p in ph.items():  # the HIP model's random init, copied to the CPU model
         pc[name].update(minitorch.tensor_from_numpy(p.value.to_numpy().copy(), cpu))
     rng = np.random.default_rng(7)
-    idx = rng.integers(0, V, (B, T)).astype(np.float32)
-    tgt = rng.integers(0, V, (B * T,)).astype(np.float32)
+    # a right-padded batch with the reference's loss weights (run_machine_translation.py:
+    # 119-141, 186-192): source tokens weight 0, target tokens 1, padding 0; the flash path
+    # masks the padding keys (kv_len)
+    from bench import synthetic_mt_batch
+    batch = synthetic_mt_batch(rng, B, T, V)
+    idx, tgt, w, kv = batch["input_ids"], batch["labels"], batch["label_token_weights"], batch["kv_len"]
 
     def step(lm, backend):
-        logits = lm(minitorch.tensor_from_numpy(idx, backend))
+        logits = lm(minitorch.tensor_from_numpy(idx, backend), kv_len=kv)
         loss = minitorch.softmax_loss(logits.view(B * T, V),
-                                      minitorch.tensor_from_numpy(tgt, backend)).sum() / (B * T)
+                                      minitorch.tensor_from_numpy(tgt.reshape(-1), backend))
+        wt = minitorch.tensor_from_numpy(w.reshape(-1), backend)
+        loss = (loss * wt).sum() / wt.sum()
         loss.backward()
         return loss.item()
 
@@ -117,5 +123,5 @@ def test_decoder_lm_step_hip_vs_cpu(mt, parity_record):
         err = float(np.abs(a - b).max()) / scale
         assert err <= 1e-4, f"{name}: max|Δgrad| / scale = {err:.2e}"
         worst = max(worst, err)
-    parity_record("test_decoder_lm_step_hip_vs_cpu", f"V={V} E={E} H={H} B={B} T={T}",
+    parity_record("test_decoder_lm_step_hip_vs_cpu", f"V={V} E={E} H={H} B={B} T={T} padded, weighted loss",
                   loss_hip=loss_h, loss_cpu=loss_c, worst_rel_grad=worst, bound_rel_grad=1e-4)
