@@ -484,9 +484,10 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
 // The fused bf16 d = 64 backward keeps its dQ partial sums (bf16, N/256 per element) in the
 // workspace; their size grows as N^2, so it runs only up to N = 8192 (C3: 1 GiB).
 static bool fused_bwd_applies(int64_t N, int64_t d) { return d == 64 && N <= 8192; }
-// whether the fused backward is the bf16 d = 64 default (the split forms stay selectable,
-// policy 121)
-static constexpr bool kFusedBwdDefault = false;
+// the fused backward is the bf16 d = 64 default where it applies: C3 1.643 vs 1.872 ms
+// non-causal, 0.991 vs 1.084 ms causal against the split defaults (interleaved A/B on one box,
+// profiles/r3_ab_bwd_fused.txt); the split forms stay selectable (policy 121)
+static constexpr bool kFusedBwdDefault = true;
 static int64_t bwd_rows_bytes(int64_t B, int64_t H, int64_t N) {
   return (2 * B * H * N * (int64_t)sizeof(float) + 255) / 256 * 256;
 }

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   // then exactly zero, as the dS image needs, and a wave-level skip would be a branch around
   // the accumulators (copies and spills in the masked steps).
   const int nhead = k0 + kKB > Nk ? nstep : CAUSAL ? min(nstep, kKB / kStep) : 0;
-  const int nfull = max(nhead, (N - qt0) / kStep);
+  const int nfull = min(nstep, max(nhead, (N - qt0) / kStep));
 #define FSUB(MASK_, SLOT_, T_, U_)                                                       \
   {                                                                                      \
     const int qt_ = qt0 + (T_) * kStep + (U_) * kQT;                                     \

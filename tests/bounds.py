@@ -11,12 +11,15 @@ elementwise, with |·| taken before the products:
 
 where |dS| = P ∘ (|dP − δ| + Δδ) and Δδ = 2^-8 · rowsum(|dO| ∘ |O|) covers δ = rowsum(dO ∘ O)
 being formed from the bf16-rounded O. r = 2^-7 is twice the two roundings (operand +
-output) each product sees. The products are formed in fp64 from the same bf16-rounded
-inputs the kernels read.
+output) each product sees. dQ gets r_dq = 1.5 · 2^-7, twice three roundings: the fused
+backward (csrc/fa_bwd_fused.hip) also rounds each 256-key block's partial sum of dS·K to
+bf16 before the ordered sum (|partial| <= Σ over the block of |dS||K|). The products are
+formed in fp64 from the same bf16-rounded inputs the kernels read.
 """
 import numpy as np
 
 R_BF16 = 2.0 ** -7
+R_BF16_DQ = 1.5 * 2.0 ** -7
 
 
 def head_terms(q, k, v, do, causal, kv=None):
@@ -43,9 +46,10 @@ def head_terms(q, k, v, do, causal, kv=None):
     return P, absdS, sc
 
 
-def grad_bounds(q, k, v, do, causal, atol=1e-3, r=R_BF16, kv=None):
+def grad_bounds(q, k, v, do, causal, atol=1e-3, r=R_BF16, kv=None, r_dq=None):
     P, absdS, sc = head_terms(q, k, v, do, causal, kv)
     q, k, do = (np.abs(np.asarray(a, np.float64)) for a in (q, k, do))
-    return (atol + r * sc * (absdS @ k),      # dQ
+    r_dq = r * R_BF16_DQ / R_BF16 if r_dq is None else r_dq
+    return (atol + r_dq * sc * (absdS @ k),   # dQ
             atol + r * sc * (absdS.T @ q),    # dK
             atol + r * (P.T @ do))            # dV
