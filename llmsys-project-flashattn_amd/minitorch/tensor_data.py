@@ -8,6 +8,7 @@ once; nothing moves back implicitly (``to_numpy`` is an explicit copy).
 """
 from __future__ import annotations
 
+import functools
 import random
 from typing import Iterable, Optional, Sequence, Tuple, Union
 
@@ -96,16 +97,21 @@ class TensorData:
             size *= s
         self.size = size
 
-    # NumPy forms of shape / strides, built on first use (the index helpers and the CPU
-    # backend take them); the device path never needs them, and building two arrays per
-    # tensor was a measurable share of minitorch's per-op host time in the config-5 step
-    @property
+    # NumPy forms of shape / strides, built on first use and cached (shape and strides are
+    # fixed at construction; the index helpers and the CPU backend take these forms); the
+    # device path never needs them, and building two arrays per tensor was a measurable
+    # share of minitorch's per-op host time in the config-5 step
+    @functools.cached_property
     def _shape(self) -> np.ndarray:
-        return np.array(self.shape, dtype=np.int64)
+        a = np.array(self.shape, dtype=np.int64)
+        a.flags.writeable = False
+        return a
 
-    @property
+    @functools.cached_property
     def _strides(self) -> np.ndarray:
-        return np.array(self.strides, dtype=np.int64)
+        a = np.array(self.strides, dtype=np.int64)
+        a.flags.writeable = False
+        return a
 
     # ---- placement --------------------------------------------------------------
     @property
