@@ -154,6 +154,16 @@ void mt_set_gemm_backend(int backend);
  * copy a host mask per call. */
 int mt_rand_uniform(float* out, int64_t n, uint64_t seed, void* stream);
 
+/* Multi-tensor Adam step over n_tensors dense fp32 device tensors (parameters, their
+ * gradients, first and second moments, numels[t] elements each), in place:
+ *   m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2;  p -= step_size m / (sqrt(v) + eps)
+ * step_size = lr sqrt(1 - b2^t) / (1 - b1^t) (host-computed bias correction). Replaces the
+ * reference's per-parameter tensor-op Adam (minitorch/optim.py:52-75), one launch per 24
+ * tensors. */
+int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                 float* const* exp_avg_sq, const int64_t* numels, float beta1, float beta2, float eps,
+                 float step_size, void* stream);
+
 /* ---- reference-compatible host-pointer wrappers (companion + combine) ----- */
 /* reference src/softmax_kernel.cu:233 (stream: hipStream_t) */
 void launch_attn_softmax(float* inp, const float* attn_mask, int batch_size, int nhead,

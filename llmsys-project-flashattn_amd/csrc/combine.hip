@@ -249,6 +249,56 @@ __global__ void rand_uniform_kernel(float* out, int64_t n, uint64_t seed) {
   }
 }
 
+// Multi-tensor Adam (minitorch/optim.py Adam.step, reference minitorch/optim.py:52-75 with
+// the second moment on (1 - beta2)): for every element of every listed tensor
+//   m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g g;  p = p - step_size m / (sqrt(v) + eps)
+// with step_size = lr sqrt(1 - b2^t) / (1 - b1^t) from the host, in the op-by-op path's
+// order and roundings (no contraction). One launch per kAdamMax tensors: workgroup blocks
+// [blk0[t], blk0[t + 1]) take tensor t, 4 elements a lane when the tensor allows it.
+constexpr int kAdamMax = 24;
+struct AdamArgs {
+  float* p[kAdamMax];
+  const float* g[kAdamMax];
+  float* m[kAdamMax];
+  float* v[kAdamMax];
+  int64_t n[kAdamMax];
+  int blk0[kAdamMax + 1];
+  int nt;
+  float b1, b2, c1, c2, step, eps;  // c1 = 1 - b1, c2 = 1 - b2
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a) {
+  m = __fadd_rn(__fmul_rn(m, a.b1), __fmul_rn(g, a.c1));
+  v = __fadd_rn(__fmul_rn(v, a.b2), __fmul_rn(__fmul_rn(g, g), a.c2));
+  p = __fsub_rn(p, __fdiv_rn(__fmul_rn(a.step, m), __fadd_rn(__fsqrt_rn(v), a.eps)));
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  int t = 0;
+  while (t + 1 < a.nt && (int)blockIdx.x >= a.blk0[t + 1]) ++t;
+  const int64_t n = a.n[t];
+  const int64_t base = (int64_t)(blockIdx.x - a.blk0[t]) * 1024;
+  float* P = a.p[t];
+  const float* G = a.g[t];
+  float* M = a.m[t];
+  float* V = a.v[t];
+  const bool vec = ((((uintptr_t)P | (uintptr_t)G | (uintptr_t)M | (uintptr_t)V) & 15) == 0);
+  const int64_t i = base + 4 * threadIdx.x;
+  if (vec && i + 4 <= n) {
+    float4 p = *(float4*)(P + i), m = *(float4*)(M + i), v = *(float4*)(V + i);
+    const float4 g = *(const float4*)(G + i);
+    adam_elem(p.x, g.x, m.x, v.x, a);
+    adam_elem(p.y, g.y, m.y, v.y, a);
+    adam_elem(p.z, g.z, m.z, v.z, a);
+    adam_elem(p.w, g.w, m.w, v.w, a);
+    *(float4*)(P + i) = p;
+    *(float4*)(M + i) = m;
+    *(float4*)(V + i) = v;
+  } else {
+    for (int64_t j = i; j < min(i + 4, n); ++j) adam_elem(P[j], G[j], M[j], V[j], a);
+  }
+}
+
 extern "C" {
 
 int mt_tensor_map(int fn, float* out, const int64_t* out_shape, const int64_t* out_strides,
@@ -389,6 +439,35 @@ int mt_rand_uniform(float* out, int64_t n, uint64_t seed, void* stream) {
   hipLaunchKernelGGL(rand_uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                      out, n, seed);
   return check_hip(hipGetLastError(), "mt_rand_uniform");
+}
+
+int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                 float* const* exp_avg_sq, const int64_t* numels, float beta1, float beta2, float eps,
+                 float step_size, void* stream) {
+  if (n_tensors < 0) return set_error("mt_adam_step: n_tensors = %d", n_tensors);
+  for (int t0 = 0; t0 < n_tensors; t0 += kAdamMax) {
+    AdamArgs a;
+    memset(&a, 0, sizeof(a));
+    a.b1 = beta1; a.b2 = beta2; a.c1 = 1.f - beta1; a.c2 = 1.f - beta2;
+    a.step = step_size; a.eps = eps;
+    int64_t blocks = 0;
+    for (int t = t0; t < std::min(n_tensors, t0 + kAdamMax); ++t) {
+      if (numels[t] < 0) return set_error("mt_adam_step: numel %lld", (long long)numels[t]);
+      if (numels[t] == 0) continue;
+      if (!params[t] || !grads[t] || !exp_avg[t] || !exp_avg_sq[t]) return set_error("mt_adam_step: null pointer");
+      a.p[a.nt] = params[t]; a.g[a.nt] = grads[t]; a.m[a.nt] = exp_avg[t]; a.v[a.nt] = exp_avg_sq[t];
+      a.n[a.nt] = numels[t];
+      a.blk0[a.nt] = (int)blocks;
+      blocks += (numels[t] + 1023) / 1024;
+      if (blocks > 0x7fffffff) return set_error("mt_adam_step: too many elements");
+      ++a.nt;
+    }
+    if (a.nt == 0) continue;
+    a.blk0[a.nt] = (int)blocks;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    if (check_hip(hipGetLastError(), "mt_adam_step")) return 1;
+  }
+  return 0;
 }
 
 }  // extern "C"

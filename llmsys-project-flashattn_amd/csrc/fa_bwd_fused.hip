@@ -458,7 +458,9 @@ int64_t bwd_fused_slab_bytes(int64_t B, int64_t H, int64_t N) {
 }
 
 // The fused pass and the dQ reduce (after fa_bwd_prep_bf16). slab: bwd_fused_slab_bytes
-// bytes, 16-B aligned.
+// bytes, 16-B aligned. (Launching the pair per group of batch rows, so that a group's
+// partials stay in the Infinity Cache for the reduce, measured 1 % faster at C3:
+// profiles/r3_ab_bwd_chunk.txt; not kept.)
 hipError_t launch_bwd_fused(const AttnArgs& a, bool causal, bf16* slab, hipStream_t st) {
   const int nkb = (a.N + kKB - 1) / kKB, nsa = (a.N + kStep - 1) / kStep;
   // causal: light/heavy pairs while the paired grid still has a workgroup per CU

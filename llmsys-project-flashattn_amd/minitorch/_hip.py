@@ -31,6 +31,7 @@ _vp = ctypes.c_void_p
 _fp = ctypes.POINTER(ctypes.c_float)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 _ip = ctypes.POINTER(ctypes.c_int)
+_vpp = ctypes.POINTER(ctypes.c_void_p)
 
 # name -> (restype, argtypes); mirrors include/minitorch_hip.h
 _PROTOS = {
@@ -59,6 +60,8 @@ _PROTOS = {
                                 ctypes.c_float, _vp]),
     "mt_matmul_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _i64p, _i64p, _vp]),
     "mt_rand_uniform": (_int, [_vp, _i64, ctypes.c_uint64, _vp]),
+    "mt_adam_step": (_int, [_int, _vpp, _vpp, _vpp, _vpp, _i64p, ctypes.c_float, ctypes.c_float,
+                            ctypes.c_float, ctypes.c_float, _vp]),
     "mt_set_gemm_backend": (None, [_int]),
     "launch_attn_softmax": (None, [_fp, _fp, _int, _int, _int, _int, ctypes.c_bool, _vp]),
     "launch_attn_softmax_bw": (None, [_fp, _fp, _int, _int, _vp]),
@@ -261,3 +264,13 @@ def flash_bwd(q, k, v, o, do, m, l, causal: bool = False, dq=None, dk=None, dv=N
 
 def exported_symbols() -> Sequence[str]:
     return tuple(_PROTOS)
+
+
+def adam_step(params, grads, exp_avg, exp_avg_sq, numels, beta1, beta2, eps, step_size) -> None:
+    """One multi-tensor Adam launch (mt_adam_step) over dense fp32 device buffers given as
+    raw pointers, in place, on the current stream."""
+    n = len(params)
+    arr = ctypes.c_void_p * max(1, n)
+    check(lib().mt_adam_step(n, arr(*params), arr(*grads), arr(*exp_avg), arr(*exp_avg_sq),
+                              (ctypes.c_int64 * max(1, n))(*numels), beta1, beta2, eps, step_size,
+                              stream_ptr()), "mt_adam_step")

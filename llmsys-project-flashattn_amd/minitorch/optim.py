@@ -1,5 +1,10 @@
 """Optimizers (reference ``minitorch/optim.py``). The reference's Adam uses
-``(1 - beta1)`` for the second moment (optim.py:70); this one uses ``(1 - beta2)``."""
+``(1 - beta1)`` for the second moment (optim.py:68); this one uses ``(1 - beta2)``.
+
+On the HIP backend, Adam updates every parameter whose value, gradient and moments are
+dense fp32 device buffers in one multi-tensor kernel (``mt_adam_step``, in place, the same
+arithmetic and order as the tensor-op form below); anything else takes the tensor-op form,
+which is also the CPU backend's path."""
 from __future__ import annotations
 
 import math
@@ -36,6 +41,7 @@ class Adam(Optimizer):
         self._states = {id(p): {} for p in parameters}
 
     def step(self) -> None:
+        fused = {}  # step count -> [(param, grad, state)]
         for p in self.parameters:
             grad = getattr(p.value, "grad", None) if p.value is not None else None
             if grad is None:
@@ -46,10 +52,35 @@ class Adam(Optimizer):
                 st["exp_avg"] = grad.zeros()
                 st["exp_avg_sq"] = grad.zeros()
             st["step"] += 1
+            if _fusable(p.value, grad, st["exp_avg"], st["exp_avg_sq"]):
+                fused.setdefault(st["step"], []).append((p, grad, st))
+                continue
             st["exp_avg"] = st["exp_avg"] * self.beta1 + grad * (1 - self.beta1)
             st["exp_avg_sq"] = st["exp_avg_sq"] * self.beta2 + (grad * grad) * (1 - self.beta2)
-            bc1 = 1.0 - self.beta1 ** st["step"]
-            bc2 = 1.0 - self.beta2 ** st["step"]
-            step_size = self.lr * math.sqrt(bc2) / bc1
-            denom = st["exp_avg_sq"] ** 0.5 + self.eps
-            p.update(p.value.detach() - step_size * st["exp_avg"] / denom)
+            p.update(p.value.detach() - self._step_size(st["step"]) * st["exp_avg"] / (st["exp_avg_sq"] ** 0.5 + self.eps))
+        for t, group in fused.items():
+            from . import _hip
+            _hip.adam_step([p.value._tensor.data_ptr() for p, _, _ in group],
+                           [g._tensor.data_ptr() for _, g, _ in group],
+                           [st["exp_avg"]._tensor.data_ptr() for _, _, st in group],
+                           [st["exp_avg_sq"]._tensor.data_ptr() for _, _, st in group],
+                           [p.value._tensor.size for p, _, _ in group],
+                           self.beta1, self.beta2, self.eps, self._step_size(t))
+
+    def _step_size(self, t: int) -> float:
+        bc1 = 1.0 - self.beta1 ** t
+        bc2 = 1.0 - self.beta2 ** t
+        return self.lr * math.sqrt(bc2) / bc1
+
+
+def _fusable(*ts) -> bool:
+    """Dense fp32 device buffers of one size, each exactly its tensor (no view offset)."""
+    n = ts[0]._tensor.size
+    for t in ts:
+        td = t._tensor
+        if not td.on_device or td.size != n or not td.is_dense():
+            return False
+        st = td._storage
+        if st.dtype.itemsize != 4 or not st.dtype.is_floating_point or st.numel() != n or st.storage_offset() != 0:
+            return False
+    return True
