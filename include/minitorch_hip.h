@@ -31,7 +31,9 @@
 extern "C" {
 #endif
 
-enum { MT_F32 = 0, MT_BF16 = 1 };
+/* MT_BF16_F32OUT (forward only): bf16 Q/K/V with an fp32 O (16-B aligned rows, strides
+ * multiples of 4), the bf16 path without the final rounding of O to bf16. */
+enum { MT_F32 = 0, MT_BF16 = 1, MT_BF16_F32OUT = 2 };
 
 /* ---- status ------------------------------------------------------------- */
 const char* mt_last_error(void);
@@ -157,12 +159,13 @@ int mt_rand_uniform(float* out, int64_t n, uint64_t seed, void* stream);
 /* Multi-tensor Adam step over n_tensors dense fp32 device tensors (parameters, their
  * gradients, first and second moments, numels[t] elements each), in place:
  *   m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2;  p -= step_size m / (sqrt(v) + eps)
- * step_size = lr sqrt(1 - b2^t) / (1 - b1^t) (host-computed bias correction). Replaces the
+ * step_size = lr sqrt(1 - b2^t) / (1 - b1^t) (host-computed bias correction); b1, b2,
+ * 1 - b1, 1 - b2, eps and step_size are each rounded to fp32 once. Replaces the
  * reference's per-parameter tensor-op Adam (minitorch/optim.py:52-75), one launch per 24
  * tensors. */
 int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
-                 float* const* exp_avg_sq, const int64_t* numels, float beta1, float beta2, float eps,
-                 float step_size, void* stream);
+                 float* const* exp_avg_sq, const int64_t* numels, double beta1, double beta2, double eps,
+                 double step_size, void* stream);
 
 /* ---- reference-compatible host-pointer wrappers (companion + combine) ----- */
 /* reference src/softmax_kernel.cu:233 (stream: hipStream_t) */

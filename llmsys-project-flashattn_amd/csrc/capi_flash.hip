@@ -446,12 +446,18 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
                              int64_t d, const int64_t* q_strides, const int64_t* k_strides,
                              const int64_t* v_strides, const int64_t* o_strides,
                              const int* kv_len, void* stream) {
+  const bool f32o = dtype == MT_BF16_F32OUT;
+  if (f32o) dtype = MT_BF16;
   if (check_sizes(dtype, B, H, N, d)) return 1;
   if (!q || !k || !v || !o) return set_error("mt_flash_attn_fwd: null tensor pointer");
   AttnArgs a;
   memset(&a, 0, sizeof(a));
   a.q = q; a.k = k; a.v = v; a.out = o; a.m = m; a.l = l;
   a.kv_len = kv_len;
+  a.o_f32 = f32o ? 1 : 0;
+#ifdef MT_DIAGNOSTICS
+  if (const char* kn = getenv("MT_KNOB")) a.knob = atoi(kn);
+#endif
   fill_strides(a.sq, q_strides, H, N, d);
   fill_strides(a.sk, k_strides, H, N, d);
   fill_strides(a.sv, v_strides, H, N, d);
@@ -461,6 +467,8 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
   a.scale_log2 = (float)(1.4426950408889634 / sqrt((double)d));
   const int es = dtype == MT_BF16 ? 2 : 4;
   const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so}, {q, k, v, o});
+  if (f32o && !vec_ok(d, 4, {a.so}, {o}))
+    return set_error("mt_flash_attn_fwd: an fp32 O needs 16-B aligned rows (d and O strides multiples of 4)");
   hipStream_t st = (hipStream_t)stream;
   const int pol = g_kernel_policy.load(std::memory_order_relaxed);
   // key padding (kv_len): the generic / ring kernels, which mask keys >= kv_len[b] (the
@@ -518,6 +526,9 @@ int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k
   a.dq = dq; a.dk = dk; a.dv = dv;
   a.m = (float*)m; a.l = (float*)l;
   a.kv_len = kv_len;
+#ifdef MT_DIAGNOSTICS
+  if (const char* kn = getenv("MT_KNOB")) a.knob = atoi(kn);
+#endif
   a.lse2 = (float*)workspace;
   a.delta = a.lse2 + B * H * N;
   a.slab = fused_bwd_applies(N, d) ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;

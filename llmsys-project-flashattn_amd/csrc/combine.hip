@@ -268,6 +268,7 @@ struct AdamArgs {
 };
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a) {
+#pragma clang fp contract(off)  // separately rounded products and sums, like the tensor ops
   m = __fadd_rn(__fmul_rn(m, a.b1), __fmul_rn(g, a.c1));
   v = __fadd_rn(__fmul_rn(v, a.b2), __fmul_rn(__fmul_rn(g, g), a.c2));
   p = __fsub_rn(p, __fdiv_rn(__fmul_rn(a.step, m), __fadd_rn(__fsqrt_rn(v), a.eps)));
@@ -442,14 +443,15 @@ int mt_rand_uniform(float* out, int64_t n, uint64_t seed, void* stream) {
 }
 
 int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
-                 float* const* exp_avg_sq, const int64_t* numels, float beta1, float beta2, float eps,
-                 float step_size, void* stream) {
+                 float* const* exp_avg_sq, const int64_t* numels, double beta1, double beta2, double eps,
+                 double step_size, void* stream) {
   if (n_tensors < 0) return set_error("mt_adam_step: n_tensors = %d", n_tensors);
   for (int t0 = 0; t0 < n_tensors; t0 += kAdamMax) {
     AdamArgs a;
     memset(&a, 0, sizeof(a));
-    a.b1 = beta1; a.b2 = beta2; a.c1 = 1.f - beta1; a.c2 = 1.f - beta2;
-    a.step = step_size; a.eps = eps;
+    // each constant rounded to fp32 once, as the tensor-op form's scalar operands are
+    a.b1 = (float)beta1; a.b2 = (float)beta2; a.c1 = (float)(1.0 - beta1); a.c2 = (float)(1.0 - beta2);
+    a.step = (float)step_size; a.eps = (float)eps;
     int64_t blocks = 0;
     for (int t = t0; t < std::min(n_tensors, t0 + kAdamMax); ++t) {
       if (numels[t] < 0) return set_error("mt_adam_step: numel %lld", (long long)numels[t]);

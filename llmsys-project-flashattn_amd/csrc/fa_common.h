@@ -194,6 +194,8 @@ struct AttnArgs {
   float* lse2; float* delta;       // bwd workspace, [B*H*N]
   void* slab;                      // bwd workspace: dQ partials of the fused bf16 backward
   const int* kv_len;               // [B] valid keys per batch row (keys >= kv_len masked), or null
+  int o_f32;                       // bf16 forward: O is fp32 (MT_BF16_F32OUT), else O has the input type
+  int knob;                        // A/B schedule knob (diagnostics build: env MT_KNOB; product: 0)
   int64_t sq[3], sk[3], sv[3], so[3], sdo[3], sdq[3], sdk[3], sdv[3];  // (b, h, n)
   int B, H, N, d;
   float scale;       // 1/sqrt(d)
@@ -204,6 +206,21 @@ struct AttnArgs {
 // key-padding length vector is given (mt_flash_attn_*_varlen).
 __device__ __forceinline__ int kv_keys(const AttnArgs& p, int b) {
   return p.kv_len ? max(0, min(p.N, p.kv_len[b])) : p.N;
+}
+
+// Row q of O in the bf16 forward kernels: bf16, or fp32 when the caller asked for an fp32
+// output (o_f32; the caller guarantees 16-B aligned rows and columns in multiples of 4).
+struct ORow {
+  void* p;
+  int f32;
+};
+__device__ __forceinline__ ORow o_row(const AttnArgs& a, int b, int hh, int64_t q) {
+  const int64_t e = b * a.so[0] + hh * a.so[1] + q * a.so[2];
+  return ORow{a.o_f32 ? (void*)((float*)a.out + e) : (void*)((bf16*)a.out + e), a.o_f32};
+}
+__device__ __forceinline__ void store4(const ORow& o, int col, float x, float y, float z, float w) {
+  if (o.f32) store4((float*)o.p + col, x, y, z, w, true);
+  else store4((bf16*)o.p + col, x, y, z, w, true);
 }
 
 }  // namespace mt

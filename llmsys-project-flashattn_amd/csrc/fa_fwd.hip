@@ -17,6 +17,8 @@
 //  * Head dims above the tile DT are handled by a d-chunked QKᵀ and a grid.z split
 //    of the O columns (each z-slice recomputes S; exact, only slower).
 //  * int64 addressing throughout (the reference overflows at 2^31 elements).
+#include <type_traits>
+
 #include "fa_common.h"
 
 namespace mt {
@@ -170,7 +172,10 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
   const float l_tot = l_run + __shfl_xor(l_run, 32);
   const float inv_l = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (my_q < N) {
-    T* Og = (T*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+    const int64_t oe = b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+    T* Og = (T*)p.out + oe;
+    float* Of = (float*)p.out + oe;  // bf16 inputs with an fp32 output (o_f32)
+    const bool f32o = !std::is_same<T, float>::value && p.o_f32;
 #pragma unroll
     for (int db = 0; db < DT / 32; ++db)
 #pragma unroll
@@ -178,7 +183,11 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
         const int col = oc + db * 32 + 8 * g + 4 * hf;
         const float a[4] = {O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
                             O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l};
-        if (VEC && col + 3 < d) {
+        if (f32o) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < d) Of[col + e] = a[e];
+        } else if (VEC && col + 3 < d) {
           store4(Og + col, a[0], a[1], a[2], a[3], true);
         } else {
 #pragma unroll
@@ -367,13 +376,19 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
   const float l_tot = l_run + __shfl_xor(l_run, 32);
   const float inv_l = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (my_q < N) {
-    T* Og = (T*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+    const int64_t oe = b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+    T* Og = (T*)p.out + oe;
+    float* Of = (float*)p.out + oe;  // bf16 inputs with an fp32 output (o_f32)
+    const bool f32o = !std::is_same<T, float>::value && p.o_f32;
 #pragma unroll
     for (int db = 0; db < DT / 32; ++db)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int col = db * 32 + 8 * g + 4 * hf;
-        if (col < d)  // d is a multiple of 4 here
+        if (col < d && f32o)  // d is a multiple of 4 here
+          store4(Of + col, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l, O[db][4 * g + 2] * inv_l,
+                 O[db][4 * g + 3] * inv_l, true);
+        else if (col < d)
           store4(Og + col, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l, O[db][4 * g + 2] * inv_l,
                  O[db][4 * g + 3] * inv_l, true);
       }

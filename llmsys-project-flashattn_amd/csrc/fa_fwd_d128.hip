@@ -428,7 +428,9 @@ static hipError_t launch_d128_t(const AttnArgs& a, hipStream_t st) {
 hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
                            bool* handled, int pair) {
   *handled = false;
-  if (a.d != D) return hipSuccess;
+  // an fp32 O (MT_BF16_F32OUT) takes the generic kernels: the epilogue's extra store path
+  // moved this kernel's register allocation into spills inside its main loop
+  if (a.d != D || a.o_f32) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;

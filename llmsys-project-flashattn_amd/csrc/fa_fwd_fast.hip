@@ -278,13 +278,13 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_fast(AttnArgs p, int n
   const float l_tot = L[0];
   const float inv_l = 1.f / l_tot;
   if (my_q < N) {
-    bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+    const ORow Og = o_row(p, b, hh, my_q);
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        store4(Og + db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
-               O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l, true);
+        store4(Og, db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
+               O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l);
     if (hf == 0) {
       const int64_t row = (int64_t)bh * N + my_q;
       if (p.m) p.m[row] = m_run * p.scale;  // natural-log units: max of s = qk/√d
@@ -491,13 +491,13 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_fwd_bf16_sp2(AttnArgs p, int nq
   const float l_tot = L[0];
   const float inv_l = 1.f / l_tot;
   if (my_q < N) {
-    bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+    const ORow Og = o_row(p, b, hh, my_q);
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        store4(Og + db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
-               O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l, true);
+        store4(Og, db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
+               O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l);
     if (hf == 0) {
       const int64_t row = (int64_t)bh * N + my_q;
       if (p.m) p.m[row] = m_run * p.scale;
@@ -730,13 +730,13 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_bf16_pp(AttnArgs p, int nq
   const float l_tot = L[0];
   const float inv_l = 1.f / l_tot;
   if (my_q < N) {
-    bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)my_q * p.so[2];
+    const ORow Og = o_row(p, b, hh, my_q);
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        store4(Og + db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
-               O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l, true);
+        store4(Og, db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv_l, O[db][4 * g + 1] * inv_l,
+               O[db][4 * g + 2] * inv_l, O[db][4 * g + 3] * inv_l);
     if (hf == 0) {
       const int64_t row = (int64_t)bh * N + my_q;
       if (p.m) p.m[row] = m_run * p.scale;

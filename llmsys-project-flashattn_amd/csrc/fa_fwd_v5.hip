@@ -673,6 +673,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
     // contiguous bytes of group g and lanes 32-63 those of group g+1: 4 dwordx4 stores
     // per block instead of 8 dwordx2 (every lane takes part in the swap; stores are guarded).
     bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)min(q, N - 1) * p.so[2];
+    if (p.o_f32) {  // fp32 output: plain 16-B stores of the lane's four columns
+      const ORow Of = o_row(p, b, hh, q);
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          if (q < N)
+            store4(Of, db * 32 + 8 * g + 4 * hf, O[db][4 * g] * inv, O[db][4 * g + 1] * inv,
+                   O[db][4 * g + 2] * inv, O[db][4 * g + 3] * inv);
+    } else {
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
       uint2 u[4];
@@ -690,6 +700,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_v5(AttnArgs p, in
         if (q < N)
           *(uint4*)(Og + db * 32 + 8 * k + 8 * hf) = uint4{rx[0], ry[0], rx[1], ry[1]};
       }
+    }
     }
     if (q < N) {
       if (hf == 0) {

@@ -555,11 +555,11 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       const float inv = 1.f / l;
       const f32x4(&O)[4][2] = blk ? OB : OA;
       if (q < N) {
-        bf16* Og = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)q * p.so[2];
+        const ORow Og = o_row(p, b, hh, q);
 #pragma unroll
         for (int db = 0; db < 4; ++db)
-          store4(Og + 16 * db + 4 * g, O[db][qh][0] * inv, O[db][qh][1] * inv, O[db][qh][2] * inv,
-                 O[db][qh][3] * inv, true);
+          store4(Og, 16 * db + 4 * g, O[db][qh][0] * inv, O[db][qh][1] * inv, O[db][qh][2] * inv,
+                 O[db][qh][3] * inv);
         if (g == 0) {
           const int64_t row = (int64_t)bh * N + q;
           if (p.m) p.m[row] = m * (PS ? p.scale / c2 : p.scale);

@@ -60,8 +60,8 @@ _PROTOS = {
                                 ctypes.c_float, _vp]),
     "mt_matmul_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _i64p, _i64p, _vp]),
     "mt_rand_uniform": (_int, [_vp, _i64, ctypes.c_uint64, _vp]),
-    "mt_adam_step": (_int, [_int, _vpp, _vpp, _vpp, _vpp, _i64p, ctypes.c_float, ctypes.c_float,
-                            ctypes.c_float, ctypes.c_float, _vp]),
+    "mt_adam_step": (_int, [_int, _vpp, _vpp, _vpp, _vpp, _i64p, ctypes.c_double, ctypes.c_double,
+                            ctypes.c_double, ctypes.c_double, _vp]),
     "mt_set_gemm_backend": (None, [_int]),
     "launch_attn_softmax": (None, [_fp, _fp, _int, _int, _int, _int, ctypes.c_bool, _vp]),
     "launch_attn_softmax_bw": (None, [_fp, _fp, _int, _int, _vp]),
@@ -197,11 +197,12 @@ def _kv_arg(kv_len, B, device):
 
 
 def flash_fwd(q, k, v, causal: bool = False, out=None, m=None, l=None, stream: Optional[int] = None,
-              kv_len=None):
+              kv_len=None, out_dtype=None):
     """Device-pointer forward on torch tensors [B,H,N,d] (fp32 or bf16, any strides
     with unit-stride d). Returns (O, m, l); O has q's dtype, m/l are fp32 [B,H,N].
     kv_len: optional [B] valid-key counts (key padding: keys >= kv_len[b] are masked,
-    mt_flash_attn_fwd_varlen)."""
+    mt_flash_attn_fwd_varlen). out_dtype=torch.float32 with bf16 inputs (or an fp32 `out`):
+    the bf16 kernels write O in fp32, without its final bf16 rounding (MT_BF16_F32OUT)."""
     torch = _torch()
     _check_dev(q, k, v)
     B, H, N, d = q.shape
@@ -209,8 +210,14 @@ def flash_fwd(q, k, v, causal: bool = False, out=None, m=None, l=None, stream: O
         raise ValueError(f"q/k/v shapes differ: {tuple(q.shape)} {tuple(k.shape)} {tuple(v.shape)}")
     if not (q.dtype == k.dtype == v.dtype):
         raise TypeError("q/k/v dtypes differ")
+    code = dtype_code(q)
+    f32o = q.dtype == torch.bfloat16 and (out_dtype == torch.float32 or
+                                          (out is not None and out.dtype == torch.float32))
     if out is None:
-        out = torch.empty_like(q, memory_format=torch.contiguous_format)
+        out = torch.empty_like(q, dtype=torch.float32 if f32o else q.dtype,
+                               memory_format=torch.contiguous_format)
+    if f32o:
+        code = 2  # MT_BF16_F32OUT
     if m is None:
         m = torch.empty((B, H, N), dtype=torch.float32, device=q.device)
     if l is None:
@@ -218,12 +225,12 @@ def flash_fwd(q, k, v, causal: bool = False, out=None, m=None, l=None, stream: O
     st = stream_ptr(q.device) if stream is None else stream
     kv = _kv_arg(kv_len, B, q.device)
     if kv is None:
-        check(lib().mt_flash_attn_fwd(dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(),
+        check(lib().mt_flash_attn_fwd(code, int(causal), q.data_ptr(), k.data_ptr(),
                                       v.data_ptr(), out.data_ptr(), m.data_ptr(), l.data_ptr(),
                                       B, H, N, d, strides3(q), strides3(k), strides3(v),
                                       strides3(out), st), "mt_flash_attn_fwd")
     else:
-        check(lib().mt_flash_attn_fwd_varlen(dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(),
+        check(lib().mt_flash_attn_fwd_varlen(code, int(causal), q.data_ptr(), k.data_ptr(),
                                              v.data_ptr(), out.data_ptr(), m.data_ptr(), l.data_ptr(),
                                              B, H, N, d, strides3(q), strides3(k), strides3(v),
                                              strides3(out), kv.data_ptr(), st),

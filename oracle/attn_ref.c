@@ -122,6 +122,9 @@ void oracle_attn_bwd_kv(const float* q, const float* k, const float* v, const fl
     double* p = (double*)malloc(sizeof(double) * (size_t)(N * N));
     double* ds = (double*)malloc(sizeof(double) * (size_t)(N * N));
     float* s = (float*)malloc(sizeof(float) * (size_t)N);
+    double* acc = (double*)malloc(sizeof(double) * (size_t)d);
+    double* accK = (double*)malloc(sizeof(double) * (size_t)(N * d));
+    double* accV = (double*)malloc(sizeof(double) * (size_t)(N * d));
 #pragma omp for schedule(dynamic, 1)
     for (int64_t bh = 0; bh < BH; ++bh) {
       const int64_t base = bh * N * d;
@@ -140,26 +143,37 @@ void oracle_attn_bwd_kv(const float* q, const float* k, const float* v, const fl
         }
         for (int64_t j = 0; j < N; ++j) ds[i * N + j] = p[i * N + j] * (ds[i * N + j] - delta);
       }
+      // The three sums run in row-major sweeps (j, then i ascending for every element, the
+      // same order as the element-at-a-time loops of attention.py) so the N x N buffers are
+      // read once each instead of once per output column.
+      for (int64_t i = 0; i < N; ++i) {
+        for (int64_t t = 0; t < d; ++t) acc[t] = 0.0;
+        for (int64_t j = 0; j < N; ++j) {
+          const double w = ds[i * N + j];
+          for (int64_t t = 0; t < d; ++t) acc[t] += w * (double)K[j * d + t];
+        }
+        for (int64_t t = 0; t < d; ++t) dq[base + i * d + t] = (float)(acc[t] * scale);
+      }
+      for (int64_t x = 0; x < N * d; ++x) accK[x] = accV[x] = 0.0;
       for (int64_t i = 0; i < N; ++i)
-        for (int64_t t = 0; t < d; ++t) {
-          double a = 0.0;
-          for (int64_t j = 0; j < N; ++j) a += ds[i * N + j] * (double)K[j * d + t];
-          dq[base + i * d + t] = (float)(a * scale);
-        }
-      for (int64_t j = 0; j < N; ++j)
-        for (int64_t t = 0; t < d; ++t) {
-          double a = 0.0, b = 0.0;
-          for (int64_t i = 0; i < N; ++i) {
-            a += ds[i * N + j] * (double)Q[i * d + t];
-            b += p[i * N + j] * (double)dO[i * d + t];
+        for (int64_t j = 0; j < N; ++j) {
+          const double a = ds[i * N + j], b = p[i * N + j];
+          for (int64_t t = 0; t < d; ++t) {
+            accK[j * d + t] += a * (double)Q[i * d + t];
+            accV[j * d + t] += b * (double)dO[i * d + t];
           }
-          dk[base + j * d + t] = (float)(a * scale);
-          dv[base + j * d + t] = (float)b;
         }
+      for (int64_t x = 0; x < N * d; ++x) {
+        dk[base + x] = (float)(accK[x] * scale);
+        dv[base + x] = (float)accV[x];
+      }
     }
     free(p);
     free(ds);
     free(s);
+    free(acc);
+    free(accK);
+    free(accV);
   }
 }
 

@@ -1,10 +1,21 @@
 """Interleaved in-process A/B timing of forward-kernel policies (diagnostics, GPU box).
-usage: python scripts/ab_fwd.py POL[,POL...] [causal] [B,H,N,d] [rounds]   (DTYPE=fp32 for fp32 I/O)"""
+usage: python scripts/ab_fwd.py POL[,POL...] [causal] [B,H,N,d] [rounds]   (DTYPE=fp32 for fp32 I/O)
+MT_DIAG=1: the diagnostics library; ENVAB=NAME:v1,v2,..: the arms are values of an environment
+knob (e.g. MT_KNOB, read per launch by the diagnostics build) under policy POL"""
 import os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "llmsys-project-flashattn_amd"))
 import torch
 from minitorch import _hip
+_DIAG = os.path.join(os.path.dirname(_hip.LIB_PATH), "diag", "libminitorch_hip_diag.so")
+if os.environ.get("MT_DIAG") == "1":
+    assert os.path.exists(_DIAG), "make -C llmsys-project-flashattn_amd DIAG=1"
+    _hip.use_library(_DIAG)
 pols = [int(x) for x in sys.argv[1].split(",")]
+env_name, env_vals = None, None
+if os.environ.get("ENVAB"):
+    env_name, _v = os.environ["ENVAB"].split(":")
+    env_vals = _v.split(",")
+arms = env_vals if env_vals else pols
 causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
 B, H, N, d = (int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "8,16,4096,64").split(","))
 rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 7
@@ -16,11 +27,15 @@ flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
 t0 = time.time()
 while time.time() - t0 < 0.5:  # clock ramp
     _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l); torch.cuda.synchronize()
-res = {p: [] for p in pols}
+res = {p: [] for p in arms}
 reps = max(3, int(2e12 / flops))
 for rnd in range(rounds):
-    for p in pols:
-        _hip.set_policy(p)
+    for p in arms:
+        if env_vals:
+            os.environ[env_name] = p
+            _hip.set_policy(pols[0])
+        else:
+            _hip.set_policy(p)
         for _ in range(2): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize(); e0.record()
@@ -29,6 +44,6 @@ for rnd in range(rounds):
         res[p].append(e0.elapsed_time(e1) / reps)
 _hip.set_policy(0)
 print(f"shape {(B, H, N, d)} {dt} causal={causal} reps={reps} rounds={rounds}")
-for p in pols:
+for p in arms:
     t = sorted(res[p]); med = t[len(t) // 2]
-    print(f"policy {p:3d}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s", flush=True)
+    print(f"{(env_name + '=' + p) if env_vals else 'policy %3d' % p}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s", flush=True)
