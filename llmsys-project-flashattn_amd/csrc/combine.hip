@@ -268,10 +268,12 @@ struct AdamArgs {
 };
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a) {
-#pragma clang fp contract(off)  // separately rounded products and sums, like the tensor ops
-  m = __fadd_rn(__fmul_rn(m, a.b1), __fmul_rn(g, a.c1));
-  v = __fadd_rn(__fmul_rn(v, a.b2), __fmul_rn(__fmul_rn(g, g), a.c2));
-  p = __fsub_rn(p, __fdiv_rn(__fmul_rn(a.step, m), __fadd_rn(__fsqrt_rn(v), a.eps)));
+  // separately rounded products and sums, like the tensor ops (plain operators under the
+  // pragma: the __f*_rn helpers are inlined from a header compiled with contraction on)
+#pragma clang fp contract(off)
+  m = m * a.b1 + g * a.c1;
+  v = v * a.b2 + (g * g) * a.c2;
+  p = p - (a.step * m) / (__fsqrt_rn(v) + a.eps);
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {

@@ -6,15 +6,20 @@ elementwise, with |·| taken before the products:
 
     |O  - O_ref|  <= atol + r · (P |V|)                    (causal rows average few keys)
     |dV - dV_ref| <= atol + r · (Pᵀ |dO|)
-    |dK - dK_ref| <= atol + r · (1/√d) · (|dS|ᵀ |Q|)
-    |dQ - dQ_ref| <= atol + r · (1/√d) · (|dS| |K|)
+    |dK - dK_ref| <= atol + (1/√d) · (r · |dS|ᵀ + (1 + r) · Eᵀ) |Q|
+    |dQ - dQ_ref| <= atol + (1/√d) · (r · |dS| + (1 + r) · E) |K|
 
-where |dS| = P ∘ (|dP − δ| + Δδ) and Δδ = 2^-8 · rowsum(|dO| ∘ |O|) covers δ = rowsum(dO ∘ O)
-being formed from the bf16-rounded O. r = 2^-7 is twice the two roundings (operand +
-output) each product sees. dQ gets r_dq = 1.5 · 2^-7, twice three roundings: the fused
-backward (csrc/fa_bwd_fused.hip) also rounds each 256-key block's partial sum of dS·K to
-bf16 before the ordered sum (|partial| <= Σ over the block of |dS||K|). The products are
-formed in fp64 from the same bf16-rounded inputs the kernels read.
+where |dS| = P ∘ |dP − δ| and E = P ∘ Δδ is the error dS inherits from δ = rowsum(dO ∘ O)
+formed from the forward's O: that O is off by at most the forward bound r · (P|V|)
+elementwise (its P and output roundings), so Δδ = r · rowsum(|dO| ∘ (P|V|)). Δδ is an
+absolute error of dP − δ and enters unscaled; scaling it by r again (the round-2 form)
+under-counted it on causal rows with a few keys, where |O| ~ 2.5 and the rounded O moves
+δ by ~1e-2 (C3 causal head (1,11), row 3: dQ off by 7.4e-3 against a 3.0e-3 bound,
+scripts/probe_dq_bound.py). r = 2^-7 is twice the two roundings (operand + output) each
+product sees. dQ gets r_dq = 1.5 · 2^-7, twice three roundings: the fused backward
+(csrc/fa_bwd_fused.hip) also rounds each 256-key block's partial sum of dS·K to bf16
+before the ordered sum (|partial| <= Σ over the block of |dS||K|). The products are formed
+in fp64 from the same bf16-rounded inputs the kernels read.
 """
 import numpy as np
 
@@ -22,9 +27,9 @@ R_BF16 = 2.0 ** -7
 R_BF16_DQ = 1.5 * 2.0 ** -7
 
 
-def head_terms(q, k, v, do, causal, kv=None):
-    """fp64 P, |dS| pieces for one head (N, d); kv: valid keys of the head's batch row
-    (key padding; a row with none gets P = 0)."""
+def head_terms(q, k, v, do, causal, kv=None, r=R_BF16):
+    """fp64 P, |dS| = P|dP − δ| and E = P·Δδ for one head (N, d); kv: valid keys of the
+    head's batch row (key padding; a row with none gets P = 0)."""
     q, k, v, do = (np.asarray(a, np.float64) for a in (q, k, v, do))
     N, d = q.shape
     sc = 1.0 / np.sqrt(d)
@@ -41,15 +46,14 @@ def head_terms(q, k, v, do, causal, kv=None):
     O = P @ v
     dP = do @ v.T
     delta = (do * O).sum(axis=1, keepdims=True)
-    ddelta = 2.0 ** -8 * (np.abs(do) * np.abs(O)).sum(axis=1, keepdims=True)
-    absdS = P * (np.abs(dP - delta) + ddelta)
-    return P, absdS, sc
+    ddelta = r * (np.abs(do) * (P @ np.abs(v))).sum(axis=1, keepdims=True)
+    return P, P * np.abs(dP - delta), P * ddelta, sc
 
 
 def grad_bounds(q, k, v, do, causal, atol=1e-3, r=R_BF16, kv=None, r_dq=None):
-    P, absdS, sc = head_terms(q, k, v, do, causal, kv)
+    P, absdS, E, sc = head_terms(q, k, v, do, causal, kv, r)
     q, k, do = (np.abs(np.asarray(a, np.float64)) for a in (q, k, do))
     r_dq = r * R_BF16_DQ / R_BF16 if r_dq is None else r_dq
-    return (atol + r_dq * sc * (absdS @ k),   # dQ
-            atol + r * sc * (absdS.T @ q),    # dK
-            atol + r * (P.T @ do))            # dV
+    return (atol + sc * ((r_dq * absdS + (1 + r_dq) * E) @ k),   # dQ
+            atol + sc * ((r * absdS + (1 + r) * E).T @ q),         # dK
+            atol + r * (P.T @ do))                                 # dV
