@@ -284,14 +284,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
   const float c2 = p.scale_log2;
   const int kend = CAUSAL ? min(N, q0 + C::kBQ) : N;
   const int ntiles = (kend + kBK - 1) / kBK;
-  // knob 4 (A/B): workgroups of odd 32-slot rounds on their XCD walk the key tiles last to
-  // first, so they start on the tiles the previous round left in the XCD's L2 (non-causal,
-  // N % 64 == 0: no masked tile). Tile t's byte offset is t0 + t * tstep; a staging past the
-  // end then has a negative offset, which the buffer range check turns into zeros as it
-  // does past-the-end offsets in the forward order.
-  const bool rev = !CAUSAL && (p.knob & 4) && N % kBK == 0 && ((slot >> 5) & 1);
-  const int ktile_b = rev ? -kBK * skn * 2 : kBK * skn * 2, vtile_b = rev ? -kBK * svn * 2 : kBK * svn * 2;
-  const int kt0 = rev ? (ntiles - 1) * kBK * skn * 2 : 0, vt0 = rev ? (ntiles - 1) * kBK * svn * 2 : 0;
+  const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
   const int nfull = CAUSAL ? min(N / kBK, q0 / kBK) : N / kBK;  // mask-free tiles
 
   // staging: issue (global -> registers, or LDS-DMA straight into the slot) and write
@@ -324,11 +317,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
     for (int i = 0; i < 4; ++i) O[i] = f32x16{};
     l_part = 0.f;
     m_run = -INFINITY;
-    D6_ISSUE_K(sK0, kt0)
-    D6_ISSUE_V(sV0, vt0)
+    D6_ISSUE_K(sK0, 0)
+    D6_ISSUE_V(sV0, 0)
     D6_WRITE_K(sK0)
     D6_WRITE_V(sV0)
-    D6_ISSUE_K(sK1, kt0 + ktile_b)
+    D6_ISSUE_K(sK1, ktile_b)
     D6_WRITE_K(sK1)
     __syncthreads();
     qk6(sK0, c, qf, SA);
@@ -341,8 +334,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
     const int t_ = (T_);                                                                     \
     const int par = t_ & 1;                                                                  \
     const bool next = t_ + 1 < ntiles;                                                       \
-    if (t_ + 2 < ntiles) D6_ISSUE_K(par ? sK1 : sK0, kt0 + (t_ + 2) * ktile_b)               \
-    if (next) D6_ISSUE_V(par ? sV0 : sV1, vt0 + (t_ + 1) * vtile_b)                          \
+    if (t_ + 2 < ntiles) D6_ISSUE_K(par ? sK1 : sK0, (t_ + 2) * ktile_b)                     \
+    if (next) D6_ISSUE_V(par ? sV0 : sV1, (t_ + 1) * vtile_b)                                \
     if (!CAUSAL || t_ * kBK <= wq_hi) {                                                      \
       if (t_ >= nfull) mask6<CAUSAL>(SA, t_ * kBK, N, my_q, hf);                             \
       const float nmc = max6(SA, O, l_part, m_run, c2);                                      \
@@ -368,8 +361,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128(AttnArgs p, 
       // into a slot nobody reads).
 #define D6_BULK(SC_, SN_, SKN_, SVC_, SKW_, SVW_, T_)                                        \
   {                                                                                         \
-    D6_ISSUE_K(SKW_, kt0 + ((T_) + 2) * ktile_b)                                            \
-    D6_ISSUE_V(SVW_, vt0 + ((T_) + 1) * vtile_b)                                            \
+    D6_ISSUE_K(SKW_, ((T_) + 2) * ktile_b)                                                  \
+    D6_ISSUE_V(SVW_, ((T_) + 1) * vtile_b)                                                  \
     bulk6(SKN_, SVC_, c, qf, SC_, SN_, O, l_part, c2, nmc);                                 \
     D6_WRITE_K(SKW_)                                                                        \
     D6_WRITE_V(SVW_)                                                                        \
