@@ -491,7 +491,11 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
 
 // The fused bf16 d = 64 backward keeps its dQ partial sums (bf16, N/256 per element) in the
 // workspace; their size grows as N^2, so it runs only up to N = 8192 (C3: 1 GiB).
-static bool fused_bwd_applies(int64_t N, int64_t d) { return d == 64 && N <= 8192; }
+// (the fused kernel stages the row constants lse2 | δ by LDS-DMA from one 32-bit-offset
+// buffer over both arrays: 2·B·H·N floats below 2^31 bytes)
+static bool fused_bwd_applies(int64_t B, int64_t H, int64_t N, int64_t d) {
+  return d == 64 && N <= 8192 && 2 * B * H * N * (int64_t)sizeof(float) < ((int64_t)1 << 31);
+}
 // the fused backward is the bf16 d = 64 default where it applies: C3 1.643 vs 1.872 ms
 // non-causal, 0.991 vs 1.084 ms causal against the split defaults (interleaved A/B on one box,
 // profiles/r3_ab_bwd_fused.txt); the split forms stay selectable (policy 121)
@@ -501,7 +505,7 @@ static int64_t bwd_rows_bytes(int64_t B, int64_t H, int64_t N) {
 }
 
 int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t d) {
-  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(N, d) ? bwd_fused_slab_bytes(B, H, N) : 0);
+  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(B, H, N, d) ? bwd_fused_slab_bytes(B, H, N) : 0);
 }
 
 int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const void* v,
@@ -531,7 +535,7 @@ int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k
 #endif
   a.lse2 = (float*)workspace;
   a.delta = a.lse2 + B * H * N;
-  a.slab = fused_bwd_applies(N, d) ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
+  a.slab = fused_bwd_applies(B, H, N, d) ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
   int64_t* dst[8] = {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv};
   for (int i = 0; i < 8; ++i) fill_strides(dst[i], strides ? strides + 3 * i : nullptr, H, N, d);
   a.B = (int)B; a.H = (int)H; a.N = (int)N; a.d = (int)d;

@@ -66,6 +66,17 @@ __device__ __forceinline__ void dma_rows(uint32_t lds, __amdgpu_buffer_rsrc_t rs
       : "memory");
 }
 
+// The same for 64 x 4 B: lane l's dword lands at lds + 4 l (row constants).
+__device__ __forceinline__ void dma_dwords(uint32_t lds, __amdgpu_buffer_rsrc_t rs, int go) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dword %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(go), "s"(lds), "s"(rs)
+      : "memory");
+}
+
 // The workgroup's dynamic-LDS base as a wave-uniform 32-bit byte address.
 __device__ __forceinline__ uint32_t lds_base(const void* smem) {
   return __builtin_amdgcn_readfirstlane(

@@ -38,6 +38,7 @@
 // f(r) ^ 4, so the transposed read of rows +8 takes its own offset (tlo / thi).
 #include "fa_bwd_bf16.h"
 
+
 namespace mt {
 
 using namespace bwdbf16;
@@ -289,28 +290,35 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     gq = (r * sqn + cs * 8) * 2;
     go = (r * son + cs * 8) * 2;
   }
-  const float* nlse = p.lse2 + (int64_t)bh * N;
-  const float* ndel = p.delta + (int64_t)bh * N;
+  // Row constants of sub-tile wu (its 32 queries' −lse2/c2, then their −δ) by one LDS-DMA
+  // instruction of wave 4·wu: lanes 0-31 read lse2, lanes 32-63 δ, both from one buffer over
+  // the workspace (δ follows lse2, fused_bwd_applies keeps it under 2^31 bytes); a query past
+  // N gets an out-of-range offset, which reads 0.
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.lse2, (short)0, (int)(2 * (int64_t)p.B * p.H * N * 4), 0x00020000);
+  const int crow = (lane >= kQT ? p.B * p.H * N : 0) + bh * N;  // + query
 
   const int qt0 = CAUSAL ? k0 : 0;
   const int step0 = qt0 / kStep;
   // a block of padding keys only (k0 >= Nk) stores zero dK / dV and no dQ partials
   const int nstep = N > qt0 && k0 < Nk ? (N - qt0 + kStep - 1) / kStep : 0;
-  float sv = 0.f;
   auto stage = [&](int t, int slot) __attribute__((always_inline)) {
     const int qs = qt0 + t * kStep + wu * kQT;
     const uint32_t img = lds0 + slot * 2 * kSub;
     dma_rows(img, rq, gq + qs * sqn * 2);
     dma_rows(img + kImg * 2, ro, go + qs * son * 2);
-    if (tid < 4 * kQT) {
-      const int q = qt0 + t * kStep + (tid >> 6) * kQT + (tid & (kQT - 1));
-      sv = q < N ? ((tid & kQT) == 0 ? nlse[q] : ndel[q]) : 0.f;
+    if (wq == 0) {
+      const int q = qs + (lane & (kQT - 1));
+      dma_dwords(img + 2 * kImg * 2, rc, q < N ? (crow + q) * 4 : 0x7ffffff0);  // wq = 0
     }
   };
-  auto publish = [&](int slot) __attribute__((always_inline)) {
-    if (tid < 4 * kQT)
-      ((float*)((bf16*)(smem + (2 * slot + (tid >> 6)) * kSub) + 2 * kImg))[tid & 63] = sv;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // after_store: the step issued its dQ partial store after the staging loads. vmcnt retires
+  // in issue order, so vmcnt(1) waits for the staging and leaves that store in flight; a
+  // vmcnt(0) here had every step wait for the store's write acknowledgement before the
+  // barrier (it was issued a few instructions earlier).
+  auto publish = [&](bool after_store) __attribute__((always_inline)) {
+    if (after_store) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
   auto dq_store = [&](const f32x4 (&acc)[2], int tl) __attribute__((always_inline)) {
     bf16x8 o;
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
 
   if (nstep > 0) {
     stage(0, 0);
-    publish(0);
+    publish(false);
   }
   __syncthreads();
   // steps: [0, nhead) causal diagonal (masked), [nhead, nfull) mask-free, [nfull, nstep) tail.
@@ -351,12 +359,12 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     if (more_) stage(t_ + 1, (SLOT_) ^ 1);                                               \
     f32x4 qa_[2] = {f32x4{}, f32x4{}};                                                   \
     const bf16* si_ = dsimg + ((SLOT_) ^ 1) * (kKB * kStep);                             \
-    if (DQ_) dq_ksteps<0, 4, kPF && !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);                              \
+    if (DQ_) dq_ksteps<0, 4, kPF && !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);             \
     FSUB(MASK_, SLOT_, t_, 0)                                                            \
-    if (DQ_) dq_ksteps<4, 8, kPF && !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);                              \
+    if (DQ_) dq_ksteps<4, 8, kPF && !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);             \
     FSUB(MASK_, SLOT_, t_, 1)                                                            \
     if (DQ_) dq_store(qa_, t_ - 1);                                                      \
-    if (more_) publish((SLOT_) ^ 1);                                                     \
+    if (more_) publish(DQ_);                                                             \
     __syncthreads();                                                                     \
   }
   if (nstep > 0) {
