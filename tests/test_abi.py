@@ -48,6 +48,10 @@ def test_python_binding_covers_header():
     assert lib.mt_flash_attn_bwd_workspace_bytes(2, 3, 5, 7) == 256
     assert lib.mt_flash_attn_bwd_workspace_bytes(8, 16, 4096, 64) == 2 * 128 * 4096 * 4 + 128 * 64 * 16 * 8192
     assert lib.mt_flash_attn_bwd_workspace_bytes(1, 16, 16384, 64) == 2 * 16 * 16384 * 4
+    # the fused form needs its lse2 | delta rows under 2^31 bytes (one LDS-DMA buffer)
+    bh = 2 ** 31 // (2 * 8192 * 4)
+    assert lib.mt_flash_attn_bwd_workspace_bytes(1, bh - 1, 8192, 64) > 2 * (bh - 1) * 8192 * 4 + 255
+    assert lib.mt_flash_attn_bwd_workspace_bytes(1, bh, 8192, 64) == 2 * bh * 8192 * 4
 
 
 def test_errors_are_reported_not_fatal():

@@ -359,6 +359,25 @@ def test_config3_bf16_grads(torch_dev, causal, parity_record):
                       max_err_over_bound=r, bound="tests/bounds.py elementwise, r = 2^-7 (dQ 1.5 * 2^-7)")
 
 
+@pytest.mark.parametrize("N,causal", [(8192, False), (8192, True), (8256, True)])
+def test_bf16_bwd_fused_limit_vs_oracle(torch_dev, N, causal, parity_record):
+    """The d = 64 backward at the fused form's limit (N = 8192, the largest slab) and just past
+    it (N = 8256: the split kernels, a ragged last block) against the C oracle under the
+    elementwise bounds of tests/bounds.py, on whole heads."""
+    from minitorch import _hip
+    torch = torch_dev
+    g = torch.Generator(device="cuda").manual_seed(N + causal)
+    q, k, v, do = (torch.randn((1, 2, N, 64), device="cuda", generator=g).to(torch.bfloat16)
+                   for _ in range(4))
+    o, m, l = _hip.flash_fwd(q, k, v, causal)
+    dq, dk, dv = _hip.flash_bwd(q, k, v, o, do, m, l, causal)
+    torch.cuda.synchronize()
+    res = _grad_check(q, k, v, do, (dq, dk, dv), causal, [(0, 0), (0, 1)], f"(1,2,{N},64)")
+    for name, (e, r) in res.items():
+        parity_record("test_bf16_bwd_fused_limit_vs_oracle", f"(1,2,{N},64) causal={causal} {name}",
+                      heads=2, max_abs=e, max_err_over_bound=r)
+
+
 @pytest.mark.parametrize("d", [64, 128])
 def test_long_causal_paired_default(torch_dev, d):
     """Causal default at long N (d = 64: 8-wave v4 from N = 8192; d = 128: 8-wave d128),
