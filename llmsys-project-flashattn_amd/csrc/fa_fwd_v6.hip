@@ -188,9 +188,19 @@ __device__ __forceinline__ float lane_max6(const Blk6& s, int qh) {
   return m;
 }
 
-__device__ __forceinline__ void dma6(bf16* dst_rows, __amdgpu_buffer_rsrc_t rs, int go, int step) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst_rows, 16,
-                                           go + step, 0, 0, 0);
+// LDS-DMA of 64 x 16 B to the LDS byte address lds (wave-uniform). Issued from inline asm:
+// with the builtin, hipcc's waitcnt pass cannot tell the destination slot from the slots the
+// phase reads and put an s_waitcnt vmcnt(0) in front of the first Vᵀ read of every tile,
+// waiting mid-tile for the K(t+2) / V(t+1) staging issued at its start. The slots are
+// published by the tile's closing vmcnt(0) + barrier, which the loop issues itself.
+__device__ __forceinline__ void dma6(uint32_t lds, __amdgpu_buffer_rsrc_t rs, int go, int step) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(go + step), "s"(lds), "s"(rs)
+      : "memory");
 }
 
 }  // namespace
@@ -269,13 +279,20 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     vdo[i] = (dr * svn + (dc ^ (((dr >> 1) & 3) << 1)) * 8) * 2;
   }
   const int ktile_b = kBK * skn * 2, vtile_b = kBK * svn * 2;
+  // the workgroup's LDS base as a wave-uniform byte address; slot pointers become constant
+  // offsets from it
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem_raw);
+  auto lds_of = [&](const bf16* sl, int i) __attribute__((always_inline)) {
+    return lds0 + (uint32_t)((sl - (const bf16*)smem_raw) + 8 * (LPT * wq + i) * D) * 2;
+  };
   auto dma_k = [&](bf16* sl, int step) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma6(sl + 8 * (LPT * wq + i) * D, rk, kdo[i], step);
+    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rk, kdo[i], step);
   };
   auto dma_v = [&](bf16* sl, int step) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma6(sl + 8 * (LPT * wq + i) * D, rv, vdo[i], step);
+    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rv, vdo[i], step);
   };
   const float c2 = p.scale_log2;
 
