@@ -53,6 +53,21 @@ def _np(t):
     return t.float().cpu().numpy()
 
 
+def _shipped(policies):
+    """The policies of `policies` the loaded library accepts (collection time, host call only):
+    the product library ships the defaults, the diagnostics build (MT_HIP_LIB) every A/B
+    schedule, so a product run collects no cases for schedules it does not contain."""
+    try:
+        from minitorch import _hip
+        lib = _hip.lib()
+    except Exception:  # noqa: BLE001 - no library: keep every case (they fail loudly)
+        return list(policies)
+    cur = lib.mt_flash_get_kernel_policy()
+    keep = [p for p in policies if lib.mt_flash_set_kernel_policy(int(p)) == 0]
+    lib.mt_flash_set_kernel_policy(cur)
+    return keep
+
+
 def _use_policy(_hip, policy):
     """Select a kernel policy, or skip: the product library takes only 0 / 1 / 120 / 121; the
     A/B schedules need the diagnostics build (MT_HIP_LIB=.../libminitorch_hip_diag.so)."""
@@ -394,7 +409,7 @@ def test_long_causal_paired_default(torch_dev, d):
     _subset_check_fwd(torch, q, k, v, o, True, [(0, 0), (0, 2)], 1e-3, 2.0 ** -7)
 
 
-@pytest.mark.parametrize("policy", [0, 67, 68, 106])
+@pytest.mark.parametrize("policy", _shipped([0, 67, 68, 106]))
 def test_v5_causal_pairs_vs_oracle(torch_dev, policy, parity_record):
     """The v5 causal form (paired light/heavy query blocks per workgroup, each wave's
     pipelined loop ending on its own masked diagonal tile, finished waves staging for the
@@ -428,7 +443,7 @@ def test_v5_causal_pairs_vs_oracle(torch_dev, policy, parity_record):
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
-@pytest.mark.parametrize("policy", [0, 76, 100, 102, 103, 105])
+@pytest.mark.parametrize("policy", _shipped([0, 76, 100, 102, 103, 105]))
 def test_v5_split_keys_vs_oracle(torch_dev, policy, parity_record):
     """v5 with the keys split between the two halves of an 8-wave workgroup (policy 76; the
     default for grids of fewer 8-wave workgroups than CUs): every head, every row against
@@ -522,7 +537,7 @@ FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 3
                  67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106)
 
 
-@pytest.mark.parametrize("policy", FAST_POLICIES)
+@pytest.mark.parametrize("policy", _shipped(FAST_POLICIES))
 def test_fast_policies_vs_oracle(torch_dev, policy):
     """Each bf16 forward variant against the oracle on the same bf16 inputs: ragged N,
     both mask modes, head dims 64 and 128 (variants without a d=128 form fall back)."""
@@ -546,7 +561,7 @@ def test_fast_policies_vs_oracle(torch_dev, policy):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("policy", FAST_POLICIES)
+@pytest.mark.parametrize("policy", _shipped(FAST_POLICIES))
 def test_huge_spike_fallback(torch_dev, policy, d):
     """A score far above the first tile's max (> 64 log2 units): v4's bulk loop leaves the
     safe range and its workgroup recomputes the block with the deferred-max path; every
@@ -575,7 +590,7 @@ def test_huge_spike_fallback(torch_dev, policy, d):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("policy", FAST_POLICIES)
+@pytest.mark.parametrize("policy", _shipped(FAST_POLICIES))
 def test_spiked_rescale(torch_dev, policy, d):
     """Force the deferred-rescale branch (rule: a rare data-dependent branch needs its own
     test): one key row aligned with one query row makes that row's max jump past the
@@ -602,7 +617,7 @@ def test_spiked_rescale(torch_dev, policy, d):
         _hip.set_policy(0)
 
 
-@pytest.mark.parametrize("policy", (0, 112, 113, 114))
+@pytest.mark.parametrize("policy", _shipped((0, 112, 113, 114)))
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 @pytest.mark.parametrize("causal", [True, False])
 def test_generic_causal_bwd_pairing_vs_oracle(torch_dev, policy, dtype, causal):
@@ -636,7 +651,7 @@ def test_generic_causal_bwd_pairing_vs_oracle(torch_dev, policy, dtype, causal):
         _hip.set_policy(0)
 
 
-@pytest.mark.parametrize("policy", (0, 109, 110, 111))
+@pytest.mark.parametrize("policy", _shipped((0, 109, 110, 111)))
 @pytest.mark.parametrize("causal", [False, True])
 def test_fp32_fwd_policies_vs_oracle(torch_dev, policy, causal):
     """fp32 forward kernels (the reference's precision): 0 default (register-Q ring, paired
@@ -659,7 +674,7 @@ def test_fp32_fwd_policies_vs_oracle(torch_dev, policy, causal):
         _hip.set_policy(0)
 
 
-@pytest.mark.parametrize("policy", (0, 40, 43, 62, 66, 69, 70, 71, 72, 73, 74, 75, 77, 107, 108, 120))
+@pytest.mark.parametrize("policy", _shipped((0, 40, 43, 62, 66, 69, 70, 71, 72, 73, 74, 75, 77, 107, 108, 120, 121)))
 @pytest.mark.parametrize("causal", [False, True])
 def test_bf16_bwd_policies_vs_oracle(torch_dev, policy, causal):
     """bf16 d=64 backward variants (0 default, 40 software-pipelined dK/dV) against the
