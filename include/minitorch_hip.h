@@ -116,6 +116,15 @@ int mt_attn_softmax_bw(float* dinp, const float* dout, const float* soft, int64_
                        int64_t softmax_len, void* stream);
 /* LayerNorm over the last dim of [rows, hidden]; var is stored with +1e-8.
  * (reference src/layernorm_kernel.cu:36-98) */
+/* Softmax cross-entropy over rows of [rows, classes] fp32 logits (contiguous rows), the
+ * reference's softmax_loss (minitorch/nn.py: logsumexp(logits) - logits[target]) in one pass:
+ * loss[r] = lse[r] - logits[r, target[r]], lse[r] = log Σ_j exp(logits[r, j]); target holds
+ * class ids as floats (minitorch's storage type). Backward:
+ * dlogits[r, j] = dloss[r] (exp(logits[r, j] - lse[r]) - [j == target[r]]). */
+int mt_softmax_xent_fw(float* loss, float* lse, const float* logits, const float* target, int64_t rows,
+                       int64_t classes, void* stream);
+int mt_softmax_xent_bw(float* dlogits, const float* dloss, const float* logits, const float* target,
+                       const float* lse, int64_t rows, int64_t classes, void* stream);
 int mt_layernorm_fw(float* ln_res, float* var, float* mean, const float* inp, const float* gamma,
                     const float* beta, int64_t rows, int64_t hidden, void* stream);
 int64_t mt_layernorm_bw_workspace_bytes(int64_t rows, int64_t hidden);

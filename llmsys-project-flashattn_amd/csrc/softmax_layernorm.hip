@@ -587,11 +587,109 @@ static int64_t ln_vec_blocks(int64_t rows, int64_t H) {
   return g > cap ? cap : (g < 1 ? 1 : g);
 }
 
+// ---- softmax cross-entropy (reference minitorch/nn.py softmax_loss) -------------------------
+// loss[r] = logsumexp(x[r, :]) - x[r, t_r], the reference's composition (max, shift, exp, sum,
+// log, one-hot pick: ten elementwise passes over the [rows, C] logits plus as many in the
+// backward) as one read of the row: an online (max, sum) per lane, combined across the
+// workgroup, lse[r] kept for the backward. Backward: dx = g[r] (exp(x - lse[r]) - [j == t_r]),
+// one read and one write. One 256-thread workgroup per row (grid-stride), 16-B vectors when
+// the rows are 16-B aligned.
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float n = fmaxf(m, m2);
+  s = (m == -INFINITY ? 0.f : s * expf(m - n)) + (m2 == -INFINITY ? 0.f : s2 * expf(m2 - n));
+  m = n;
+}
+__device__ __forceinline__ void lse_add(float& m, float& s, float x) {
+  if (x > m) {
+    s = (m == -INFINITY ? 0.f : s * expf(m - x)) + 1.f;
+    m = x;
+  } else {
+    s += expf(x - m);
+  }
+}
+
+__global__ __launch_bounds__(256) void xent_fw_kernel(float* loss, float* lse, const float* x,
+                                                      const float* tgt, int64_t rows, int64_t C,
+                                                      int vec) {
+  __shared__ float red_m[4], red_s[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const float* xr = x + r * C;
+    float m = -INFINITY, s = 0.f;
+    int64_t j0 = 0;
+    if (vec) {
+      for (int64_t j = 4 * (int64_t)tid; j + 3 < C; j += 1024) {
+        const float4 v = *(const float4*)(xr + j);
+        lse_add(m, s, v.x); lse_add(m, s, v.y); lse_add(m, s, v.z); lse_add(m, s, v.w);
+      }
+      j0 = C / 4 * 4;
+    }
+    for (int64_t j = j0 + tid; j < C; j += 256) lse_add(m, s, xr[j]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lse_merge(m, s, __shfl_xor(m, o), __shfl_xor(s, o));
+    if (lane == 0) { red_m[w] = m; red_s[w] = s; }
+    __syncthreads();
+    if (tid == 0) {
+      float M = red_m[0], S = red_s[0];
+      for (int i = 1; i < 4; ++i) lse_merge(M, S, red_m[i], red_s[i]);
+      const float l = M + logf(S);
+      const int64_t t = (int64_t)tgt[r];
+      lse[r] = l;
+      loss[r] = l - ((t >= 0 && t < C) ? xr[t] : 0.f);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void xent_bw_kernel(float* dx, const float* g, const float* x,
+                                                      const float* tgt, const float* lse,
+                                                      int64_t rows, int64_t C, int vec) {
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const float* xr = x + r * C;
+    float* dr = dx + r * C;
+    const float gr = g[r], l = lse[r];
+    const int64_t t = (int64_t)tgt[r];
+    int64_t j0 = 0;
+    if (vec) {
+      for (int64_t j = 4 * (int64_t)threadIdx.x; j + 3 < C; j += 1024) {
+        const float4 v = *(const float4*)(xr + j);
+        float4 o = make_float4(gr * (expf(v.x - l) - (j == t ? 1.f : 0.f)),
+                               gr * (expf(v.y - l) - (j + 1 == t ? 1.f : 0.f)),
+                               gr * (expf(v.z - l) - (j + 2 == t ? 1.f : 0.f)),
+                               gr * (expf(v.w - l) - (j + 3 == t ? 1.f : 0.f)));
+        *(float4*)(dr + j) = o;
+      }
+      j0 = C / 4 * 4;
+    }
+    for (int64_t j = j0 + threadIdx.x; j < C; j += 256) dr[j] = gr * (expf(xr[j] - l) - (j == t ? 1.f : 0.f));
+  }
+}
+
 }  // namespace mt
 
 using namespace mt;
 
 extern "C" {
+
+int mt_softmax_xent_fw(float* loss, float* lse, const float* logits, const float* target, int64_t rows,
+                       int64_t classes, void* stream) {
+  if (rows <= 0 || classes <= 0) return set_error("mt_softmax_xent_fw: bad sizes");
+  const int vec = (classes % 4 == 0) && al16(logits);
+  const unsigned grid = (unsigned)(rows < 65536 ? rows : 65536);
+  hipLaunchKernelGGL(xent_fw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, loss, lse, logits, target,
+                     rows, classes, vec);
+  return check_hip(hipGetLastError(), "mt_softmax_xent_fw");
+}
+
+int mt_softmax_xent_bw(float* dlogits, const float* dloss, const float* logits, const float* target,
+                       const float* lse, int64_t rows, int64_t classes, void* stream) {
+  if (rows <= 0 || classes <= 0) return set_error("mt_softmax_xent_bw: bad sizes");
+  const int vec = (classes % 4 == 0) && al16(logits) && al16(dlogits);
+  const unsigned grid = (unsigned)(rows < 65536 ? rows : 65536);
+  hipLaunchKernelGGL(xent_bw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dlogits, dloss, logits,
+                     target, lse, rows, classes, vec);
+  return check_hip(hipGetLastError(), "mt_softmax_xent_bw");
+}
 
 int mt_attn_softmax_fw(float* out, const float* inp, const float* mask, int64_t B, int64_t nh,
                        int64_t from_len, int64_t to_len, const int64_t* mask_strides,

@@ -51,6 +51,8 @@ _PROTOS = {
     "mt_attn_softmax_fw": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _int, _vp]),
     "mt_attn_softmax_bw": (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_layernorm_fw": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
+    "mt_softmax_xent_fw": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp]),
+    "mt_softmax_xent_bw": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_layernorm_bw_workspace_bytes": (_i64, [_i64, _i64]),
     "mt_layernorm_bw": (_int, [_vp] * 9 + [_i64, _i64, _vp, _vp]),
     "mt_tensor_map": (_int, [_int, _vp, _i64p, _i64p, _int, _vp, _i64p, _i64p, _int, _vp]),

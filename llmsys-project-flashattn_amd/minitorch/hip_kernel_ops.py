@@ -207,6 +207,27 @@ class HipKernelOps(TensorOps):
 
     # ---- fused kernels -------------------------------------------------------------------
     @staticmethod
+    def softmax_xent_fw(logits: Tensor, target: Tensor):
+        """(loss[rows], lse[rows]) of the reference's softmax_loss (nn.py) in one pass."""
+        x = _dense(logits)
+        t = _dense(target)
+        rows, C = x.shape
+        loss = _out(x, (rows,))
+        lse = _out(x, (rows,))
+        _hip.check(_hip.lib().mt_softmax_xent_fw(_ptr(loss), _ptr(lse), _ptr(x), _ptr(t), rows, C,
+                                                 _stream()), "softmax_xent_fw")
+        return loss, lse
+
+    @staticmethod
+    def softmax_xent_bw(grad: Tensor, logits: Tensor, target: Tensor, lse: Tensor) -> Tensor:
+        g, x, t = _dense(grad), _dense(logits), _dense(target)
+        rows, C = x.shape
+        dx = _out(x, (rows, C))
+        _hip.check(_hip.lib().mt_softmax_xent_bw(_ptr(dx), _ptr(g), _ptr(x), _ptr(t), _ptr(lse), rows, C,
+                                                 _stream()), "softmax_xent_bw")
+        return dx
+
+    @staticmethod
     def attn_softmax_fw(inp: Tensor, mask: Optional[Tensor], mask_future: bool = False) -> Tensor:
         B, nh, T_from, T_to = inp.shape
         x = inp if inp._tensor.is_dense() else inp.contiguous()

@@ -85,6 +85,14 @@ def logsumexp(input: Tensor, dim: int) -> Tensor:  # noqa: A002
 
 
 def softmax_loss(logits: Tensor, target: Tensor) -> Tensor:
+    """Per-row cross-entropy logsumexp(logits) - logits[target] (reference minitorch/nn.py).
+    A backend with a fused kernel (HipKernelOps.softmax_xent_fw / _bw) computes it in one pass
+    each way; otherwise the reference's composition."""
     batch = logits.shape[0]
+    be = logits.backend
+    if getattr(be, "softmax_xent_fw", None) is not None and logits.dims == 2 and logits._tensor.on_device:
+        from .tensor_functions import SoftmaxXent
+        t = target if target._tensor.is_dense() else target.contiguous()
+        return SoftmaxXent.apply(logits, t if t.dims == 1 else t.view(batch))
     picked = (logits * one_hot(target, logits.shape[1])).sum(dim=1)
     return (logsumexp(logits, dim=1) - picked).view(batch)

@@ -238,6 +238,23 @@ class Permute(Function):
         return grad_output._new(grad_output._tensor.permute(*inv)), 0.0
 
 
+class SoftmaxXent(Function):
+    """Per-row softmax cross-entropy, the reference's softmax_loss (minitorch/nn.py:
+    logsumexp(logits, 1) - logits[target]) as one backend kernel each way; target (class
+    ids) gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, logits, target):
+        loss, lse = logits.f.softmax_xent_fw(logits, target)
+        ctx.save_for_backward(logits, target, lse)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        logits, target, lse = ctx.saved_values
+        return logits.f.softmax_xent_bw(grad_output, logits, target, lse), 0.0
+
+
 class View(Function):
     @staticmethod
     def forward(ctx, a, shape):

@@ -110,6 +110,9 @@ class TensorBackend:
         self.cuda = ops.cuda
         # optional device RNG (HipKernelOps.rand_uniform); None -> host draws
         self.rand_uniform = getattr(ops, "rand_uniform", None)
+        # fused softmax cross-entropy (optional: a backend without it keeps the composition)
+        self.softmax_xent_fw = getattr(ops, "softmax_xent_fw", None)
+        self.softmax_xent_bw = getattr(ops, "softmax_xent_bw", None)
         # fused kernels
         self.attn_softmax_fw = ops.attn_softmax_fw
         self.attn_softmax_bw = ops.attn_softmax_bw
