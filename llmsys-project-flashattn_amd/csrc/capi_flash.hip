@@ -25,6 +25,7 @@ hipError_t launch_fwd_v5(const AttnArgs& a, bool causal, int ahead, int var, hip
 hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled);
 hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hipStream_t st,
                            bool* handled, int pair = 0);
+hipError_t launch_fwd_d128v2(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st, int pair, bool ring);
@@ -112,6 +113,10 @@ enum : int {
   kPolBwdF32Lds = 114,  // fp32 backward: fa_bwd.hip's LDS-row kernels instead of the register-row ring
   kPolBwdFused = 120,   // bf16 d = 64: dQ folded into the dK/dV pass (fa_bwd_fused.hip)
   kPolBwdSplit = 121,   // bf16 d = 64: the split backward's defaults (dK/dV pass + dQ pass)
+  // d = 128 non-causal on the 16x16x32 MFMA with LDS-DMA K/V (fa_fwd_d128v2.hip): 130 MFMA
+  // row sums, 131 VALU row sums, 132 = 130 + s_setprio 1 for waves 4-7, 133 / 134 = 130 / 131
+  // with 4-wave workgroups (two per CU)
+  kPolD128v2 = 130, kPolD128v2Vs = 131, kPolD128v2Prio = 132, kPolD128v2w4 = 133, kPolD128v2w4Vs = 134,
 };
 static const int kProductPolicies[] = {kPolDefault, kPolGeneric, kPolBwdFused, kPolBwdSplit};
 #ifdef MT_DIAGNOSTICS
@@ -123,7 +128,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs};
 #endif
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
@@ -237,6 +242,11 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
 #ifdef MT_DIAGNOSTICS
     case 101: e = launch_fwd_v6(a, causal, 1, st, handled); break;  // reduced precision (timing)
 #endif
+    case kPolD128v2: case kPolD128v2Vs: case kPolD128v2Prio: case kPolD128v2w4: case kPolD128v2w4Vs: {
+      static const int kVar[5] = {0, 1, 2, 16, 17};
+      e = launch_fwd_d128v2(a, causal, kVar[pol - kPolD128v2], st, handled);
+      break;
+    }
     case kPolV5Causal8: case kPolV5Causal4:
       if (causal)
         e = launch_fwd_v5(a, true, 2, pol == kPolV5Causal8 ? v5::kDefault : v5::kDefault & ~v5::kW8,

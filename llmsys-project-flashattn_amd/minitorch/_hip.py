@@ -89,6 +89,15 @@ def lib() -> ctypes.CDLL:
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with `make -C {os.path.dirname(_HERE)}` "
                 "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        # One HIP runtime per process: torch's. Device buffers and streams are torch's, and
+        # loaded first the library would bind /opt/rocm's libamdhip64 beside torch's bundled
+        # one, which on some boxes then reports "no ROCm-capable device" for every call
+        # (scripts/probe_runtime.py). With torch imported first, the library's libamdhip64
+        # dependency resolves (by soname) to the runtime torch already mapped.
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # plain C-ABI use without torch: the library's own runtime
+            pass
         l = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _PROTOS.items():
             fn = getattr(l, name)

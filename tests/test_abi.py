@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     from minitorch import _hip
     if not os.path.exists(_hip.LIB_PATH):
         pytest.skip("library not built")
-    lib = ctypes.CDLL(_hip.LIB_PATH)
+    lib = _hip.lib()  # torch first: one HIP runtime per process
     missing = []
     for h in HEADERS:
         for name in _declared(h):

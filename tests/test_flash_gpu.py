@@ -479,6 +479,39 @@ def test_v5_split_keys_vs_oracle(torch_dev, policy, parity_record):
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
+@pytest.mark.parametrize("policy", _shipped([0, 130, 131, 132, 133, 134]))
+def test_d128_vs_oracle(torch_dev, policy, parity_record):
+    """The d = 128 non-causal forward (the default and policy 130, the 16x16x32 kernel with
+    LDS-DMA staging and MFMA row sums): every head, every row against the C oracle at the
+    elementwise bound. Shapes: two tiles (no steady-state iteration), three tiles (one
+    iteration plus the odd tail), a partial last query block (N = 320: waves past N), an even
+    and an odd tile count at more heads, and a large score in a late tile (the frozen
+    first-tile reference meets it)."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(128)
+    worst = 0.0
+    try:
+        _use_policy(_hip, policy)
+        for (B, H, N) in ((1, 2, 128), (1, 1, 192), (1, 2, 320), (2, 3, 1024), (1, 4, 1600)):
+            q, k, v = (A.bf16_round(rng.standard_normal((B, H, N, 128)).astype(np.float32))
+                       for _ in range(3))
+            k[0, 0, N - 5] = A.bf16_round(q[0, 0, 7] * 0.5)  # a large score in the last tile
+            o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), False)
+            torch.cuda.synchronize()
+            o_ref, m_ref, l_ref = cref.attn_fwd(q.reshape(B * H, N, 128), k.reshape(B * H, N, 128),
+                                                v.reshape(B * H, N, 128), False)
+            err = np.abs(_np(o) - o_ref.reshape(B, H, N, 128))
+            bound = 1e-3 + 2.0 ** -7 * _pv_abs(q, k, v, causal=False)
+            assert np.all(err <= bound), f"{(B, H, N)}: max err/bound {float((err / bound).max()):.3f}"
+            _check_ml(_np(m), _np(l), m_ref.reshape(B, H, N), l_ref.reshape(B, H, N), exact=False)
+            worst = max(worst, float((err / bound).max()))
+    finally:
+        _hip.set_policy(0)
+    parity_record("test_d128_vs_oracle", f"policy {policy}", max_err_over_bound=worst,
+                  bound="1e-3 + 2^-7 * (P|V|) elementwise")
+
+
 def _pv_abs(q, k, v, causal=True):
     """(P |V|) per element (the O term of tests/bounds.py), from the C oracle run on |V|."""
     B, H, N, d = q.shape
@@ -531,10 +564,11 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # kernel policies of the bf16 forward (mt_flash_set_kernel_policy; what each id selects is
 # listed with the kPol* enum in csrc/capi_flash.hip): 0 the default, 2-6 fa_fwd_fast.hip,
 # 21-26 v4, 27-31 / 35-39 / 46-49 / 54-58 / 61 v5, 32 / 33 / 44 / 45 d = 128, 50-53 / 63-65
-# causal heavy + light query-block pairs, 100 v6. Every one computes the same attention.
+# causal heavy + light query-block pairs, 100 v6, 130 the 16x16x32 d = 128 kernel. Every one
+# computes the same attention.
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
                  44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
-                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106)
+                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106, 130, 131, 132, 133, 134)
 
 
 @pytest.mark.parametrize("policy", _shipped(FAST_POLICIES))
