@@ -114,7 +114,7 @@ enum : int {
   kPolBwdFused = 120,   // bf16 d = 64: dQ folded into the dK/dV pass (fa_bwd_fused.hip)
   kPolBwdSplit = 121,   // bf16 d = 64: the split backward's defaults (dK/dV pass + dQ pass)
   // d = 128 non-causal on the 16x16x32 MFMA with LDS-DMA K/V (fa_fwd_d128v2.hip): 130 MFMA
-  // row sums, 131 VALU row sums, 132 = 130 + s_setprio 1 for waves 4-7, 133 / 134 = 130 / 131
+  // row sums (the default for non-causal d = 128, N % 64 == 0), 131 VALU row sums, 132 = 130 + s_setprio 1 for waves 4-7, 133 / 134 = 130 / 131
   // with 4-wave workgroups (two per CU)
   kPolD128v2 = 130, kPolD128v2Vs = 131, kPolD128v2Prio = 132, kPolD128v2w4 = 133, kPolD128v2w4Vs = 134,
 };
@@ -349,7 +349,8 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     // r1_ab_causal_pair.txt).
     int nw = -1, pair = 0;
     bool dma = false;
-    switch (pol) {
+    if (pol == kPolDefault && !causal) e = launch_fwd_d128v2(a, false, 0, st, handled);
+    switch (*handled ? -1 : pol) {
       case kPolDefault: nw = 8; pair = causal ? 2 : 0; break;
       case kPolD128w8: nw = 8; break;
       case kPolD128w4: nw = 4; break;
@@ -420,7 +421,11 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
     if (!*handled)
       e = launch_fwd_v4(a, causal, causal && N >= 8192 ? 8 : 4, !causal, st, handled, causal ? 2 : 0);
   }
-  // d = 128: 8 waves, causal with paired query blocks (profiles/r1_ab_d128_warm.txt)
+  // d = 128 non-causal, N % 64 == 0: the 16x16x32 kernel with LDS-DMA staging and MFMA row
+  // sums (policy 130: C4 shard 13.37 vs 14.90 ms, (8,16,4096,128) 0.897 vs 0.992 ms,
+  // profiles/r3_ab_d128v2.txt); else 8 waves of fa_fwd_d128.hip, causal with paired query
+  // blocks (profiles/r1_ab_d128_warm.txt)
+  if (!*handled && a.d == 128 && !causal) e = launch_fwd_d128v2(a, false, 0, st, handled);
   if (!*handled && a.d == 128) e = launch_fwd_d128(a, causal, 8, false, st, handled, causal ? 2 : 0);
   // anything else those decline (buffer range): the single-phase 8-wave kernel
   if (!*handled) e = launch_fwd_fast(a, causal, 2, st, handled);

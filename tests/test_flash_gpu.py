@@ -329,7 +329,8 @@ def test_config3_bf16_full_size(torch_dev, causal, parity_record):
     ((2, 3, 200, 64), True, True),
     ((1, 4, 1024, 64), False, True),   # small grid: v5 with the keys split
     ((2, 4, 2048, 64), True, True),    # v6 causal
-    ((1, 2, 256, 128), False, False),  # d = 128: the fp32 O takes the generic kernels
+    ((1, 2, 256, 128), False, True),   # d = 128 non-causal: the 16x16x32 kernel writes either O
+    ((1, 2, 256, 128), True, False),   # d = 128 causal: the fp32 O takes the generic kernels
     ((1, 2, 100, 32), True, True),     # d = 32: generic
 ])
 def test_fp32_out_option(torch_dev, shape, causal, same_kernel):
