@@ -116,7 +116,10 @@ enum : int {
   // d = 128 non-causal on the 16x16x32 MFMA with LDS-DMA K/V (fa_fwd_d128v2.hip): 130 MFMA
   // row sums (the default for non-causal d = 128, N % 64 == 0), 131 VALU row sums, 132 = 130 + s_setprio 1 for waves 4-7, 133 / 134 = 130 / 131
   // with 4-wave workgroups (two per CU)
+  // 135 / 136 = 130 with the operand reads 3 / 4 fragments ahead
   kPolD128v2 = 130, kPolD128v2Vs = 131, kPolD128v2Prio = 132, kPolD128v2w4 = 133, kPolD128v2w4Vs = 134,
+  kPolD128v2Ah3 = 135, kPolD128v2Ah4 = 136,
+  kPolD128v2Causal = 137,  // the causal form (paired light / heavy query blocks, per-wave diagonal)
 };
 static const int kProductPolicies[] = {kPolDefault, kPolGeneric, kPolBwdFused, kPolBwdSplit};
 #ifdef MT_DIAGNOSTICS
@@ -128,7 +131,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal};
 #endif
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
@@ -242,9 +245,10 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
 #ifdef MT_DIAGNOSTICS
     case 101: e = launch_fwd_v6(a, causal, 1, st, handled); break;  // reduced precision (timing)
 #endif
-    case kPolD128v2: case kPolD128v2Vs: case kPolD128v2Prio: case kPolD128v2w4: case kPolD128v2w4Vs: {
-      static const int kVar[5] = {0, 1, 2, 16, 17};
-      e = launch_fwd_d128v2(a, causal, kVar[pol - kPolD128v2], st, handled);
+    case kPolD128v2: case kPolD128v2Vs: case kPolD128v2Prio: case kPolD128v2w4: case kPolD128v2w4Vs:
+    case kPolD128v2Ah3: case kPolD128v2Ah4: case kPolD128v2Causal: {
+      static const int kVar[8] = {0, 1, 2, 16, 17, 4, 8, 32};
+      if ((pol == kPolD128v2Causal) == causal) e = launch_fwd_d128v2(a, causal, kVar[pol - kPolD128v2], st, handled);
       break;
     }
     case kPolV5Causal8: case kPolV5Causal4:
@@ -349,7 +353,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     // r1_ab_causal_pair.txt).
     int nw = -1, pair = 0;
     bool dma = false;
-    if (pol == kPolDefault && !causal) e = launch_fwd_d128v2(a, false, 0, st, handled);
+    if (pol == kPolDefault) e = launch_fwd_d128v2(a, causal, causal ? 32 : 0, st, handled);
     switch (*handled ? -1 : pol) {
       case kPolDefault: nw = 8; pair = causal ? 2 : 0; break;
       case kPolD128w8: nw = 8; break;
@@ -421,11 +425,13 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
     if (!*handled)
       e = launch_fwd_v4(a, causal, causal && N >= 8192 ? 8 : 4, !causal, st, handled, causal ? 2 : 0);
   }
-  // d = 128 non-causal, N % 64 == 0: the 16x16x32 kernel with LDS-DMA staging and MFMA row
-  // sums (policy 130: C4 shard 13.37 vs 14.90 ms, (8,16,4096,128) 0.897 vs 0.992 ms,
-  // profiles/r3_ab_d128v2.txt); else 8 waves of fa_fwd_d128.hip, causal with paired query
+  // d = 128, N % 64 == 0: the 16x16x32 kernel with LDS-DMA staging and MFMA row sums
+  // (policy 130: C4 shard 13.37 vs 14.90 ms, (8,16,4096,128) 0.897 vs 0.992 ms,
+  // profiles/r3_ab_d128v2.txt; causal, paired light / heavy blocks, policy 137: 7.53 vs
+  // 8.14 ms at (8,16,16384,128), 0.537 vs 0.591 ms at (8,16,4096,128),
+  // r3_ab_d128v2_ahead_causal.txt); else 8 waves of fa_fwd_d128.hip, causal with paired query
   // blocks (profiles/r1_ab_d128_warm.txt)
-  if (!*handled && a.d == 128 && !causal) e = launch_fwd_d128v2(a, false, 0, st, handled);
+  if (!*handled && a.d == 128) e = launch_fwd_d128v2(a, causal, causal ? 32 : 0, st, handled);
   if (!*handled && a.d == 128) e = launch_fwd_d128(a, causal, 8, false, st, handled, causal ? 2 : 0);
   // anything else those decline (buffer range): the single-phase 8-wave kernel
   if (!*handled) e = launch_fwd_fast(a, causal, 2, st, handled);

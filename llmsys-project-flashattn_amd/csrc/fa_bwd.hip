@@ -23,25 +23,67 @@
 namespace mt {
 
 // ---------------------------------------------------------------------------
-template <typename T>
+// 16 lanes per row, 16 rows per 256-thread workgroup and pass, kPrepPasses passes with every
+// load issued first. VEC (16-B rows and strides): each lane reads 16-B chunks sub, sub + 16, ..
+// of its row; else elements sub, sub + 16, ... (One wave per row, 4 rows per workgroup, had
+// run the C2 fp32 prep at ≈2.2 TB/s: 32768 workgroups of 4-B loads.)
+constexpr int kPrepPasses = 4;
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void fa_bwd_prep(AttnArgs p) {
-  const int lane = threadIdx.x & 63;
   const int64_t rows = (int64_t)p.B * p.H * p.N;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int n = (int)(row % p.N);
-  const int64_t bh = row / p.N;
-  const int b = (int)(bh / p.H), hh = (int)(bh % p.H);
-  const T* O = (const T*)p.o + b * p.so[0] + hh * p.so[1] + (int64_t)n * p.so[2];
-  const T* dO = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + (int64_t)n * p.sdo[2];
-  float acc = 0.f;
-  for (int c = lane; c < p.d; c += 64) acc += to_f32(O[c]) * to_f32(dO[c]);
+  const int sub = threadIdx.x & 15;
+  const int64_t row0 = (int64_t)blockIdx.x * 16 * kPrepPasses + (threadIdx.x >> 4);
+  constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
+  float acc[kPrepPasses];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  if (lane == 0) {
-    p.delta[row] = acc;
-    p.lse2[row] = p.m[row] * kLog2e + log2f(p.l[row]);
+  for (int u = 0; u < kPrepPasses; ++u) {
+    acc[u] = 0.f;
+    const int64_t row = row0 + 16 * u;
+    if (row >= rows) continue;
+    const int n = (int)(row % p.N);
+    const int64_t bh = row / p.N;
+    const int b = (int)(bh / p.H), hh = (int)(bh % p.H);
+    const T* O = (const T*)p.o + b * p.so[0] + hh * p.so[1] + (int64_t)n * p.so[2];
+    const T* dO = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + (int64_t)n * p.sdo[2];
+    if (VEC) {
+      for (int c = sub * EPC; c < p.d; c += 16 * EPC) {
+        const uint4 x = *(const uint4*)(O + c), y = *(const uint4*)(dO + c);
+        const T* xo = (const T*)&x;
+        const T* yo = (const T*)&y;
+#pragma unroll
+        for (int j = 0; j < EPC; ++j) acc[u] += to_f32(xo[j]) * to_f32(yo[j]);
+      }
+    } else {
+      for (int c = sub; c < p.d; c += 16) acc[u] += to_f32(O[c]) * to_f32(dO[c]);
+    }
   }
+#pragma unroll
+  for (int u = 0; u < kPrepPasses; ++u) {
+    float a = acc[u];
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) a += __shfl_xor(a, off);
+    const int64_t row = row0 + 16 * u;
+    if (sub == 0 && row < rows) {
+      p.delta[row] = a;
+      p.lse2[row] = p.m[row] * kLog2e + log2f(p.l[row]);
+    }
+  }
+}
+
+// 16-B chunks of O and dO rows: d, the row strides and the bases on 16-B boundaries.
+static bool prep_vec(const AttnArgs& a, int esize) {
+  const int epc = 16 / esize;
+  return a.d % epc == 0 && a.so[0] % epc == 0 && a.so[1] % epc == 0 && a.so[2] % epc == 0 &&
+         a.sdo[0] % epc == 0 && a.sdo[1] % epc == 0 && a.sdo[2] % epc == 0 &&
+         ((uintptr_t)a.o & 15) == 0 && ((uintptr_t)a.dout & 15) == 0;
+}
+template <typename T>
+static hipError_t launch_prep(const AttnArgs& a, hipStream_t st) {
+  const int64_t rows = (int64_t)a.B * a.H * a.N;
+  const dim3 grid((unsigned)((rows + 16 * kPrepPasses - 1) / (16 * kPrepPasses)));
+  if (prep_vec(a, sizeof(T))) hipLaunchKernelGGL((fa_bwd_prep<T, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((fa_bwd_prep<T, false>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -431,9 +473,7 @@ static hipError_t launch_bwd_t(const AttnArgs& a, hipStream_t st) {
   const int nz = (a.d + DT - 1) / DT;
   const int nblk = PAIR ? ((a.N + 127) / 128 + 1) / 2 : (a.N + 127) / 128;
   {
-    const int64_t rows = (int64_t)a.B * a.H * a.N;
-    hipLaunchKernelGGL(fa_bwd_prep<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
-    hipError_t e = hipGetLastError();
+    const hipError_t e = launch_prep<T>(a, st);
     if (e != hipSuccess) return e;
   }
   {
@@ -478,12 +518,7 @@ hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
                               hipStream_t st, int pair, bool ring) {
   const bool pr = pair == 1 || (pair == 2 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
   if (ring && vec && (bf16_io ? a.d < 64 : a.d <= 64)) {
-    const int64_t rows = (int64_t)a.B * a.H * a.N;
-    if (bf16_io)
-      hipLaunchKernelGGL(fa_bwd_prep<bf16>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL(fa_bwd_prep<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
-    const hipError_t e = hipGetLastError();
+    const hipError_t e = bf16_io ? launch_prep<bf16>(a, st) : launch_prep<float>(a, st);
     if (e != hipSuccess) return e;
     return launch_bwd_ring(a, bf16_io, causal, pr, st);
   }

@@ -26,28 +26,48 @@ namespace mt {
 using namespace bwdbf16;
 
 // ---------------------------------------------------------------------------------------
-// prep: nlse = −(m·log2e + log2 l)/c2, ndel = −rowsum(dO ∘ O); 8 lanes per row.
+// prep: nlse = −(m·log2e + log2 l)/c2, ndel = −rowsum(dO ∘ O); 8 lanes per row, kPrepRows
+// rows per lane group (all loads issued first: with one row per 32-row workgroup the
+// C3 prep ran 16384 tiny workgroups at ≈2.2 TB/s).
+constexpr int kPrepRows = 4;
 __global__ __launch_bounds__(256) void fa_bwd_prep_bf16(AttnArgs p) {
   const int64_t rows = (int64_t)p.B * p.H * p.N;
-  const int64_t row = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int64_t row0 = (int64_t)blockIdx.x * 32 * kPrepRows + (threadIdx.x >> 3);
   const int sub = threadIdx.x & 7;
-  float acc = 0.f;
-  if (row < rows) {
-    const int n = (int)(row % p.N);
-    const int64_t bh = row / p.N;
-    const int b = (int)(bh / p.H), hh = (int)(bh % p.H);
-    const bf16* O = (const bf16*)p.o + b * p.so[0] + hh * p.so[1] + (int64_t)n * p.so[2];
-    const bf16* dO = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + (int64_t)n * p.sdo[2];
-    const bf16x8 o = *(const bf16x8*)(O + 8 * sub), g = *(const bf16x8*)(dO + 8 * sub);
+  bf16x8 o[kPrepRows], g[kPrepRows];
+  float mm[kPrepRows], ll[kPrepRows];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += (float)o[j] * (float)g[j];
+  for (int u = 0; u < kPrepRows; ++u) {
+    const int64_t row = row0 + 32 * u;
+    o[u] = bf16x8{};
+    g[u] = bf16x8{};
+    mm[u] = 0.f;
+    ll[u] = 1.f;
+    if (row < rows) {
+      const int n = (int)(row % p.N);
+      const int64_t bh = row / p.N;
+      const int b = (int)(bh / p.H), hh = (int)(bh % p.H);
+      o[u] = *(const bf16x8*)((const bf16*)p.o + b * p.so[0] + hh * p.so[1] + (int64_t)n * p.so[2] + 8 * sub);
+      g[u] = *(const bf16x8*)((const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + (int64_t)n * p.sdo[2] + 8 * sub);
+      if (sub == 0) {
+        mm[u] = p.m[row];
+        ll[u] = p.l[row];
+      }
+    }
   }
-  acc += __shfl_xor(acc, 1);
-  acc += __shfl_xor(acc, 2);
-  acc += __shfl_xor(acc, 4);
-  if (row < rows && sub == 0) {
-    p.delta[row] = -acc;
-    p.lse2[row] = -(p.m[row] * kLog2e + log2f(p.l[row])) / p.scale_log2;
+#pragma unroll
+  for (int u = 0; u < kPrepRows; ++u) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += (float)o[u][j] * (float)g[u][j];
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    const int64_t row = row0 + 32 * u;
+    if (row < rows && sub == 0) {
+      p.delta[row] = -acc;
+      p.lse2[row] = -(mm[u] * kLog2e + log2f(ll[u])) / p.scale_log2;
+    }
   }
 }
 
@@ -1066,7 +1086,7 @@ template <bool CAUSAL>
 static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t st) {
   // (variant is adjusted below for shapes a form does not take)
   const int64_t rows = (int64_t)a.B * a.H * a.N;
-  hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 32 * kPrepRows - 1) / (32 * kPrepRows))), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // 20: dQ folded into the dK/dV pass (fa_bwd_fused.hip: 5 products instead of 7)

@@ -100,18 +100,18 @@ __device__ __forceinline__ void sm_slot(int m, const Sc& s, int kb, float c2, co
 
 // QKᵀ phase over 16-key blocks kb0, kb0 + 1 of the tile at sk into S (16 MFMAs: fragment f =
 // m >> 1 = (block, k-step), query half m & 1), beside the softmax of block skb of s_in.
-template <bool SOFT, bool VS = false>
+template <bool SOFT, bool VS = false, int AH = 2>
 __device__ __forceinline__ void qk_phase(const bf16* sk, const int (&ko)[4], const bf16x8 (&qf)[2][4],
                                          Sc& S, int kb0, const Sc& s_in, int skb, float c2,
                                          const float (&nmc)[2], Pf& pf, f32x2* acc = nullptr) {
   bf16x8 kf[8];
-  kf[0] = kread(sk, ko, kb0, 0);
-  kf[1] = kread(sk, ko, kb0, 1);
+#pragma unroll
+  for (int f = 0; f < AH; ++f) kf[f] = kread(sk, ko, kb0 + (f >> 2), f & 3);
   f32x2 ep;
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
     const int f = m >> 1, kb = kb0 + (f >> 2), ks = f & 3, qh = m & 1;
-    if (!(m & 1) && f + 2 < 8) kf[f + 2] = kread(sk, ko, kb0 + ((f + 2) >> 2), (f + 2) & 3);
+    if (!(m & 1) && f + AH < 8) kf[f + AH] = kread(sk, ko, kb0 + ((f + AH) >> 2), (f + AH) & 3);
     S.s[kb][qh] = mma16(kf[f], qf[qh][ks], ks ? S.s[kb][qh] : f32x4{});
     if (SOFT) sm_slot<VS>(m, s_in, skb, c2, nmc, pf, ep, acc);
     __builtin_amdgcn_sched_barrier(0);
@@ -121,19 +121,19 @@ __device__ __forceinline__ void qk_phase(const bf16* sk, const int (&ko)[4], con
 // PV phase of key half hv of the tile at sv with P operand pp (16 MFMAs: Vᵀ fragment f = m >> 1
 // = d block, query half m & 1; plus, unless VS, the two row-sum MFMAs R[qh] += ones·Pᵀ),
 // beside the softmax of block skb of s_in.
-template <bool SOFT, bool VS = false>
+template <bool SOFT, bool VS = false, int AH = 2>
 __device__ __forceinline__ void pv_phase(const bf16* sv, const int (&vo)[8], f32x4 (&O)[8][2], const Pf& pp,
                                          int hv, f32x4 (&R)[2], const Sc& s_in, int skb, float c2,
                                          const float (&nmc)[2], Pf& pf, f32x2* acc = nullptr) {
   const bf16x8 ones = __builtin_bit_cast(bf16x8, s16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
   bf16x8 vf[8];
-  vf[0] = vread(sv, vo, hv, 0);
-  vf[1] = vread(sv, vo, hv, 1);
+#pragma unroll
+  for (int f = 0; f < AH; ++f) vf[f] = vread(sv, vo, hv, f);
   f32x2 ep;
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
     const int db = m >> 1, qh = m & 1;
-    if (!(m & 1) && db + 2 < 8) vf[db + 2] = vread(sv, vo, hv, db + 2);
+    if (!(m & 1) && db + AH < 8) vf[db + AH] = vread(sv, vo, hv, db + AH);
     O[db][qh] = mma16(vf[db], pp.p[qh], O[db][qh]);
     if (!VS && db == 0) R[qh] = mma16(ones, pp.p[qh], R[qh]);
     if (SOFT) sm_slot<VS>(m, s_in, skb, c2, nmc, pf, ep, acc);
@@ -177,12 +177,15 @@ __device__ __forceinline__ void dma(uint32_t lds, __amdgpu_buffer_rsrc_t rs, int
 // (K slots 0, 1 then V slots 0, 1). NW = 8: one workgroup per CU; NW = 4: two (the two waves
 // of a SIMD from different workgroups, not tied to one barrier). VAR 1: row sums by VALU adds
 // instead of MFMAs; VAR 2: s_setprio 1 for the second half of the waves (MI355X_MICROARCH.md,
-// 'Two waves per SIMD' item 4).
+// 'Two waves per SIMD' item 4); VAR 4 / 8: operand fragments read 3 / 4 fragments (6 / 8
+// MFMAs) ahead instead of 2; VAR 32: causal, a workgroup runs query block u (light) and then
+// nqb - 1 - u (heavy) of one head, as v6's causal form.
 template <int NW, int VAR>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p, int nqb) {
   constexpr int kBQ = 32 * NW;
   constexpr int LPT = TILE * 2 / 1024 / NW;  // 1-KiB LDS-DMA pieces per wave per tile and tensor
-  constexpr bool VS = VAR & 1;
+  constexpr bool VS = VAR & 1, CAUSAL = VAR & 32;
+  constexpr int AH = (VAR & 4) ? 3 : (VAR & 8) ? 4 : 2;  // operand fragments read ahead
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* const sK = (bf16*)smem_raw;  // [2][TILE]
   bf16* const sV = sK + 2 * TILE;    // [2][TILE]
@@ -195,7 +198,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
   const int nblk = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
   const int logical = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + slot;
-  const int bh = logical / nqb, qb = logical % nqb;
+  const int nunit = CAUSAL ? (nqb + 1) / 2 : nqb;  // causal: light / heavy block pairs
+  const int bh = logical / nunit, qb = logical % nunit;
   const int b = bh / p.H, hh = bh % p.H;
 
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
@@ -240,7 +244,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
   const float c2 = p.scale_log2;
   if ((VAR & 2) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
-  const int q0 = qb * kBQ;
+  const int ntiles_all = N / kBK;
+
+  // One query block [q0, q0 + kBQ) of head bh. Causal: wave w's queries qw .. qw + 31 see the
+  // keys up to their own, so it computes tiles 0 .. tD = qw / 64 (the last one masked in
+  // registers); the workgroup stages the tiles its last wave needs, and a wave that is done
+  // keeps staging its share and joins every barrier (fa_fwd_v6.hip's causal scheme).
+  auto run_block = [&](const int q0) __attribute__((always_inline)) {
   const int qw = q0 + wave * 32;  // this wave's first query
   bf16x8 qf[2][4];                // [qh][ks]
 #pragma unroll
@@ -249,7 +259,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qf[qh][ks] = *(const bf16x8*)(qr + 32 * ks + 8 * g);
   }
-  const int ntiles = N / kBK;
+  const int ntiles = CAUSAL ? min(N, q0 + kBQ) / kBK : ntiles_all;  // tiles the workgroup stages
+  const int tD = qw / kBK;
+  const int nbulk = CAUSAL ? (qw < N ? tD + 1 : 0) : ntiles;      // tiles this wave computes
+  // causal: key 16 kb + 4 g + r of the wave's diagonal tile tD is after query 16 qh + i of the
+  // wave when 64 tD + 16 kb + 4 g + r > qw + 16 qh + i
+  auto mask_diag = [&](Sc& S) __attribute__((always_inline)) {
+    const int off = kBK * tD - qw;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (off + 16 * kb + 4 * g + r > 16 * qh + i16) S.s[kb][qh][r] = -INFINITY;
+  };
 
   f32x4 O[8][2];
   auto zero_o = [&]() __attribute__((always_inline)) {
@@ -265,15 +289,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
   dma_k(1, ktile_b);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  {
-    Sc SA, SB;
-    Pf dpf, pl0, pl1, ph;
-    {
-      const float z[2] = {0.f, 0.f};
-      qk_phase<false>(sK, ko, qf, SA, 0, SA, 0, c2, z, dpf);
-      qk_phase<false>(sK, ko, qf, SA, 2, SA, 0, c2, z, dpf);
-    }
-    __syncthreads();  // every wave is done with K slot 0 (iteration 0 stages K(2) into it)
+  Sc SA, SB;
+  Pf dpf, pl0, pl1, ph;
+  if (nbulk >= 1) {
+    const float z[2] = {0.f, 0.f};
+    qk_phase<false>(sK, ko, qf, SA, 0, SA, 0, c2, z, dpf);
+    qk_phase<false>(sK, ko, qf, SA, 2, SA, 0, c2, z, dpf);
+  }
+  __syncthreads();  // every wave is done with K slot 0 (iteration 0 stages K(2) into it)
+  if (nbulk >= 1) {
+    if (CAUSAL && tD == 0) mask_diag(SA);  // tile 0 is the wave's diagonal: the reference over visible keys
     float nmc[2];
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
@@ -289,27 +314,37 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
     }
 
     // iteration t: S(t) in SC with P(t) keys 0-31 in PC; K(t + 1) in slot (t + 1) & 1, V(t) in
-    // slot t & 1; stages K(t + 2) into slot t & 1 and V(t + 1) into slot (t + 1) & 1.
-    auto iter = [&](int t, int par, const Sc& SC, Sc& SN, const Pf& PC, Pf& PN) __attribute__((always_inline)) {
+    // slot t & 1; stages K(t + 2) into slot t & 1 and V(t + 1) into slot (t + 1) & 1. MASK:
+    // S(t + 1) is the wave's diagonal tile, masked before its first exponentials (P3).
+    auto iter = [&](int t, int par, const Sc& SC, Sc& SN, const Pf& PC, Pf& PN, bool mask) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
       dma_k(par, (t + 2) * ktile_b);
       dma_v(par ^ 1, (t + 1) * vtile_b);
       const bf16* skn_ = sK + (par ^ 1) * TILE;
       const bf16* svc = sV + par * TILE;
-      qk_phase<true, VS>(skn_, ko, qf, SN, 0, SC, 2, c2, nmc, ph, acc);    // P1
-      qk_phase<true, VS>(skn_, ko, qf, SN, 2, SC, 3, c2, nmc, ph, acc);    // P2
-      pv_phase<true, VS>(svc, vo, O, PC, 0, R, SN, 0, c2, nmc, PN, acc);   // P3
-      pv_phase<true, VS>(svc, vo, O, ph, 1, R, SN, 1, c2, nmc, PN, acc);   // P4
+      qk_phase<true, VS, AH>(skn_, ko, qf, SN, 0, SC, 2, c2, nmc, ph, acc);    // P1
+      qk_phase<true, VS, AH>(skn_, ko, qf, SN, 2, SC, 3, c2, nmc, ph, acc);    // P2
+      if (CAUSAL && mask) mask_diag(SN);
+      pv_phase<true, VS, AH>(svc, vo, O, PC, 0, R, SN, 0, c2, nmc, PN, acc);   // P3
+      pv_phase<true, VS, AH>(svc, vo, O, ph, 1, R, SN, 1, c2, nmc, PN, acc);   // P4
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     };
+    // iterations 0 .. nbulk - 2 (causal: the last computes QKᵀ of the diagonal tile)
+    const int L = nbulk - 1, Lu = CAUSAL ? L - 1 : L;
     int t = 0;
-    for (; t + 2 < ntiles; t += 2) {
-      iter(t, 0, SA, SB, pl0, pl1);
-      iter(t + 1, 1, SB, SA, pl1, pl0);
+    for (; t + 2 <= Lu; t += 2) {
+      iter(t, 0, SA, SB, pl0, pl1, false);
+      iter(t + 1, 1, SB, SA, pl1, pl0, false);
     }
-    if (t + 1 < ntiles) {
-      iter(t, 0, SA, SB, pl0, pl1);
+    if (t < Lu) {
+      iter(t, 0, SA, SB, pl0, pl1, false);
+      ++t;
+      SA = SB;
+      pl0 = pl1;
+    }
+    if (CAUSAL && t < L) {  // runtime slot parity
+      iter(t, t & 1, SA, SB, pl0, pl1, true);
       ++t;
       SA = SB;
       pl0 = pl1;
@@ -332,10 +367,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
     l[0] = R[0][0];
     l[1] = R[1][0];
   }
+  if (CAUSAL) {
+    // tail: this wave's share of the staging of the tiles the other waves still need
+    for (int t = nbulk > 0 ? nbulk - 1 : 0; t + 1 < ntiles; ++t) {
+      dma_k(t & 1, (t + 2) * ktile_b);
+      dma_v((t + 1) & 1, (t + 1) * vtile_b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
 
   // ---- serial path: every tile again with the per-tile deferred-max bookkeeping, when a
   // row sum left 2^64 (the workgroup starts over) ----------------------------------------
-  const bool bad = !(l[0] <= kLimit) || !(l[1] <= kLimit);
+  const bool bad = nbulk > 0 && (!(l[0] <= kLimit) || !(l[1] <= kLimit));
   if (__syncthreads_or(bad)) {
     zero_o();
     f32x2 acc[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
@@ -347,11 +391,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
       dma_v(0, t * vtile_b);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (t >= nbulk) continue;  // causal: past this wave's diagonal (or its queries past N)
       Sc S;
-      Pf plo, phi, dpf;
+      Pf plo, phi, dpf2;
       const float z[2] = {0.f, 0.f};
-      qk_phase<false>(sK, ko, qf, S, 0, S, 0, c2, z, dpf);
-      qk_phase<false>(sK, ko, qf, S, 2, S, 0, c2, z, dpf);
+      qk_phase<false>(sK, ko, qf, S, 0, S, 0, c2, z, dpf2);
+      qk_phase<false>(sK, ko, qf, S, 2, S, 0, c2, z, dpf2);
+      if (CAUSAL && t == tD) mask_diag(S);
       float nmc[2];
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) {
@@ -375,8 +421,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
           fin_pair(e, kb, j, kb < 2 ? plo : phi);
         }
       f32x4 dR[2] = {f32x4{}, f32x4{}};
-      pv_phase<false>(sV, vo, O, plo, 0, dR, S, 0, c2, nmc, dpf);
-      pv_phase<false>(sV, vo, O, phi, 1, dR, S, 0, c2, nmc, dpf);
+      pv_phase<false>(sV, vo, O, plo, 0, dR, S, 0, c2, nmc, dpf2);
+      pv_phase<false>(sV, vo, O, phi, 1, dR, S, 0, c2, nmc, dpf2);
     }
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) l[qh] = quad_sum(acc[qh][0] + acc[qh][1]);
@@ -400,6 +446,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
       }
     }
   }
+  };  // run_block
+
+  if (CAUSAL) {  // the light query block first, then the heavy one of the same head
+    const int heavy = nqb - 1 - qb;
+    run_block(qb * kBQ);
+    if (heavy != qb) {
+      __syncthreads();  // every wave is done with the light block's LDS tiles
+      run_block(heavy * kBQ);
+    }
+  } else {
+    run_block(qb * kBQ);
+  }
 }
 
 template <int NW, int VAR>
@@ -409,7 +467,7 @@ static hipError_t launch_v2_t(const AttnArgs& a, hipStream_t st) {
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
   const int nqb = (a.N + 32 * NW - 1) / (32 * NW);
-  const int64_t nblk = (int64_t)nqb * a.B * a.H;
+  const int64_t nblk = (int64_t)((VAR & 32) ? (nqb + 1) / 2 : nqb) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(64 * NW), smem, st, a, nqb);
   return hipGetLastError();
@@ -420,18 +478,21 @@ static hipError_t launch_v2_t(const AttnArgs& a, hipStream_t st) {
 // 0-1 the kernel's VAR.
 hipError_t launch_fwd_d128v2(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled) {
   *handled = false;
-  if (causal || a.d != D || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
+  if (causal != ((var & 32) != 0) || a.d != D || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
-  switch (var) {
+  switch (var) {  // product build: the defaults 0 / 32; the rest are A/B policies
     case 0: return launch_v2_t<8, 0>(a, st);
+    case 32: return launch_v2_t<8, 32>(a, st);
 #ifdef MT_DIAGNOSTICS
     case 1: return launch_v2_t<8, 1>(a, st);
     case 2: return launch_v2_t<8, 2>(a, st);
     case 16: return launch_v2_t<4, 0>(a, st);
     case 17: return launch_v2_t<4, 1>(a, st);
+    case 4: return launch_v2_t<8, 4>(a, st);
+    case 8: return launch_v2_t<8, 8>(a, st);
 #endif
     default: return hipErrorInvalidValue;
   }

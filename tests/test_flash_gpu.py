@@ -330,7 +330,7 @@ def test_config3_bf16_full_size(torch_dev, causal, parity_record):
     ((1, 4, 1024, 64), False, True),   # small grid: v5 with the keys split
     ((2, 4, 2048, 64), True, True),    # v6 causal
     ((1, 2, 256, 128), False, True),   # d = 128 non-causal: the 16x16x32 kernel writes either O
-    ((1, 2, 256, 128), True, False),   # d = 128 causal: the fp32 O takes the generic kernels
+    ((1, 2, 256, 128), True, True),    # d = 128 causal: the same kernel (paired form)
     ((1, 2, 100, 32), True, True),     # d = 32: generic
 ])
 def test_fp32_out_option(torch_dev, shape, causal, same_kernel):
@@ -480,7 +480,7 @@ def test_v5_split_keys_vs_oracle(torch_dev, policy, parity_record):
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
-@pytest.mark.parametrize("policy", _shipped([0, 130, 131, 132, 133, 134]))
+@pytest.mark.parametrize("policy", _shipped([0, 130, 131, 132, 133, 134, 135, 136]))
 def test_d128_vs_oracle(torch_dev, policy, parity_record):
     """The d = 128 non-causal forward (the default and policy 130, the 16x16x32 kernel with
     LDS-DMA staging and MFMA row sums): every head, every row against the C oracle at the
@@ -510,6 +510,39 @@ def test_d128_vs_oracle(torch_dev, policy, parity_record):
     finally:
         _hip.set_policy(0)
     parity_record("test_d128_vs_oracle", f"policy {policy}", max_err_over_bound=worst,
+                  bound="1e-3 + 2^-7 * (P|V|) elementwise")
+
+
+@pytest.mark.parametrize("policy", _shipped([0, 137]))
+def test_d128_causal_vs_oracle(torch_dev, policy, parity_record):
+    """The d = 128 causal forward (the default and policy 137, the 16x16x32 kernel's paired
+    light / heavy form with each wave's masked diagonal tile): every head, every row against
+    the C oracle at the elementwise causal bound. Shapes: the smallest (N = 128: the wave of
+    queries 0-31 has only its diagonal tile), three tiles, a partial last query block, an even
+    and an odd number of query blocks (N = 2304: the middle block runs alone), and a large score
+    on a diagonal."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(137)
+    worst = 0.0
+    try:
+        _use_policy(_hip, policy)
+        for (B, H, N) in ((1, 2, 128), (1, 1, 192), (1, 2, 320), (2, 3, 1024), (1, 1, 2304)):
+            q, k, v = (A.bf16_round(rng.standard_normal((B, H, N, 128)).astype(np.float32))
+                       for _ in range(3))
+            k[0, 0, 70] = A.bf16_round(q[0, 0, 70] * 0.5)  # a large score on the diagonal
+            o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), True)
+            torch.cuda.synchronize()
+            o_ref, m_ref, l_ref = cref.attn_fwd(q.reshape(B * H, N, 128), k.reshape(B * H, N, 128),
+                                                v.reshape(B * H, N, 128), True)
+            err = np.abs(_np(o) - o_ref.reshape(B, H, N, 128))
+            bound = 1e-3 + 2.0 ** -7 * _pv_abs(q, k, v, causal=True)
+            assert np.all(err <= bound), f"{(B, H, N)}: max err/bound {float((err / bound).max()):.3f}"
+            _check_ml(_np(m), _np(l), m_ref.reshape(B, H, N), l_ref.reshape(B, H, N), exact=False)
+            worst = max(worst, float((err / bound).max()))
+    finally:
+        _hip.set_policy(0)
+    parity_record("test_d128_causal_vs_oracle", f"policy {policy}", max_err_over_bound=worst,
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
@@ -569,7 +602,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # computes the same attention.
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
                  44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
-                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106, 130, 131, 132, 133, 134)
+                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106, 130, 131, 132, 133, 134, 135, 136, 137)
 
 
 @pytest.mark.parametrize("policy", _shipped(FAST_POLICIES))
