@@ -119,7 +119,10 @@ enum : int {
   // 135 / 136 = 130 with the operand reads 3 / 4 fragments ahead
   kPolD128v2 = 130, kPolD128v2Vs = 131, kPolD128v2Prio = 132, kPolD128v2w4 = 133, kPolD128v2w4Vs = 134,
   kPolD128v2Ah3 = 135, kPolD128v2Ah4 = 136,
-  kPolD128v2Causal = 137,  // the causal form (paired light / heavy query blocks, per-wave diagonal)
+  kPolD128v2Causal = 137,
+  // v6 with the widened (16-B) epilogue stores: 140 = 102 (non-causal), 141 = 105 (split keys),
+  // 142 = 106 (causal)
+  kPolV6Wide = 140, kPolV6SplitWide = 141, kPolV6CausalWide = 142,  // the causal form (paired light / heavy query blocks, per-wave diagonal)
 };
 static const int kProductPolicies[] = {kPolDefault, kPolGeneric, kPolBwdFused, kPolBwdSplit};
 #ifdef MT_DIAGNOSTICS
@@ -131,7 +134,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal, kPolV6Wide, kPolV6SplitWide, kPolV6CausalWide};
 #endif
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
@@ -239,6 +242,11 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     case kPolV6RowSumNoKeep: e = launch_fwd_v6(a, causal, 6, st, handled); break;
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
     case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
+    case kPolV6Wide: e = launch_fwd_v6(a, causal, 66, st, handled); break;
+    case kPolV6SplitWide: e = launch_fwd_v6(a, causal, 82, st, handled); break;
+    case kPolV6CausalWide:
+      if (causal) e = launch_fwd_v6(a, true, 98, st, handled);
+      break;
     case kPolV6Causal:
       if (causal) e = launch_fwd_v6(a, true, 34, st, handled);
       break;
@@ -264,7 +272,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     // MFMA, which the chip clocks higher) with the row sums on the MFMA pipe (policy 102:
     // 1129 vs 1089 TF/s for v5 at C3, 1169 vs 1111 at (1,16,8192,64), profiles/r2_ab_v6.txt).
     // Shapes it does not take (N % 64 != 0, N < 128) fall through to v5 / v4.
-    e = launch_fwd_v6(a, false, 2, st, handled);
+    e = launch_fwd_v6(a, false, 66, st, handled);
   else if (!causal && !*handled && pol == kPolDefault && a.d == 64 &&
            (int64_t)((N + 255) / 256) * a.B * a.H >= 256)
     // fewer 8-wave workgroups than CUs, but at least one per CU once the keys are split
@@ -338,7 +346,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     // policy 106): 1137 vs 1084 TF/s at (1,16,16384,64), even at C3 causal (980 vs 981,
     // profiles/r2_ab_v6.txt); v5 stays for the shapes v6 does not take.
   {
-    e = launch_fwd_v6(a, true, 34, st, handled);
+    e = launch_fwd_v6(a, true, 98, st, handled);
     if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
   }
   if (!*handled && pol == kPolDefault && a.d == 64)
@@ -398,11 +406,13 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
   const int64_t bh = (int64_t)a.B * a.H;
   if (a.d == 64) {
     if (!causal) {
-      // v6 (v5's schedule on the 16x16x32 MFMA, row sums on the MFMA pipe, policy 102) with
-      // at least one 8-wave workgroup per CU; with the keys split between the workgroup
-      // halves (policy 105) at one 256-query workgroup per CU (the 8-GPU C3 shard)
+      // v6 (v5's schedule on the 16x16x32 MFMA, row sums on the MFMA pipe, 16-B epilogue
+      // stores: policy 140, 102 with the widened stores, profiles/r3_ab_v6_wide.txt) with at
+      // least one 8-wave workgroup per CU; with the keys split between the workgroup halves
+      // (policy 105; its widened form 141 spills: -2.6 %) at one 256-query workgroup per CU
+      // (the 8-GPU C3 shard)
       if ((int64_t)((N + 511) / 512) * bh >= 256)
-        e = launch_fwd_v6(a, false, 2, st, handled);
+        e = launch_fwd_v6(a, false, 66, st, handled);
       else if ((int64_t)((N + 255) / 256) * bh >= 256)
         e = launch_fwd_v6(a, false, 18, st, handled);
       if (!*handled) {
@@ -416,8 +426,9 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       }
     } else if ((int64_t)((N + 511) / 512 + 1) / 2 * bh >= 256) {
       // causal with at least one 8-wave workgroup per CU: paired light / heavy query blocks
-      // with each wave's diagonal inside the pipeline, v6 (policy 106), else v5 (67)
-      e = launch_fwd_v6(a, true, 34, st, handled);
+      // with each wave's diagonal inside the pipeline, v6 with the widened epilogue stores
+      // (policy 142: +1.8 % over 106, r3_ab_v6_wide.txt), else v5 (67)
+      e = launch_fwd_v6(a, true, 98, st, handled);
       if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
     }
     // ragged N, short N, small causal grids: v4 (causal: paired, light block first, 8 waves

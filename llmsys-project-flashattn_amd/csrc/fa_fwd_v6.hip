@@ -222,6 +222,7 @@ __device__ __forceinline__ void dma6(uint32_t lds, __amdgpu_buffer_rsrc_t rs, in
 template <int VAR>
 __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nqb) {
   constexpr bool PS = VAR & 1, RS = VAR & 2, EV = RS && (VAR & 8), SPLIT = VAR & 16, CAUSAL = VAR & 32;
+  constexpr bool WIDE = VAR & 64;  // 16-B epilogue stores (T21)
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
   constexpr int NWQ = SPLIT ? 4 : kNW;  // waves sharing one query block and its key tiles
@@ -571,12 +572,31 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       const float m = blk ? mB[qh] : mA[qh];
       const float inv = 1.f / l;
       const f32x4(&O)[4][2] = blk ? OB : OA;
+      if (WIDE && !p.o_f32) {
+        // Widened store (cdna_hip_programming.md T21): lane (i, g) holds d 16db + 4g .. + 3;
+        // one v_permlane16_swap per dword pairs the 16-lane rows g, g + 1 (even g keeps d block
+        // 2k and takes its partner's next four d, odd g the same for block 2k + 1), so every
+        // lane stores 16 contiguous bytes: 4 dwordx4 instead of 8 dwordx2 per query half.
+        bf16* Ob = (bf16*)p.out + b * p.so[0] + hh * p.so[1] + (int64_t)min(q, N - 1) * p.so[2];
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const f32x4 &x = O[2 * k][qh], &y = O[2 * k + 1][qh];
+          const uint2 ux = __builtin_bit_cast(uint2, bf16x4{(bf16)(x[0] * inv), (bf16)(x[1] * inv), (bf16)(x[2] * inv), (bf16)(x[3] * inv)});
+          const uint2 uy = __builtin_bit_cast(uint2, bf16x4{(bf16)(y[0] * inv), (bf16)(y[1] * inv), (bf16)(y[2] * inv), (bf16)(y[3] * inv)});
+          const auto rx = __builtin_amdgcn_permlane16_swap(ux.x, uy.x, false, false);
+          const auto ry = __builtin_amdgcn_permlane16_swap(ux.y, uy.y, false, false);
+          if (q < N) *(uint4*)(Ob + 32 * k + 16 * (g & 1) + 4 * (g & 2)) = uint4{rx[0], ry[0], rx[1], ry[1]};
+        }
+      }
       if (q < N) {
         const ORow Og = o_row(p, b, hh, q);
+        if (!WIDE || p.o_f32) {
 #pragma unroll
-        for (int db = 0; db < 4; ++db)
-          store4(Og, 16 * db + 4 * g, O[db][qh][0] * inv, O[db][qh][1] * inv, O[db][qh][2] * inv,
-                 O[db][qh][3] * inv);
+          for (int db = 0; db < 4; ++db)
+            store4(Og, 16 * db + 4 * g, O[db][qh][0] * inv, O[db][qh][1] * inv, O[db][qh][2] * inv,
+                   O[db][qh][3] * inv);
+        }
         if (g == 0) {
           const int64_t row = (int64_t)bh * N + q;
           if (p.m) p.m[row] = m * (PS ? p.scale / c2 : p.scale);
@@ -604,7 +624,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
 // the 31-bit buffer range.
 hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled) {
   *handled = false;
-  const bool split = (var & 16) != 0;
+  const bool split = (var & 16) != 0;  // (var & 64: the widened epilogue stores)
   if (causal != ((var & 32) != 0) || a.d != 64 || a.N % kBK != 0 || a.N < 2 * kBK) return hipSuccess;
   if (split && (a.N % (2 * kBK) != 0 || a.N < 4 * kBK)) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
@@ -613,11 +633,14 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   *handled = true;
   const size_t smem = (size_t)(split ? 2 : 1) * (kKSlots + kVSlots) * TILE * sizeof(bf16);
   void (*kern)(AttnArgs, int) = nullptr;
-  switch (var) {  // product build: the defaults 2 / 18 / 34; the rest are A/B policies
-    case 2: kern = fa_fwd_bf16_v6<2>; break;
+  switch (var) {  // product build: the defaults 66 / 18 / 98; the rest are A/B policies
+    case 66: kern = fa_fwd_bf16_v6<66>; break;
     case 18: kern = fa_fwd_bf16_v6<18>; break;
-    case 34: kern = fa_fwd_bf16_v6<34>; break;
+    case 98: kern = fa_fwd_bf16_v6<98>; break;
 #ifdef MT_DIAGNOSTICS
+    case 2: kern = fa_fwd_bf16_v6<2>; break;
+    case 34: kern = fa_fwd_bf16_v6<34>; break;
+    case 82: kern = fa_fwd_bf16_v6<82>; break;
     case 0: kern = fa_fwd_bf16_v6<0>; break;
     case 6: kern = fa_fwd_bf16_v6<6>; break;
     case 10: kern = fa_fwd_bf16_v6<10>; break;

@@ -410,7 +410,7 @@ def test_long_causal_paired_default(torch_dev, d):
     _subset_check_fwd(torch, q, k, v, o, True, [(0, 0), (0, 2)], 1e-3, 2.0 ** -7)
 
 
-@pytest.mark.parametrize("policy", _shipped([0, 67, 68, 106]))
+@pytest.mark.parametrize("policy", _shipped([0, 67, 68, 106, 142]))
 def test_v5_causal_pairs_vs_oracle(torch_dev, policy, parity_record):
     """The v5 causal form (paired light/heavy query blocks per workgroup, each wave's
     pipelined loop ending on its own masked diagonal tile, finished waves staging for the
@@ -444,7 +444,7 @@ def test_v5_causal_pairs_vs_oracle(torch_dev, policy, parity_record):
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
-@pytest.mark.parametrize("policy", _shipped([0, 76, 100, 102, 103, 105]))
+@pytest.mark.parametrize("policy", _shipped([0, 76, 100, 102, 103, 105, 140, 141]))
 def test_v5_split_keys_vs_oracle(torch_dev, policy, parity_record):
     """v5 with the keys split between the two halves of an 8-wave workgroup (policy 76; the
     default for grids of fewer 8-wave workgroups than CUs): every head, every row against
@@ -602,7 +602,8 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 # computes the same attention.
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
                  44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
-                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106, 130, 131, 132, 133, 134, 135, 136, 137)
+                 67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106, 130, 131, 132, 133, 134, 135, 136, 137,
+                 140, 141, 142)
 
 
 @pytest.mark.parametrize("policy", _shipped(FAST_POLICIES))
