@@ -146,7 +146,7 @@ static bool policy_valid(int p) {
     if (v == p) return true;
   // wrong-result ablations (timing only): v5 80-86 / 97 / 98, v4 91-96, fast 10-15, bwd 87-90;
   // 101 v6 with Q pre-scaled (reduced precision)
-  if ((p >= 80 && p <= 98) || p == 101 || (p >= 10 && p <= 15)) return true;
+  if ((p >= 80 && p <= 98) || p == 101 || (p >= 10 && p <= 15) || p == 150 || p == 151 || p == 152) return true;
 #endif
   return false;
 }
@@ -253,6 +253,15 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
 #ifdef MT_DIAGNOSTICS
     case 101: e = launch_fwd_v6(a, causal, 1, st, handled); break;  // reduced precision (timing)
 #endif
+    case 150:  // wrong results possible (timing only): d128 v2 without the staging wait
+      e = launch_fwd_d128v2(a, causal, 128, st, handled);
+      break;
+    case 151:  // wrong results (timing only): d128 v2 without the tile barrier
+      e = launch_fwd_d128v2(a, causal, 256, st, handled);
+      break;
+    case 152:  // wrong results (timing only): the v6 default without the tile barrier
+      e = launch_fwd_v6(a, causal, 194, st, handled);
+      break;
     case kPolD128v2: case kPolD128v2Vs: case kPolD128v2Prio: case kPolD128v2w4: case kPolD128v2w4Vs:
     case kPolD128v2Ah3: case kPolD128v2Ah4: case kPolD128v2Causal: {
       static const int kVar[8] = {0, 1, 2, 16, 17, 4, 8, 32};

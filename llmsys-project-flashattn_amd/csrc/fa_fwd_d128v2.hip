@@ -185,6 +185,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
   constexpr int kBQ = 32 * NW;
   constexpr int LPT = TILE * 2 / 1024 / NW;  // 1-KiB LDS-DMA pieces per wave per tile and tensor
   constexpr bool VS = VAR & 1, CAUSAL = VAR & 32;
+  // VAR 128 (diagnostics, timing only, may read stale tiles): no staging wait before the tile
+  // barrier (what the DMA latency costs); VAR 256 (the same, racy): no tile barrier
   constexpr int AH = (VAR & 4) ? 3 : (VAR & 8) ? 4 : 2;  // operand fragments read ahead
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* const sK = (bf16*)smem_raw;  // [2][TILE]
@@ -327,8 +329,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_bf16_d128v2(AttnArgs p
       if (CAUSAL && mask) mask_diag(SN);
       pv_phase<true, VS, AH>(svc, vo, O, PC, 0, R, SN, 0, c2, nmc, PN, acc);   // P3
       pv_phase<true, VS, AH>(svc, vo, O, ph, 1, R, SN, 1, c2, nmc, PN, acc);   // P4
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if (!(VAR & 128)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!(VAR & 256)) __syncthreads();
     };
     // iterations 0 .. nbulk - 2 (causal: the last computes QKᵀ of the diagonal tile)
     const int L = nbulk - 1, Lu = CAUSAL ? L - 1 : L;
@@ -493,6 +495,8 @@ hipError_t launch_fwd_d128v2(const AttnArgs& a, bool causal, int var, hipStream_
     case 17: return launch_v2_t<4, 1>(a, st);
     case 4: return launch_v2_t<8, 4>(a, st);
     case 8: return launch_v2_t<8, 8>(a, st);
+    case 128: return launch_v2_t<8, 128>(a, st);
+    case 256: return launch_v2_t<8, 256>(a, st);
 #endif
     default: return hipErrorInvalidValue;
   }

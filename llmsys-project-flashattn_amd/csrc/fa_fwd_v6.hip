@@ -223,6 +223,7 @@ template <int VAR>
 __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nqb) {
   constexpr bool PS = VAR & 1, RS = VAR & 2, EV = RS && (VAR & 8), SPLIT = VAR & 16, CAUSAL = VAR & 32;
   constexpr bool WIDE = VAR & 64;  // 16-B epilogue stores (T21)
+  constexpr bool NOBAR = VAR & 128;  // diagnostics, timing only, racy: no tile barrier in the bulk loop
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
   constexpr int NWQ = SPLIT ? 4 : kNW;  // waves sharing one query block and its key tiles
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       qk6<true, PS, RS, EV>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
       pv6<true, K2, PS, RS, EV>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if (!NOBAR) __syncthreads();
     };
     int t = 0;
     for (; t + 4 < nbulk; t += 4) {
@@ -638,6 +639,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 18: kern = fa_fwd_bf16_v6<18>; break;
     case 98: kern = fa_fwd_bf16_v6<98>; break;
 #ifdef MT_DIAGNOSTICS
+    case 194: kern = fa_fwd_bf16_v6<194>; break;
     case 2: kern = fa_fwd_bf16_v6<2>; break;
     case 34: kern = fa_fwd_bf16_v6<34>; break;
     case 82: kern = fa_fwd_bf16_v6<82>; break;
