@@ -30,28 +30,31 @@ using namespace bwdbf16;
 // rows per lane group (all loads issued first: with one row per 32-row workgroup the
 // C3 prep ran 16384 tiny workgroups at ≈2.2 TB/s).
 constexpr int kPrepRows = 4;
+// grid (ceil(N / (32 kPrepRows)), B·H): the head from blockIdx.y, no 64-bit division per row
+// (the 1-D form divided each row index by N and H)
 __global__ __launch_bounds__(256) void fa_bwd_prep_bf16(AttnArgs p) {
-  const int64_t rows = (int64_t)p.B * p.H * p.N;
-  const int64_t row0 = (int64_t)blockIdx.x * 32 * kPrepRows + (threadIdx.x >> 3);
+  const int bh = blockIdx.y;
+  const int b = bh / p.H, hh = bh % p.H;
+  const int n0 = blockIdx.x * 32 * kPrepRows + (threadIdx.x >> 3);
   const int sub = threadIdx.x & 7;
+  const int64_t row0 = (int64_t)bh * p.N;
+  const bf16* O = (const bf16*)p.o + b * p.so[0] + hh * p.so[1] + 8 * sub;
+  const bf16* dO = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + 8 * sub;
   bf16x8 o[kPrepRows], g[kPrepRows];
   float mm[kPrepRows], ll[kPrepRows];
 #pragma unroll
   for (int u = 0; u < kPrepRows; ++u) {
-    const int64_t row = row0 + 32 * u;
+    const int n = n0 + 32 * u;
     o[u] = bf16x8{};
     g[u] = bf16x8{};
     mm[u] = 0.f;
     ll[u] = 1.f;
-    if (row < rows) {
-      const int n = (int)(row % p.N);
-      const int64_t bh = row / p.N;
-      const int b = (int)(bh / p.H), hh = (int)(bh % p.H);
-      o[u] = *(const bf16x8*)((const bf16*)p.o + b * p.so[0] + hh * p.so[1] + (int64_t)n * p.so[2] + 8 * sub);
-      g[u] = *(const bf16x8*)((const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + (int64_t)n * p.sdo[2] + 8 * sub);
+    if (n < p.N) {
+      o[u] = *(const bf16x8*)(O + (int64_t)n * p.so[2]);
+      g[u] = *(const bf16x8*)(dO + (int64_t)n * p.sdo[2]);
       if (sub == 0) {
-        mm[u] = p.m[row];
-        ll[u] = p.l[row];
+        mm[u] = p.m[row0 + n];
+        ll[u] = p.l[row0 + n];
       }
     }
   }
@@ -63,10 +66,10 @@ __global__ __launch_bounds__(256) void fa_bwd_prep_bf16(AttnArgs p) {
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
     acc += __shfl_xor(acc, 4);
-    const int64_t row = row0 + 32 * u;
-    if (row < rows && sub == 0) {
-      p.delta[row] = -acc;
-      p.lse2[row] = -(mm[u] * kLog2e + log2f(ll[u])) / p.scale_log2;
+    const int n = n0 + 32 * u;
+    if (n < p.N && sub == 0) {
+      p.delta[row0 + n] = -acc;
+      p.lse2[row0 + n] = -(mm[u] * kLog2e + log2f(ll[u])) / p.scale_log2;
     }
   }
 }
@@ -1086,7 +1089,9 @@ template <bool CAUSAL>
 static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t st) {
   // (variant is adjusted below for shapes a form does not take)
   const int64_t rows = (int64_t)a.B * a.H * a.N;
-  hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((rows + 32 * kPrepRows - 1) / (32 * kPrepRows))), dim3(256), 0, st, a);
+  (void)rows;
+  hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((a.N + 32 * kPrepRows - 1) / (32 * kPrepRows)), (unsigned)(a.B * a.H)),
+                     dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // 20: dQ folded into the dK/dV pass (fa_bwd_fused.hip: 5 products instead of 7)
@@ -1178,6 +1183,7 @@ hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStrea
   const int64_t lim = (int64_t)1 << 31;
   for (const int64_t s : {a.sq[2], a.sk[2], a.sv[2], a.sdo[2]})
     if (((int64_t)a.N + 64) * s * 2 >= lim) return hipSuccess;
+  if ((int64_t)a.B * a.H > 65535) return hipSuccess;  // the prep kernel's grid.y
   *handled = true;
   return causal ? launch_bwd_bf16_t<true>(a, variant, st) : launch_bwd_bf16_t<false>(a, variant, st);
 }

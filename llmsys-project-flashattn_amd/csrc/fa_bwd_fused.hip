@@ -437,7 +437,16 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, const bf16* 
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i] = 0.f;
   int k = 0;
-  for (; k + 4 <= nk; k += 4) {  // four 16-B loads in flight per lane
+  for (; k + 8 <= nk; k += 8) {  // eight 16-B loads in flight per lane (the sum order is unchanged)
+    bf16x8 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = __builtin_nontemporal_load((const bf16x8*)(src + (int64_t)(k + u) * 4096));
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] += (float)x[u][i];
+  }
+  for (; k + 4 <= nk; k += 4) {
     bf16x8 x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load((const bf16x8*)(src + (int64_t)(k + u) * 4096));
