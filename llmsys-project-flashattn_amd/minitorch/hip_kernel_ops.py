@@ -29,7 +29,7 @@ import numpy as np
 from . import _hip
 from . import operators
 from .tensor import Tensor
-from .tensor_data import TensorData, shape_broadcast
+from .tensor_data import TensorData, _prod, shape_broadcast
 from .tensor_ops import MapProto, TensorOps
 
 
@@ -50,11 +50,8 @@ def _i64(vals) -> ctypes.Array:
 def _out(like: Tensor, shape) -> Tensor:
     """Uninitialised dense fp32 device output (every kernel below writes all of it)."""
     import torch
-    shape = tuple(int(s) for s in shape)
-    size = 1
-    for s in shape:
-        size *= s
-    st = torch.empty(size, dtype=torch.float32, device="cuda")
+    shape = tuple(map(int, shape))
+    st = torch.empty(_prod(shape), dtype=torch.float32, device="cuda")
     return Tensor(TensorData(st, shape), backend=like.backend)
 
 

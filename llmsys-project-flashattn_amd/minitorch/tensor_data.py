@@ -48,25 +48,44 @@ def broadcast_index(big_index: Index, big_shape: Shape, shape: Shape, out_index:
         out_index[d] = 0 if shape[d] == 1 else big_index[d + off]
 
 
-def shape_broadcast(shape1: UserShape, shape2: UserShape) -> Tuple[int, ...]:
-    a, b = list(shape1), list(shape2)
+@functools.lru_cache(maxsize=4096)
+def _shape_broadcast(a: Tuple[int, ...], b: Tuple[int, ...]) -> Tuple[int, ...]:
     n = max(len(a), len(b))
-    a = [1] * (n - len(a)) + a
-    b = [1] * (n - len(b)) + b
+    a = (1,) * (n - len(a)) + a
+    b = (1,) * (n - len(b)) + b
     out = []
     for x, y in zip(a, b):
         if x != y and x != 1 and y != 1:
-            raise IndexingError(f"Cannot broadcast {tuple(shape1)} and {tuple(shape2)}")
+            raise IndexingError(f"Cannot broadcast {a} and {b}")
         out.append(max(x, y))
     return tuple(out)
 
 
-def strides_from_shape(shape: UserShape) -> Tuple[int, ...]:
+def shape_broadcast(shape1: UserShape, shape2: UserShape) -> Tuple[int, ...]:
+    # memoised on the int tuples: a model step broadcasts the same few shape pairs hundreds
+    # of times (host time of the config-5 step)
+    return _shape_broadcast(tuple(map(int, shape1)), tuple(map(int, shape2)))
+
+
+@functools.lru_cache(maxsize=4096)
+def _strides_from_shape(shape: Tuple[int, ...]) -> Tuple[int, ...]:
     out, acc = [], 1
-    for s in reversed(list(shape)):
+    for s in reversed(shape):
         out.append(acc)
-        acc *= int(s)
+        acc *= s
     return tuple(reversed(out))
+
+
+def strides_from_shape(shape: UserShape) -> Tuple[int, ...]:
+    return _strides_from_shape(tuple(map(int, shape)))
+
+
+@functools.lru_cache(maxsize=4096)
+def _prod(shape: Tuple[int, ...]) -> int:
+    size = 1
+    for s in shape:
+        size *= s
+    return size
 
 
 def _is_device(storage) -> bool:
@@ -83,19 +102,14 @@ class TensorData:
             self._storage = np.array(storage, dtype=datatype).reshape(-1)
         else:  # device storage (torch tensor)
             self._storage = storage
-        shape = tuple(int(s) for s in shape)
-        if strides is None:
-            strides = strides_from_shape(shape)
-        strides = tuple(int(s) for s in strides)
+        shape = tuple(map(int, shape))
+        strides = _strides_from_shape(shape) if strides is None else tuple(map(int, strides))
         if len(strides) != len(shape):
             raise IndexingError(f"Len of strides {strides} must match {shape}.")
         self.shape = shape
         self.strides = strides
         self.dims = len(shape)
-        size = 1
-        for s in shape:
-            size *= s
-        self.size = size
+        self.size = _prod(shape)
 
     # NumPy forms of shape / strides, built on first use and cached (shape and strides are
     # fixed at construction; the index helpers and the CPU backend take these forms); the
