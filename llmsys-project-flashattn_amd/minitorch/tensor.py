@@ -158,7 +158,7 @@ class Tensor:
 
     def item(self) -> float:
         assert self.size == 1
-        return self._tensor.get(tuple(0 for _ in range(self.dims)))
+        return self._tensor.get((0,) * self.dims)
 
     def sum(self, dim: Optional[int] = None) -> "Tensor":
         if dim is None:

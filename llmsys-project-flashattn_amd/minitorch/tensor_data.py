@@ -183,10 +183,13 @@ class TensorData:
         index = tuple(index)
         if len(index) != self.dims:
             raise IndexingError(f"Index {index} must be size of {self.shape}.")
-        for i, s in zip(index, self.shape):
+        pos = 0
+        for i, s, st in zip(index, self.shape, self.strides):
+            i = int(i)
             if i >= s or i < 0:
                 raise IndexingError(f"Index {index} out of range {self.shape}.")
-        return index_to_position(index, self._strides)
+            pos += i * st
+        return pos
 
     def indices(self) -> Iterable[UserIndex]:
         lshape = self._shape
