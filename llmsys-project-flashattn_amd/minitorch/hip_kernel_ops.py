@@ -157,10 +157,19 @@ class HipKernelOps(TensorOps):
         """Batched a @ b over broadcast leading dims (reference cuda_kernel_ops.py:340-437
         flattens to 3-D the same way)."""
         both_2d = a.dims == 2 and b.dims == 2
+
+        def lift(t: Tensor) -> Tensor:
+            # a 2-D operand as a batch of one over the same storage (a backend op: no autodiff
+            # View, whose shape tensor and Function record cost host time on every matmul)
+            if not t._tensor.is_dense():
+                t = t.contiguous()
+            st = t._tensor.strides
+            return _wrap(t._tensor._storage, (1,) + tuple(t.shape), t.backend, (t.size,) + tuple(st))
+
         if a.dims == 2:
-            a = a.view(1, *a.shape) if a._tensor.is_dense() else a.contiguous().view(1, *a.shape)
+            a = lift(a)
         if b.dims == 2:
-            b = b.view(1, *b.shape) if b._tensor.is_dense() else b.contiguous().view(1, *b.shape)
+            b = lift(b)
         lead = tuple(shape_broadcast(a.shape[:-2], b.shape[:-2]))
         M, K = a.shape[-2], a.shape[-1]
         K2, N = b.shape[-2], b.shape[-1]
@@ -189,7 +198,7 @@ class HipKernelOps(TensorOps):
         _hip.check(_hip.lib().mt_matmul_f32(_ptr(out), _ptr(a), _ptr(b), batch, M, N, K,
                                             _i64(sa), _i64(sb), _i64(so), _stream()), "matmul")
         if both_2d:
-            return out.view(M, N)
+            return _wrap(out._tensor._storage, (M, N), out.backend)
         return out
 
     @staticmethod
