@@ -546,6 +546,32 @@ def test_d128_causal_vs_oracle(torch_dev, policy, parity_record):
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
+@pytest.mark.parametrize("causal", [False, True])
+def test_d128_strided_views(torch_dev, causal):
+    """The d = 128 kernels on Q/K/V/O as permuted views of [B, N, H, d] tensors (row stride
+    H·d: the LDS-DMA source offsets and the buffer ranges use the strides), against the C
+    oracle at the elementwise bound."""
+    from minitorch import _hip
+    torch = torch_dev
+    B, N, H, d = 2, 384, 3, 128
+    rng = np.random.default_rng(384 + int(causal))
+    x = [A.bf16_round(rng.standard_normal((B, N, H, d)).astype(np.float32)) for _ in range(3)]
+    q, k, v = (_dev(torch, a, torch.bfloat16).permute(0, 2, 1, 3) for a in x)
+    o_full = torch.zeros((B, N, H, d), device="cuda", dtype=torch.bfloat16)
+    o = o_full.permute(0, 2, 1, 3)
+    m = torch.empty((B, H, N), device="cuda")
+    l = torch.empty_like(m)
+    _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
+    torch.cuda.synchronize()
+    qh, kh, vh = (a.transpose(0, 2, 1, 3) for a in x)
+    o_ref, m_ref, l_ref = cref.attn_fwd(qh.reshape(B * H, N, d), kh.reshape(B * H, N, d),
+                                        vh.reshape(B * H, N, d), causal)
+    err = np.abs(_np(o) - o_ref.reshape(B, H, N, d))
+    bound = 1e-3 + 2.0 ** -7 * _pv_abs(qh, kh, vh, causal=causal)
+    assert np.all(err <= bound), f"max err/bound {float((err / bound).max()):.3f}"
+    _check_ml(_np(m), _np(l), m_ref.reshape(B, H, N), l_ref.reshape(B, H, N), exact=False)
+
+
 def _pv_abs(q, k, v, causal=True):
     """(P |V|) per element (the O term of tests/bounds.py), from the C oracle run on |V|."""
     B, H, N, d = q.shape
