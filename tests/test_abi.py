@@ -63,6 +63,28 @@ def test_errors_are_reported_not_fatal():
     assert b"dtype" in lib.mt_last_error()
 
 
+@pytest.mark.parametrize("sizes,msg", [
+    ((0, 1, 64, 64), b"bad sizes"),        # empty batch
+    ((1, 0, 64, 64), b"bad sizes"),        # no heads
+    ((1, 1, 0, 64), b"bad sizes"),         # empty sequence
+    ((1, 1, 64, 0), b"bad sizes"),         # zero head dim
+    ((1, 1, 64, 4097), b"out of range"),   # d > 4096
+    ((1, 1, 2 ** 30 + 1, 64), b"out of range"),
+])
+def test_size_validation_before_any_device_call(sizes, msg):
+    """Empty and oversized shapes are refused with a status and a message before the library
+    touches the device (so this runs without a GPU), forward and backward alike."""
+    from minitorch import _hip
+    lib = _hip.lib()
+    for dtype in (0, 1):  # MT_F32, MT_BF16
+        assert lib.mt_flash_attn_fwd(dtype, 0, None, None, None, None, None, None, *sizes,
+                                     None, None, None, None, None) != 0
+        assert msg in lib.mt_last_error()
+        assert lib.mt_flash_attn_bwd(dtype, 1, None, None, None, None, None, None, None, None,
+                                     None, None, *sizes, None, None, None) != 0
+        assert msg in lib.mt_last_error()
+
+
 def test_kernel_policy_switch_rejects_unknown_ids():
     """Only policies that compute the default's attention are selectable: the timing-only
     ablations (wrong results by construction) are not in the product library, and unknown
