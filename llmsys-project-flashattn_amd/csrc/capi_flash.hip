@@ -123,6 +123,9 @@ enum : int {
   // v6 with the widened (16-B) epilogue stores: 140 = 102 (non-causal), 141 = 105 (split keys),
   // 142 = 106 (causal)
   kPolV6Wide = 140, kPolV6SplitWide = 141, kPolV6CausalWide = 142,  // the causal form (paired light / heavy query blocks, per-wave diagonal)
+  // 143 = 142 with two 4-wave halves per workgroup, each walking its own light / heavy pair of
+  // 256-query blocks (N % 1024 == 0)
+  kPolV6CausalDual = 143,
 };
 static const int kProductPolicies[] = {kPolDefault, kPolGeneric, kPolBwdFused, kPolBwdSplit};
 #ifdef MT_DIAGNOSTICS
@@ -134,7 +137,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal, kPolV6Wide, kPolV6SplitWide, kPolV6CausalWide};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal, kPolV6Wide, kPolV6SplitWide, kPolV6CausalWide, kPolV6CausalDual};
 #endif
 static std::atomic<int> g_kernel_policy{kPolDefault};
 
@@ -246,6 +249,9 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     case kPolV6SplitWide: e = launch_fwd_v6(a, causal, 82, st, handled); break;
     case kPolV6CausalWide:
       if (causal) e = launch_fwd_v6(a, true, 98, st, handled);
+      break;
+    case kPolV6CausalDual:
+      if (causal) e = launch_fwd_v6(a, true, 354, st, handled);
       break;
     case kPolV6Causal:
       if (causal) e = launch_fwd_v6(a, true, 34, st, handled);

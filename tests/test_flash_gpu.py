@@ -513,6 +513,43 @@ def test_d128_vs_oracle(torch_dev, policy, parity_record):
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
+@pytest.mark.parametrize("policy", _shipped([0, 142, 143]))
+def test_v6_causal_dual_vs_oracle(torch_dev, policy, parity_record):
+    """The v6 causal forward with two 4-wave halves per workgroup (policy 143: each half walks
+    its own light / heavy pair of 256-query blocks, N % 1024 == 0) against the C oracle at the
+    elementwise causal bound: every head and row, including rows whose score far below the
+    diagonal exceeds the first tile's reference by > 64 log2 units, which send both halves
+    through the serial pass of both their blocks (one spike per workgroup half, one in a light
+    and one in a heavy block)."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(143)
+    worst = 0.0
+    try:
+        _use_policy(_hip, policy)
+        for (B, H, N, spikes) in ((2, 2, 1024, ()), (1, 1, 2048, ((900, 700),)),
+                                  (1, 2, 4096, ((300, 200), (3900, 3000)))):
+            q, k, v = (rng.standard_normal((B, H, N, 64)).astype(np.float32) for _ in range(3))
+            q *= 0.3
+            k *= 0.3
+            for row, key in spikes:
+                k[0, 0, key] = q[0, 0, row] * 150.0
+            q, k, v = (A.bf16_round(x) for x in (q, k, v))
+            o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), True)
+            torch.cuda.synchronize()
+            o_ref, m_ref, l_ref = cref.attn_fwd(q.reshape(B * H, N, 64), k.reshape(B * H, N, 64),
+                                                v.reshape(B * H, N, 64), True)
+            err = np.abs(_np(o) - o_ref.reshape(B, H, N, 64))
+            bound = 1e-3 + 2.0 ** -7 * _pv_abs(q, k, v, causal=True)
+            assert np.all(err <= bound), f"{(B, H, N)}: max err/bound {float((err / bound).max()):.3f}"
+            _check_ml(_np(m), _np(l), m_ref.reshape(B, H, N), l_ref.reshape(B, H, N), exact=False)
+            worst = max(worst, float((err / bound).max()))
+    finally:
+        _hip.set_policy(0)
+    parity_record("test_v6_causal_dual_vs_oracle", f"policy {policy}", max_err_over_bound=worst,
+                  bound="1e-3 + 2^-7 * (P|V|) elementwise")
+
+
 @pytest.mark.parametrize("policy", _shipped([0, 137]))
 def test_d128_causal_vs_oracle(torch_dev, policy, parity_record):
     """The d = 128 causal forward (the default and policy 137, the 16x16x32 kernel's paired
@@ -629,7 +666,7 @@ def test_kernel_variants_agree(torch_dev, causal, d):
 FAST_POLICIES = (0, 3, 2, 4, 5, 6, 21, 22, 23, 24, 25, 26, 27, 28, 29, 31, 32, 35, 36, 37, 38, 39,
                  44, 45, 33, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 61, 63, 64, 65,
                  67, 68, 76, 78, 79, 100, 102, 103, 104, 105, 106, 130, 131, 132, 133, 134, 135, 136, 137,
-                 140, 141, 142)
+                 140, 141, 142, 143)
 
 
 @pytest.mark.parametrize("policy", _shipped(FAST_POLICIES))
