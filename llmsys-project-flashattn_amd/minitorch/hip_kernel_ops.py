@@ -174,7 +174,7 @@ class HipKernelOps(TensorOps):
         M, K = a.shape[-2], a.shape[-1]
         K2, N = b.shape[-2], b.shape[-1]
         assert K == K2, f"matmul shape mismatch {a.shape} @ {b.shape}"
-        batch = int(np.prod(lead)) if lead else 1
+        batch = _prod(lead) if lead else 1
 
         def batch_view(t: Tensor):
             # (batch stride, row stride, col stride); a broadcast operand gets stride 0.
@@ -182,7 +182,7 @@ class HipKernelOps(TensorOps):
                 bs = 0 if t.shape[0] == 1 and batch > 1 else t._tensor.strides[0]
                 return t, (bs, t._tensor.strides[1], t._tensor.strides[2])
             tl = t.shape[:-2]
-            if int(np.prod(tl)) == 1 and batch > 1:
+            if _prod(tuple(tl)) == 1 and batch > 1:
                 return t, (0, t._tensor.strides[-2], t._tensor.strides[-1])
             if tuple(tl) != lead:
                 raise NotImplementedError(f"partial batch broadcast {t.shape} vs {lead}")

@@ -222,15 +222,20 @@ class Tensor:
         if self.shape == other.shape:
             return other
         true_shape = shape_broadcast(self.shape, other.shape)
-        buf = self.zeros(true_shape)
-        self.backend.id_map(other, buf)
-        if self.shape == true_shape:
-            return buf
-        out = buf
+        if self.shape == true_shape or other.shape != true_shape:
+            buf = self.zeros(true_shape)
+            self.backend.id_map(other, buf)
+            if self.shape == true_shape:
+                return buf
+            out = buf
+        else:  # the reductions below read `other` through its strides: no staging copy
+            out = other
         orig_shape = [1] * (len(out.shape) - len(self.shape)) + list(self.shape)
         for dim, s in enumerate(out.shape):
             if orig_shape[dim] == 1 and s != 1:
                 out = self.backend.add_reduce(out, dim)
+        if out is other:  # no reduction ran (only leading size-1 dims differ): a dense copy
+            out = self.backend.id_map(other)
         assert out.size == self.size, f"{out.shape} {self.shape}"
         return Tensor.make(out._tensor._storage, self.shape, backend=self.backend)
 
@@ -248,7 +253,11 @@ class Tensor:
     def accumulate_derivative(self, x: Any) -> None:
         assert self.is_leaf(), "Only leaf variables can have derivatives."
         if self.grad is None:
-            self.grad = self.zeros(self.shape)
+            # the first gradient is copied (0 + x without the zero fill and the add); the copy
+            # keeps the gradient's storage its own, as the optimizer and the bucketed
+            # all-reduce update it in place
+            self.grad = Tensor(self.backend.id_map(x)._tensor, backend=self.backend)
+            return
         self.grad = Tensor(self.backend.add_zip(self.grad, x)._tensor, backend=self.backend)
 
     def is_leaf(self) -> bool:

@@ -16,7 +16,7 @@ import numpy as np
 
 from . import operators
 from .autodiff import Context
-from .tensor_data import TensorData, UserShape, datatype, strides_from_shape
+from .tensor_data import TensorData, UserShape, _prod, datatype, strides_from_shape
 
 
 def wrap_tuple(x: Any) -> tuple:
@@ -397,7 +397,7 @@ def zeros(shape: UserShape, backend=None):
     shape = tuple(int(s) for s in shape)
     if backend.cuda:
         import torch
-        size = int(np.prod(shape)) if shape else 1
+        size = _prod(shape) if shape else 1
         st = torch.zeros(size, dtype=torch.float32, device="cuda")
         return Tensor(TensorData(st, shape), backend=backend)
     t = Tensor.make(np.zeros(int(np.prod(shape)) if shape else 1, dtype=datatype), shape, backend=backend)
