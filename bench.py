@@ -263,7 +263,12 @@ def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2):
                                              / max(tg - wall, 1e-9) / 1e9, 2),
         }
         result["end_to_end"] = serial
-        chunks = args.chunks if args.chunks is not None else (4 if args.config == "c4" else 2)
+        # default: as many chunks (up to 4) as keep each chunk's forward grid at one
+        # workgroup per CU (minitorch/shard.py occupancy_chunks: C3 from 4 ranks up stays
+        # unchunked, C4 at 8 ranks takes 4)
+        from minitorch.shard import occupancy_chunks
+        chunks = args.chunks if args.chunks is not None else occupancy_chunks(
+            B, H, N, d, world, args.causal, max_chunks=4)
         BHg = B * H
         if chunks > 1 and BHg % (world * chunks) == 0:
             from minitorch.shard import chunk_rows
@@ -541,7 +546,8 @@ def parse_args(argv=None):
     ap.add_argument("--policy", type=int, default=0, help="kernel policy (0 default)")
     ap.add_argument("--chunks", type=int, default=None,
                     help="end-to-end leg: chunks of the rank's rows whose all-gather overlaps "
-                         "the next chunk's forward (default 2 for c3, 4 for c4; 1 = serial)")
+                         "the next chunk's forward (default: minitorch.shard.occupancy_chunks, "
+                         "up to 4 while each chunk keeps a workgroup per CU; 1 = serial)")
     ap.add_argument("--shape", type=int, nargs=4, default=None, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 

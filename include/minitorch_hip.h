@@ -68,8 +68,10 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
                              const int64_t* v_strides, const int64_t* o_strides,
                              const int* kv_len, void* stream);
 
-/* Scratch bytes mt_flash_attn_bwd needs: fp32 δ and log2-LSE per row (256-B aligned) and,
- * at d = 64 with N <= 8192, the bf16 dQ partial sums of the fused bf16 backward. */
+/* Scratch bytes the backward needs: fp32 δ and log2-LSE per row (256-B aligned) and, at
+ * d = 64 (N <= 46336), the fused bf16 backward's arrival counters and the dQ partial sums of
+ * one group of heads (at most 1 GiB). The layout changed in ABI version 3: size the workspace
+ * with this function, never by a formula (mt_flash_attn_bwd_v3 checks the size). */
 int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t d);
 
 /* dQ, dK, dV of the forward above, from Q, K, V, O, dO and the forward's (m, l).
@@ -85,6 +87,13 @@ int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k
                              void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
                              int64_t d, const int64_t* strides, const int* kv_len,
                              void* workspace, void* stream);
+/* ABI 3: mt_flash_attn_bwd_varlen (kv_len may be NULL) with the workspace's size in bytes;
+ * returns an error, launching nothing, when it is below mt_flash_attn_bwd_workspace_bytes. */
+int mt_flash_attn_bwd_v3(int dtype, int causal, const void* q, const void* k, const void* v,
+                         const void* o, const void* dout, const float* m, const float* l,
+                         void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
+                         int64_t d, const int64_t* strides, const int* kv_len,
+                         void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ---- FlashAttention, reference-compatible host pointers (fp32) ------------ */
 /* reference src/flashattention_kernel.cu:259 */

@@ -29,7 +29,7 @@ hipError_t launch_fwd_d128v2(const AttnArgs& a, bool causal, int var, hipStream_
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st, int pair, bool ring);
-int64_t bwd_fused_slab_bytes(int64_t B, int64_t H, int64_t N);
+int64_t bwd_fused_ws_bytes(int64_t B, int64_t H, int64_t N);
 #ifdef MT_DIAGNOSTICS
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
@@ -361,7 +361,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     // policy 106): 1137 vs 1084 TF/s at (1,16,16384,64), even at C3 causal (980 vs 981,
     // profiles/r2_ab_v6.txt); v5 stays for the shapes v6 does not take.
   {
-    e = launch_fwd_v6(a, true, 98, st, handled);
+    e = launch_fwd_v6(a, true, a.o_f32 ? 610 : 98, st, handled);
     if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
   }
   if (!*handled && pol == kPolDefault && a.d == 64)
@@ -442,8 +442,10 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
     } else if ((int64_t)((N + 511) / 512 + 1) / 2 * bh >= 256) {
       // causal with at least one 8-wave workgroup per CU: paired light / heavy query blocks
       // with each wave's diagonal inside the pipeline, v6 with the widened epilogue stores
-      // (policy 142: +1.8 % over 106, r3_ab_v6_wide.txt), else v5 (67)
-      e = launch_fwd_v6(a, true, 98, st, handled);
+      // (policy 142: +1.8 % over 106, r3_ab_v6_wide.txt), else v5 (67). An fp32 O
+      // (MT_BF16_F32OUT) takes the fp16-PV form (610): P rounded to 11 bits instead of 8,
+      // within north_star's flat 1e-3 on the causal heads.
+      e = launch_fwd_v6(a, true, a.o_f32 ? 610 : 98, st, handled);
       if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
     }
     // ragged N, short N, small causal grids: v4 (causal: paired, light block first, 8 waves
@@ -478,7 +480,9 @@ int mt_flash_set_kernel_policy(int policy) {
   return 0;
 }
 int mt_flash_get_kernel_policy(void) { return g_kernel_policy.load(std::memory_order_relaxed); }
-int mt_abi_version(void) { return 2; }
+// 3 (round 4): the fused backward's workspace layout changed (arrival counters + a capped
+// slab) and mt_flash_attn_bwd_v3 takes the workspace size
+int mt_abi_version(void) { return 3; }
 
 int mt_flash_attn_fwd(int dtype, int causal, const void* q, const void* k, const void* v,
                       void* o, float* m, float* l, int64_t B, int64_t H, int64_t N, int64_t d,
@@ -537,11 +541,14 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
 }
 
 // The fused bf16 d = 64 backward keeps its dQ partial sums (bf16, N/256 per element) in the
-// workspace; their size grows as N^2, so it runs only up to N = 8192 (C3: 1 GiB).
+// workspace for the last-arriving workgroup of each (head, query step) to sum; a launch's
+// partials are capped at 1 GiB (C3 exactly), longer sequences and larger batches run the pass
+// over groups of heads that reuse the slab, up to N = 46340 (one head's slab within the cap).
 // (the fused kernel stages the row constants lse2 | δ by LDS-DMA from one 32-bit-offset
 // buffer over both arrays: 2·B·H·N floats below 2^31 bytes)
 static bool fused_bwd_applies(int64_t B, int64_t H, int64_t N, int64_t d) {
-  return d == 64 && N <= 8192 && 2 * B * H * N * (int64_t)sizeof(float) < ((int64_t)1 << 31);
+  return d == 64 && bwd_fused_ws_bytes(B, H, N) > 0 &&
+         2 * B * H * N * (int64_t)sizeof(float) < ((int64_t)1 << 31);
 }
 // the fused backward is the bf16 d = 64 default where it applies: C3 1.643 vs 1.872 ms
 // non-causal, 0.991 vs 1.084 ms causal against the split defaults (interleaved A/B on one box,
@@ -552,7 +559,7 @@ static int64_t bwd_rows_bytes(int64_t B, int64_t H, int64_t N) {
 }
 
 int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t d) {
-  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(B, H, N, d) ? bwd_fused_slab_bytes(B, H, N) : 0);
+  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(B, H, N, d) ? bwd_fused_ws_bytes(B, H, N) : 0);
 }
 
 int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const void* v,
@@ -593,11 +600,12 @@ int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k
                           {q, k, v, o, dout, dq, dk, dv});
   const int pol = g_kernel_policy.load(std::memory_order_relaxed);
   // key padding (kv_len): the fused bf16 d = 64 kernel or the generic / ring kernels, which
-  // mask keys >= kv_len[b]
-  if (dtype == MT_BF16 && vec && pol != kPolGeneric && (!kv_len || a.slab)) {
+  // mask keys >= kv_len[b] (the split bf16 kernels do not: policy 121 with kv_len runs the
+  // generic kernels)
+  if (dtype == MT_BF16 && vec && pol != kPolGeneric && (!kv_len || (a.slab && pol != kPolBwdSplit))) {
     bool handled = false;
-    // 20: the fused backward (dQ in the dK/dV pass, fa_bwd_fused.hip), wherever its dQ partial
-    // slab fits the workspace (N <= 8192) and kFusedBwdDefault says so; else the split forms.
+    // 20: the fused backward (dQ in the dK/dV pass, fa_bwd_fused.hip), wherever it applies
+    // (d = 64, N <= 46340) and kFusedBwdDefault says so; else the split forms.
     // the split backward's defaults: dK/dV with 8 waves and LDS-DMA (variant 5, policy 69)
     // non-causal; causal paired light / heavy blocks (18, policy 107: 1.065 vs 1.172 ms at C3
     // causal, profiles/r2m_ab_bwd_pair.txt) once the paired dK/dV grid fills two workgroups
@@ -635,6 +643,20 @@ int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k
                                       pol == kPolBwdGenNoPair ? 0 : pol == kPolBwdGenPair ? 1 : 2,
                                       pol != kPolBwdF32Lds && pol != kPolGeneric),
                    "mt_flash_attn_bwd");
+}
+
+int mt_flash_attn_bwd_v3(int dtype, int causal, const void* q, const void* k, const void* v,
+                         const void* o, const void* dout, const float* m, const float* l,
+                         void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
+                         int64_t d, const int64_t* strides, const int* kv_len,
+                         void* workspace, int64_t workspace_bytes, void* stream) {
+  if (check_sizes(dtype, B, H, N, d)) return 1;
+  const int64_t need = mt_flash_attn_bwd_workspace_bytes(B, H, N, d);
+  if (workspace_bytes < need)
+    return set_error("mt_flash_attn_bwd_v3: workspace of %lld bytes, %lld needed "
+                     "(mt_flash_attn_bwd_workspace_bytes)", (long long)workspace_bytes, (long long)need);
+  return mt_flash_attn_bwd_varlen(dtype, causal, q, k, v, o, dout, m, l, dq, dk, dv, B, H, N, d,
+                                  strides, kv_len, workspace, stream);
 }
 
 // ---- reference-compatible host-pointer wrappers ---------------------------------

@@ -35,6 +35,10 @@ constexpr int kPrepRows = 4;
 __global__ __launch_bounds__(256) void fa_bwd_prep_bf16(AttnArgs p) {
   const int bh = blockIdx.y;
   const int b = bh / p.H, hh = bh % p.H;
+  if (p.dq_cnt && blockIdx.x == 0) {  // the fused backward's arrival counters of this head
+    const int nsa = (p.N + 63) / 64;
+    for (int i = threadIdx.x; i < nsa; i += 256) p.dq_cnt[(int64_t)bh * nsa + i] = 0u;
+  }
   const int n0 = blockIdx.x * 32 * kPrepRows + (threadIdx.x >> 3);
   const int sub = threadIdx.x & 7;
   const int64_t row0 = (int64_t)bh * p.N;
@@ -1079,7 +1083,7 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb
 }
 
 // ---------------------------------------------------------------------------------------
-hipError_t launch_bwd_fused(const AttnArgs& a, bool causal, bf16* slab, hipStream_t st);
+hipError_t launch_bwd_fused(const AttnArgs& a, bool causal, void* ws, hipStream_t st);
 #ifdef MT_DIAGNOSTICS
 hipError_t launch_dkv_w64(const AttnArgs& a, int nkb, unsigned nblk, size_t smem, hipStream_t st);
 hipError_t launch_dq_pipe(const AttnArgs& a, int nqb, unsigned nblk, hipStream_t st);
@@ -1088,14 +1092,15 @@ hipError_t launch_dq_pipe(const AttnArgs& a, int nqb, unsigned nblk, hipStream_t
 template <bool CAUSAL>
 static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t st) {
   // (variant is adjusted below for shapes a form does not take)
-  const int64_t rows = (int64_t)a.B * a.H * a.N;
-  (void)rows;
+  // 20: dQ folded into the dK/dV pass (fa_bwd_fused.hip: 5 products instead of 7); its
+  // workspace (a.slab) starts with the arrival counters, which the prep kernel zeroes
+  AttnArgs ap = a;
+  ap.dq_cnt = variant == 20 ? (unsigned*)a.slab : nullptr;
   hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((a.N + 32 * kPrepRows - 1) / (32 * kPrepRows)), (unsigned)(a.B * a.H)),
-                     dim3(256), 0, st, a);
+                     dim3(256), 0, st, ap);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // 20: dQ folded into the dK/dV pass (fa_bwd_fused.hip: 5 products instead of 7)
-  if (variant == 20) return launch_bwd_fused(a, CAUSAL, (bf16*)a.slab, st);
+  if (variant == 20) return launch_bwd_fused(a, CAUSAL, a.slab, st);
 #ifndef MT_DIAGNOSTICS
   // product build: the split defaults 5 (non-causal), 18 / 0 (causal paired / not); the
   // other forms are A/B policies of the diagnostics build

@@ -21,14 +21,24 @@
 //    read with ds_read_b64_tr_b16;
 //  * the strip is a partial sum over this workgroup's keys: it goes to a bf16 slab
 //    [bh][step][key block][wave][lane][8] in the accumulator's own register order (one 16-B
-//    store per lane), and fa_bwd_dq_reduce sums the key blocks in a fixed order
-//    (deterministic, no atomics) and writes dQ.
+//    store per lane, sc1: written through, not held in this XCD's L2);
+//  * the last workgroup to finish a (head, query step) sums that step's partials and writes
+//    dQ, inside this launch (round 4; round 3 ran a separate reduce kernel over the whole
+//    slab, ≈ 170 µs at C3). The hand-off is MI355X_MICROARCH.md 'Valid forms' row 1: every
+//    storing wave waits for its partial store, the workgroup barrier follows, then one lane
+//    adds 1 to the step's arrival counter (agent scope) and the add's return value names the
+//    last arriver, which reads the partials with sc1 loads. Every sum runs in key-block
+//    order in f32 (deterministic, the round-3 reduce's arithmetic), and no workgroup ever
+//    waits for another (no spin, so no co-residency assumption). The adds are issued a step
+//    late and their return values read a step later still, by when they have long returned;
+//    a workgroup that turns out last for some steps reduces them after its pass (their
+//    partials are then fresh in the Infinity Cache).
 // Why slabs and not float atomics: at 256 keys per workgroup dQ is summed over N/256
 // workgroups, 2.1 GB of f32 adds at C3, whose floor at the chip's ≈1.3 TB/s atomic rate
 // (MI355X_MICROARCH.md, Global float atomics) is 1.65 ms, longer than the whole split
-// backward. The bf16 slabs are 1 GiB written during the pass and read once by the reduce
-// (≈0.17 ms at HBM rate); a bf16 partial adds one rounding of 2^-9 of the partial, inside
-// tests/bounds.py's 2^-7 (three roundings: dS, partial, output).
+// backward. A bf16 partial adds one rounding of 2^-9 of the partial, inside tests/bounds.py's
+// 2^-7 (three roundings: dS, partial, output). The slab of one launch is capped at
+// kSlabCap; longer sequences and bigger batches run the pass over groups of heads.
 //
 // LDS images are single copies read both by rows (ds_read_b128: the A operands of S, dP)
 // and by columns (ds_read_b64_tr_b16: dVᵀ, dKᵀ, dQᵀ), with the chunk swizzle
@@ -37,6 +47,8 @@
 // f flips between rows 4m, 4m+1 and 4m+2, 4m+3 (transposed reads conflict-free); f(r + 8) =
 // f(r) ^ 4, so the transposed read of rows +8 takes its own offset (tlo / thi).
 #include "fa_bwd_bf16.h"
+
+#include <algorithm>
 
 
 namespace mt {
@@ -53,7 +65,12 @@ constexpr int kRingB = 4 * kSub;                    // 2 slots x 2 sub-tiles
 constexpr int kKImgB = kKB * D * 2;                 // K image [256][64]
 constexpr int kDsB = kKB * kStep * 2;               // dS image [256][64]
 constexpr int kSmemFused = kRingB + kKImgB + 2 * kDsB;
-static_assert(kSmemFused <= 160 * 1024, "LDS budget");
+constexpr int kMaxRed = 1024;                       // query steps (of 64) a pass can own: N <= 65536
+constexpr int kSmemAll = kSmemFused + (kMaxRed + 4) * 4;  // + the pass's list of steps to reduce
+static_assert(kSmemAll <= 160 * 1024, "LDS budget");
+constexpr int kSc1 = 16;                            // buffer cache policy bits: sc1
+constexpr int64_t kSlabCap = (int64_t)1 << 30;      // dQ partial bytes per launch (C3: exactly 1 GiB)
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 static_assert(kSub % 16 == 0, "16-B aligned sub-tiles");
 
 __device__ __forceinline__ int swf(int r) {
@@ -215,14 +232,16 @@ __device__ __forceinline__ void dq_ksteps(const bf16* kimg, const bf16* si, int 
 }
 }  // namespace
 
-// grid: (N / 256 key blocks) x B·H, XCD-aware order (one head's blocks on one XCD); 512
-// threads; kSmemFused bytes of LDS. nsa = ceil(N / 64) query steps of the whole sequence (the
-// slab's step axis).
+// grid: (N / 256 key blocks) x the ngrp heads [bh0, bh0 + ngrp), XCD-aware order (one head's
+// blocks on one XCD); 512 threads; kSmemAll bytes of LDS. nsa = ceil(N / 64) query steps of the
+// whole sequence (the slab's and the counters' step axis). ws_bytes: the arrival counters
+// (slab_off bytes) and the group's slab behind them, one buffer resource over both.
 // PAIR (causal): a workgroup owns key blocks nkb - 1 - u (light: the fewest query steps) and
 // then u (heavy) of one head, so every workgroup walks about nkb + 1 blocks' worth of steps
 // (the split kernels' pairing, fa_bwd_bf16.hip); the two blocks are two passes of one body.
 template <bool CAUSAL, bool PAIR = false>
-__global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb, int nsa, bf16* slab) {
+__global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb, int nsa, int bh0,
+                                                             int slab_off, int ws_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
@@ -234,8 +253,13 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   const int N = p.N;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int nslot = PAIR ? (nkb + 1) / 2 : nkb;
-  const int bh = logical / nslot, u_ = logical % nslot;
+  const int bhl = logical / nslot, u_ = logical % nslot;  // head within the group
+  const int bh = bh0 + bhl;
   const int b = bh / p.H, hh = bh % p.H;
+  // the dQ hand-off: one buffer resource over the arrival counters (atomics) and the group's
+  // slab (sc1 stores and loads), and the pass's list of steps this workgroup reduces
+  const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(p.dq_cnt, (short)0, ws_bytes, 0x00020000);
+  int* const red = (int*)(smem + kSmemFused);  // [0]: count, [1 ..]: query steps
 #pragma nounroll
   for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
   const int kb = PAIR ? (pass == 0 ? nkb - 1 - u_ : u_) : u_;
@@ -272,8 +296,10 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   // this wave's dQᵀ strip: queries 16·(wave & 3) .., d 32·(wave >> 2) ..
   const int q16 = wave & 3, d32 = wave >> 2;
   const int oa0 = dq_off(lane, 32 * d32), oa1 = dq_off(lane, 32 * d32 + 16), ob = dq_off(lane, 16 * q16);
-  bf16* const slab_w = slab + (((int64_t)bh * nsa * nkb + kb) * 8 + wave) * 512 + lane * 8;
-  const int64_t slab_step = (int64_t)nkb * 8 * 512;
+  // byte offsets in the group's slab: this wave's partial of step s at slab_w + s · slab_step
+  const int slab_w = slab_off + ((bhl * nsa * nkb + kb) * 8 + wave) * 1024 + lane * 16;
+  const int slab_step = nkb * 8 * 1024;
+  const int nkv = (Nk + kKB - 1) / kKB;  // key blocks holding keys that attend
 
   // LDS-DMA staging: wave w fills rows 8(w & 3) .. + 7 of sub-tile w >> 2's Q and dO images
   const bf16* Qg = (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
@@ -324,7 +350,30 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     bf16x8 o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) { o[i] = (bf16)acc[0][i]; o[4 + i] = (bf16)acc[1][i]; }
-    *(bf16x8*)(slab_w + (int64_t)(step0 + tl) * slab_step) = o;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rsl, slab_w + (step0 + tl) * slab_step, 0, kSc1);
+  };
+  // Arrivals (wave 0; the add by lane 0): arrive(s) first settles the previous add, whose
+  // return value the caller has waited for (the next step's vmcnt, or settle's own wait at the
+  // end), then adds 1 to step s's counter. The contributors of step s are the key blocks below
+  // nkv (keys that attend) and, causal, at or before it (4 kb <= s).
+  int pend_s = -1, nred = 0;  // wave-uniform
+  int pend_old = 0;           // lane 0
+  auto settle = [&]() __attribute__((always_inline)) {
+    if (pend_s >= 0) {
+      const int tgt = CAUSAL ? min(nkv, pend_s / (kKB / kStep) + 1) : nkv;
+      if (__builtin_amdgcn_readfirstlane(pend_old) + 1 == tgt) {
+        if (lane == 0) red[1 + nred] = pend_s;
+        ++nred;
+      }
+      pend_s = -1;
+    }
+  };
+  auto arrive = [&](int s) __attribute__((always_inline)) {
+    if (wave == 0) {
+      settle();
+      if (lane == 0) pend_old = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rsl, (bh * nsa + s) * 4, 0, 0);
+      pend_s = s;
+    }
   };
 
   f32x16 dK[2], dV[2];
@@ -364,8 +413,9 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     if (DQ_) dq_ksteps<4, 8, kPF && !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);             \
     FSUB(MASK_, SLOT_, t_, 1)                                                            \
     if (DQ_) dq_store(qa_, t_ - 1);                                                      \
-    if (more_) publish(DQ_);                                                             \
+    if (more_ || (DQ_)) publish(DQ_);  /* DQ_: the store of step t - 2 has completed */  \
     __syncthreads();                                                                     \
+    if (t_ >= 2) arrive(step0 + t_ - 2);                                                 \
   }
   if (nstep > 0) {
     if (nhead > 0 || nfull == 0) FSTEP(true, 0, 0, false) else FSTEP(false, 0, 0, false)
@@ -397,6 +447,15 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     dq_ksteps<4, 8, kPF>(kimg, dsimg + ((nstep - 1) & 1) * (kKB * kStep), oa0, oa1, ob, qa);
     dq_store(qa, nstep - 1);
   }
+  // the last two steps' arrivals: every wave's stores complete, the barrier, the adds
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nstep >= 2) arrive(step0 + nstep - 2);
+  if (nstep >= 1) arrive(step0 + nstep - 1);
+  if (wave == 0) {
+    settle();
+    if (lane == 0) red[0] = nred;
+  }
 
   if (my_k < N) {
     bf16* dKg = (bf16*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
@@ -412,88 +471,100 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
         store4(dVg + col, dV[db][4 * g], dV[db][4 * g + 1], dV[db][4 * g + 2], dV[db][4 * g + 3], true);
       }
   }
+
+  // dQ of the steps this workgroup arrived last at: wave w sums its strip's partials over the
+  // step's contributing key blocks in key-block order (fp32, one rounding at the end: the
+  // round-3 reduce kernel's arithmetic), from sc1 loads, eight 16-B loads in flight per lane.
+  // Lane l holds d = 32 (w >> 2) + 4 (l >> 4) + 0..3 (+ 16) of query 64 s + 16 (w & 3) + (l & 15).
+  __syncthreads();  // red[] is written
+  const int nr = red[0];
+  bf16* const dQh = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + 32 * (wave >> 2) + 4 * (lane >> 4);
+  const float sc = p.scale;
+  for (int i = 0; i < nr; ++i) {
+    const int st = red[1 + i];
+    const int nk = CAUSAL ? min(nkv, st / (kKB / kStep) + 1) : nkv;
+    const int src = slab_off + ((bhl * nsa + st) * nkb * 8 + wave) * 1024 + lane * 16;
+    float a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = 0.f;
+    int k = 0;
+    for (; k + 8 <= nk; k += 8) {
+      u32x4 x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rsl, src + (k + u) * 8192, 0, kSc1);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bf16x8 y = __builtin_bit_cast(bf16x8, x[u]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += (float)y[j];
+      }
+    }
+    for (; k < nk; ++k) {
+      const bf16x8 y = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsl, src + k * 8192, 0, kSc1));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += (float)y[j];
+    }
+    const int q = st * kStep + 16 * (wave & 3) + (lane & 15);
+    if (q < N) {
+      bf16* dst = dQh + (int64_t)q * p.sdq[2];
+      store4(dst, a[0] * sc, a[1] * sc, a[2] * sc, a[3] * sc, true);
+      store4(dst + 16, a[4] * sc, a[5] * sc, a[6] * sc, a[7] * sc, true);
+    }
+  }
+  // a head whose keys are all padding (kv_len = 0): nothing arrives, its dQ is zero
+  if (nkv == 0 && kb == 0) {
+    bf16* dQz = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1];
+    for (int r = tid >> 3; r < N; r += 64) *(uint4*)(dQz + (int64_t)r * p.sdq[2] + 8 * (tid & 7)) = uint4{0, 0, 0, 0};
+  }
   }  // pass
 }
 
-// dQ = scale · Σ_kb slab[bh][step][kb] in key-block order. One wave per (bh, step, strip w):
-// lane l holds d = 32·(w >> 2) + 4·(l >> 4) + 0..3 (+16 for its second 4) of query
-// 64·step + 16·(w & 3) + (l & 15) (the 16x16 dQᵀ accumulator layout). Causal: key block kb
-// holds partials only for steps >= 4·kb; blocks of padding keys only (kb·256 >= kv_len)
-// hold none.
-__global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, const bf16* slab, int nkb,
-                                                        int nsa, int causal) {
-  const int lane = threadIdx.x & 63;
-  const int64_t unit = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (unit >= (int64_t)p.B * p.H * nsa * 8) return;
-  const int w = (int)(unit & 7);
-  const int64_t bs = unit >> 3;
-  const int s = (int)(bs % nsa);
-  const int bh = (int)(bs / nsa);
-  const int q = s * kStep + 16 * (w & 3) + (lane & 15);
-  const int nkv = (kv_keys(p, bh / p.H) + kKB - 1) / kKB;
-  const int nk = min(nkv, causal ? min(nkb, s / (kKB / kStep) + 1) : nkb);
-  const bf16* src = slab + (bs * nkb * 8 + w) * 512 + lane * 8;
-  float a[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) a[i] = 0.f;
-  int k = 0;
-  for (; k + 8 <= nk; k += 8) {  // eight 16-B loads in flight per lane (the sum order is unchanged)
-    bf16x8 x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = __builtin_nontemporal_load((const bf16x8*)(src + (int64_t)(k + u) * 4096));
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] += (float)x[u][i];
-  }
-  for (; k + 4 <= nk; k += 4) {
-    bf16x8 x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load((const bf16x8*)(src + (int64_t)(k + u) * 4096));
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] += (float)x[u][i];
-  }
-  for (; k < nk; ++k) {
-    const bf16x8 x = __builtin_nontemporal_load((const bf16x8*)(src + (int64_t)k * 4096));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] += (float)x[i];
-  }
-  if (q >= p.N) return;
-  const int b = bh / p.H, hh = bh % p.H;
-  bf16* dst = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)q * p.sdq[2] + 32 * (w >> 2) + 4 * (lane >> 4);
-  const float sc = p.scale;
-  store4(dst, a[0] * sc, a[1] * sc, a[2] * sc, a[3] * sc, true);
-  store4(dst + 16, a[4] * sc, a[5] * sc, a[6] * sc, a[7] * sc, true);
+// The fused backward's workspace beyond the prep rows: the arrival counters ([B·H][nsa] u32,
+// 256-B padded) and the slab of one head group (at most kSlabCap bytes); 0 when a single
+// head's slab exceeds the cap (N > 46340: the split backward runs instead).
+static int64_t fused_head_slab(int64_t N) {
+  return ((N + kStep - 1) / kStep) * ((N + kKB - 1) / kKB) * 8 * 512 * 2;
+}
+static int64_t fused_counter_bytes(int64_t B, int64_t H, int64_t N) {
+  return (B * H * ((N + kStep - 1) / kStep) * 4 + 255) / 256 * 256;
+}
+static int64_t fused_group_heads(int64_t B, int64_t H, int64_t N) {
+  return std::min<int64_t>(B * H, kSlabCap / fused_head_slab(N));
+}
+int64_t bwd_fused_ws_bytes(int64_t B, int64_t H, int64_t N) {
+  // (one buffer resource with 32-bit offsets spans the counters and the slab)
+  if (fused_head_slab(N) > kSlabCap || fused_counter_bytes(B, H, N) + kSlabCap > 0x7fffffff) return 0;
+  return fused_counter_bytes(B, H, N) + fused_group_heads(B, H, N) * fused_head_slab(N);
 }
 
-// Slab bytes the fused backward needs beyond the prep workspace.
-int64_t bwd_fused_slab_bytes(int64_t B, int64_t H, int64_t N) {
-  const int64_t nkb = (N + kKB - 1) / kKB, nsa = (N + kStep - 1) / kStep;
-  return B * H * nsa * nkb * 8 * 512 * 2;
-}
-
-// The fused pass and the dQ reduce (after fa_bwd_prep_bf16). slab: bwd_fused_slab_bytes
-// bytes, 16-B aligned. (Launching the pair per group of batch rows, so that a group's
-// partials stay in the Infinity Cache for the reduce, measured 1 % faster at C3:
-// profiles/r3_ab_bwd_chunk.txt; not kept.)
-hipError_t launch_bwd_fused(const AttnArgs& a, bool causal, bf16* slab, hipStream_t st) {
+// The fused pass (after fa_bwd_prep_bf16, which zeroes the arrival counters), launched once
+// per group of at most fused_group_heads heads so that the partials of a launch stay within
+// kSlabCap (C3: one launch of 128 heads); the groups reuse the slab in stream order. ws: the
+// bwd_fused_ws_bytes region of the workspace, 256-B aligned.
+hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream_t st) {
+  AttnArgs a = a0;
+  const int64_t B = a.B, H = a.H, N = a.N;
+  if (fused_head_slab(N) > kSlabCap || fused_counter_bytes(B, H, N) + kSlabCap > 0x7fffffff)
+    return hipErrorInvalidValue;
+  a.dq_cnt = (unsigned*)ws;
   const int nkb = (a.N + kKB - 1) / kKB, nsa = (a.N + kStep - 1) / kStep;
+  const int64_t grp = fused_group_heads(B, H, N);
   // causal: light/heavy pairs while the paired grid still has a workgroup per CU
-  const bool pair = causal && (int64_t)((nkb + 1) / 2) * a.B * a.H >= 256;
-  const int64_t nblk = (int64_t)(pair ? (nkb + 1) / 2 : nkb) * a.B * a.H;
-  const int64_t nunit = (int64_t)a.B * a.H * nsa * 8;
-  if (nblk > 0x7fffffff || (nunit + 3) / 4 > 0x7fffffff) return hipErrorInvalidValue;
+  const bool pair = causal && (int64_t)((nkb + 1) / 2) * grp >= 256;
   auto kfn = pair ? fa_bwd_fused_bf16<true, true> : causal ? fa_bwd_fused_bf16<true> : fa_bwd_fused_bf16<false>;
-  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kSmemFused);
+  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kSmemAll);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(512), kSmemFused, st, a, nkb, nsa, slab);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(fa_bwd_dq_reduce, dim3((unsigned)((nunit + 3) / 4)), dim3(256), 0, st, a,
-                     (const bf16*)slab, nkb, nsa, causal ? 1 : 0);
-  return hipGetLastError();
+  for (int64_t bh0 = 0; bh0 < B * H; bh0 += grp) {
+    const int64_t ng = std::min<int64_t>(grp, B * H - bh0);
+    const int64_t nblk = (int64_t)(pair ? (nkb + 1) / 2 : nkb) * ng;
+    if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)nblk), dim3(512), kSmemAll, st, a, nkb, nsa, (int)bh0,
+                       (int)fused_counter_bytes(B, H, N),
+                       (int)(fused_counter_bytes(B, H, N) + ng * fused_head_slab(N)));
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace mt

@@ -193,6 +193,7 @@ struct AttnArgs {
   float* m; float* l;              // fwd outputs / bwd inputs, [B*H*N]
   float* lse2; float* delta;       // bwd workspace, [B*H*N]
   void* slab;                      // bwd workspace: dQ partials of the fused bf16 backward
+  unsigned* dq_cnt;                // bwd workspace: its per-(head, query step) arrival counters
   const int* kv_len;               // [B] valid keys per batch row (keys >= kv_len masked), or null
   int o_f32;                       // bf16 forward: O is fp32 (MT_BF16_F32OUT), else O has the input type
   int knob;                        // A/B schedule knob (diagnostics build: env MT_KNOB; product: 0)

@@ -43,6 +43,9 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
 struct Blk6 {
   f32x4 s[4][2];  // scores of one 32-query block and 64-key tile: [16-key block kb][query half qh]
@@ -53,6 +56,28 @@ struct Pf6 {
 
 __device__ __forceinline__ f32x4 mma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// The PV product: bf16, or with H fp16 operands (the Vᵀ fragments read from an image the
+// kernel converted to fp16, the P operand packed as fp16) held in the same registers.
+template <bool H>
+__device__ __forceinline__ f32x4 mma_pv(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if (!H) return mma16(a, b, c);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// H: the in-LDS bf16 -> fp16 conversion of a staged V tile, 16 B per thread of the workgroup
+// (exact for |v| < 65520; larger values become inf and send the block to the bf16 serial pass).
+__device__ __forceinline__ u32x4 vcvt_read(const bf16* tile, int tid) {
+  return *(const u32x4*)((const char*)tile + tid * 16);
+}
+__device__ __forceinline__ void vcvt_write(bf16* tile, int tid, const u32x4& x) {
+  u32x4 y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x2 f = {__uint_as_float(x[j] << 16), __uint_as_float(x[j] & 0xffff0000u)};
+    y[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(f, f16x2));
+  }
+  *(u32x4*)((char*)tile + tid * 16) = y;
 }
 
 // K fragment f of a tile: 16-key block f >> 1, k-step f & 1 (d 32ks + 8g ..)
@@ -85,12 +110,19 @@ __device__ __forceinline__ f32x2 sm6_exp(const Blk6& s, int kk, int i, float c2,
   return f32x2{__builtin_amdgcn_exp2f(x0), __builtin_amdgcn_exp2f(x1)};
 }
 // RS: no row-sum adds (the PV phase sums the packed P on the MFMA pipe)
-template <bool RS = false>
+// H: P packed as fp16 (v_cvt_pk_f16_f32, round to nearest even: 11 significant bits).
+template <bool RS = false, bool H = false>
 __device__ __forceinline__ void sm6_fin(const f32x2& e, int i, f32x2 (&acc)[2], Pf6& pf) {
   const int kbl = i >> 2, qh = (i >> 1) & 1, r0 = 2 * (i & 1);
   if (!RS) {
     acc[qh][0] += e[0];
     acc[qh][1] += e[1];
+  }
+  if (H) {
+    u32x4 w = __builtin_bit_cast(u32x4, pf.p[qh]);
+    w[2 * kbl + (i & 1)] = __builtin_bit_cast(unsigned, __builtin_convertvector(e, f16x2));
+    pf.p[qh] = __builtin_bit_cast(bf16x8, w);
+    return;
   }
   pf.p[qh][4 * kbl + r0] = (bf16)e[0];
   pf.p[qh][4 * kbl + r0 + 1] = (bf16)e[1];
@@ -100,11 +132,11 @@ __device__ __forceinline__ void sm6_fin(const f32x2& e, int i, f32x2 (&acc)[2], 
 // m / 2 in the even slot, its row-sum adds and bf16 pack in the odd one. EV (with RS only):
 // one exponential per slot, and in odd slots the pack of the previous pair (the last pair is
 // packed after the phase's last MFMA): 12 / 16 cycles of issue per slot instead of 24 / 4.
-template <bool PS, bool RS, bool EV>
+template <bool PS, bool RS, bool EV, bool H = false>
 __device__ __forceinline__ void sm6_slot(int m, const Blk6& s_in, int kk, float c2, const float (&nmc)[2],
                                          f32x2 (&acc)[2], Pf6& pf, f32x2& ep, f32x2& ec) {
   if (!EV) {
-    if (m & 1) sm6_fin<RS>(ep, m >> 1, acc, pf);
+    if (m & 1) sm6_fin<RS, H>(ep, m >> 1, acc, pf);
     else ep = sm6_exp<PS>(s_in, kk, m >> 1, c2, nmc);
     return;
   }
@@ -112,7 +144,7 @@ __device__ __forceinline__ void sm6_slot(int m, const Blk6& s_in, int kk, float 
   const float v = s_in.s[2 * kk + kbl][qh][r];
   ec[j] = __builtin_amdgcn_exp2f(PS ? v : __builtin_fmaf(v, c2, nmc[qh]));
   if (j) {
-    if (i) sm6_fin<true>(ep, i - 1, acc, pf);
+    if (i) sm6_fin<true, H>(ep, i - 1, acc, pf);
     ep = ec;
   }
 }
@@ -120,7 +152,7 @@ __device__ __forceinline__ void sm6_slot(int m, const Blk6& s_in, int kk, float 
 // QKᵀ phase: 16 MFMAs into S (16-key blocks in order, so keys 0-31 finish first), beside the
 // softmax of half kk of s_in. MFMA m: fragment f = m >> 1 (block f >> 1, k-step f & 1),
 // query half m & 1. The chains start from ci[qh] (zero, or the PS shift).
-template <bool SOFT, bool PS, bool RS = false, bool EV = false>
+template <bool SOFT, bool PS, bool RS = false, bool EV = false, bool H = false>
 __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf16x8 (&qf)[2][2], Blk6& S,
                                     const f32x4 (&ci)[2], const Blk6& s_in, int kk, float c2,
                                     const float (&nmc)[2], f32x2 (&acc)[2], Pf6& pf) {
@@ -133,10 +165,10 @@ __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf
     const int f = m >> 1, kb = f >> 1, ks = f & 1, qh = m & 1;
     if (!(m & 1) && f + 2 < 8) kf[f + 2] = kread6(sk, ko, f + 2);
     S.s[kb][qh] = mma16(kf[f], qf[qh][ks], ks ? S.s[kb][qh] : ci[qh]);
-    if (SOFT) sm6_slot<PS, RS, EV>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
+    if (SOFT) sm6_slot<PS, RS, EV, H>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (SOFT && EV) sm6_fin<true>(ep, 7, acc, pf);
+  if (SOFT && EV) sm6_fin<true, H>(ep, 7, acc, pf);
 }
 
 // PV phase: 16 MFMAs into O with the P operands of halves 0 (plo) and 1 (phi), beside the
@@ -144,12 +176,13 @@ __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf
 // query half m & 1. KEEP: 1 = read the Vᵀ fragments and leave them in vk, 2 = take them
 // from vk (P2 and P4 multiply the same V(t)). RS: R[qh] += ones·Pᵀ right after each P
 // operand's first MFMA (every element of R[qh] is then the running row sum of its query).
-template <bool SOFT, int KEEP, bool PS, bool RS = false, bool EV = false>
+template <bool SOFT, int KEEP, bool PS, bool RS = false, bool EV = false, bool H = false>
 __device__ __forceinline__ void pv6(const bf16* sv, const int (&vo)[4], f32x4 (&O)[4][2], const Pf6& plo,
                                     const Pf6& phi, const Blk6& s_in, int kk, float c2,
                                     const float (&nmc)[2], f32x2 (&acc)[2], Pf6& pf, bf16x8 (&vk)[8],
                                     f32x4 (&R)[2]) {
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, s16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
+  constexpr short one = H ? 0x3c00 : 0x3f80;  // 1.0 in fp16 / bf16
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, s16x8{one, one, one, one, one, one, one, one});
   bf16x8 vf_own[8];
   bf16x8(&vf)[8] = KEEP ? vk : vf_own;
   if (KEEP != 2) {
@@ -161,12 +194,12 @@ __device__ __forceinline__ void pv6(const bf16* sv, const int (&vo)[4], f32x4 (&
   for (int m = 0; m < 16; ++m) {
     const int f = m >> 1, hv = f >> 2, db = f & 3, qh = m & 1;
     if (KEEP != 2 && !(m & 1) && f + 2 < 8) vf[f + 2] = vread6(sv, vo, f + 2);
-    O[db][qh] = mma16(vf[f], (hv ? phi : plo).p[qh], O[db][qh]);
-    if (RS && db == 0) R[qh] = mma16(ones, (hv ? phi : plo).p[qh], R[qh]);
-    if (SOFT) sm6_slot<PS, RS, EV>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
+    O[db][qh] = mma_pv<H>(vf[f], (hv ? phi : plo).p[qh], O[db][qh]);
+    if (RS && db == 0) R[qh] = mma_pv<H>(ones, (hv ? phi : plo).p[qh], R[qh]);
+    if (SOFT) sm6_slot<PS, RS, EV, H>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (SOFT && EV) sm6_fin<true>(ep, 7, acc, pf);
+  if (SOFT && EV) sm6_fin<true, H>(ep, 7, acc, pf);
 }
 
 // max over the four lanes that share a query (i, i + 16, i + 32, i + 48)
@@ -228,8 +261,15 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // through its own K/V rings (the halves' pairs have equal tile counts, so their barriers
   // line up); wave-tile utilisation 95.6 % instead of 90.3 % at C3
   constexpr bool DUAL = VAR & 256;
+  // causal, fp16 PV (VAR 512, the fp32-output default): V tiles are staged two ahead into a
+  // 4-slot ring and converted to fp16 in LDS the tile before use; P is packed as fp16 (11
+  // significant bits instead of 8) for the PV and row-sum MFMAs, which takes the rounding
+  // of P, the error that dominates rows with few keys, down 8x
+  constexpr bool H = VAR & 512;
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   static_assert(!DUAL || CAUSAL, "dual halves: causal");
+  static_assert(!H || (CAUSAL && !DUAL && !PS && RS && !EV), "fp16 PV: the causal default form");
+  constexpr int VS = H ? 4 : kVSlots;  // V ring slots
   constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
   constexpr int NWQ = (SPLIT || DUAL) ? 4 : kNW;  // waves sharing one query block and its key tiles
   constexpr int LPT = kNW / NWQ;        // LDS-DMA instructions per wave per tile
@@ -243,8 +283,8 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   const int half = (SPLIT || DUAL) ? (wave >> 2) : 0;
   const int wq = (SPLIT || DUAL) ? (wave & 3) : wave;  // this wave's 64 queries within the block
   const int Nk = SPLIT ? N / 2 : N;          // keys this wave's half walks
-  bf16* const sK = (bf16*)smem_raw + half * (kKSlots + kVSlots) * TILE;  // [kKSlots][TILE]
-  bf16* const sV = sK + kKSlots * TILE;                                  // [kVSlots][TILE]
+  bf16* const sK = (bf16*)smem_raw + half * (kKSlots + VS) * TILE;  // [kKSlots][TILE]
+  bf16* const sV = sK + kKSlots * TILE;                             // [VS][TILE]
 
   const int nblk = gridDim.x, hw = blockIdx.x;
   const int xcd = hw & 7, slot = hw >> 3, qd = nblk >> 3, rm = nblk & 7;
@@ -367,8 +407,13 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   dma_k(sK, 0);
   dma_v(sV, 0);
   dma_k(sK + TILE, ktile_b);
+  if (H) dma_v(sV + TILE, vtile_b);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (H) {  // V(0) to fp16 (V(1) is converted in iteration 0)
+    vcvt_write(sV, tid, vcvt_read(sV, tid));
+    __syncthreads();
+  }
   if (nbulk >= 1) {  // non-causal: the launcher guarantees N >= 128
     Blk6 SA, SB;
     {
@@ -403,17 +448,22 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     f32x2 accA[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, accB[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
     Pf6 pB0, pB1, pA0, pA1;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sm6_fin<RS>(sm6_exp<PS>(SB, 0, i, c2, nmcB), i, accB, pB0);
+    for (int i = 0; i < 8; ++i) sm6_fin<RS, H>(sm6_exp<PS>(SB, 0, i, c2, nmcB), i, accB, pB0);
     f32x4 RA[2] = {f32x4{}, f32x4{}}, RB[2] = {f32x4{}, f32x4{}};
 
     // iteration t: K(t) in slot t % 4, K(t + 1) in slot (t + 1) % 4, V(t) in slot t % 2;
     // stages K(t + 2) and V(t + 1). Unrolled by the K ring size (slot offsets immediate).
+    // H: V(t + 2) is staged (4-slot V ring) and V(t + 1), landed by the previous tile's
+    // barrier, is converted to fp16 beside P1 (read before it, written after it).
     auto iter = [&](int t, int s0) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
       dma_k(sK + ((s0 + 2) & 3) * TILE, (t + 2) * ktile_b);
-      dma_v(sV + ((s0 + 1) & 1) * TILE, (t + 1) * vtile_b);
+      if (H) dma_v(sV + ((s0 + 2) & 3) * TILE, (t + 2) * vtile_b);
+      else dma_v(sV + ((s0 + 1) & 1) * TILE, (t + 1) * vtile_b);
+      u32x4 vraw;
+      if (H) vraw = vcvt_read(sV + ((s0 + 1) & 3) * TILE, tid);
       int koA[2], koB[2], vv[4];
-      const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & 1) * TILE;
+      const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & (VS - 1)) * TILE;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         koA[ks] = ko[ks] + kslA;
@@ -421,10 +471,11 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       }
 #pragma unroll
       for (int db = 0; db < 4; ++db) vv[db] = vo[db] + vsl;
-      qk6<true, PS, RS, EV>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
-      pv6<true, K1, PS, RS, EV>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
-      qk6<true, PS, RS, EV>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
-      pv6<true, K2, PS, RS, EV>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
+      qk6<true, PS, RS, EV, H>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
+      if (H) vcvt_write(sV + ((s0 + 1) & 3) * TILE, tid, vraw);
+      pv6<true, K1, PS, RS, EV, H>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
+      qk6<true, PS, RS, EV, H>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
+      pv6<true, K2, PS, RS, EV, H>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!NOBAR) __syncthreads();
     };
@@ -441,16 +492,16 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) koA[ks] = ko[ks] + (t & 3) * TILE;
 #pragma unroll
-      for (int db = 0; db < 4; ++db) vv[db] = vo[db] + (t & 1) * TILE;
+      for (int db = 0; db < 4; ++db) vv[db] = vo[db] + (t & (VS - 1)) * TILE;
       if (CAUSAL) mask_diag(SB, 32);  // S_B(tD): keys 32-63 are block B's diagonal
-      qk6<true, PS, RS, EV>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
+      qk6<true, PS, RS, EV, H>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
       if (CAUSAL) mask_diag(SA, 0);  // S_A(tD): keys 0-31 its diagonal, 32-63 above it
-      pv6<true, K1, PS, RS, EV>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);
+      pv6<true, K1, PS, RS, EV, H>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sm6_fin<RS>(sm6_exp<PS>(SA, 1, i, c2, nmcA), i, accA, pA1);
+      for (int i = 0; i < 8; ++i) sm6_fin<RS, H>(sm6_exp<PS>(SA, 1, i, c2, nmcA), i, accA, pA1);
       f32x2 d2[2];
       Pf6 dpf;
-      pv6<false, K2, PS, RS>(sV, vv, OA, pA0, pA1, SA, 0, c2, nmcA, d2, dpf, vk, RA);
+      pv6<false, K2, PS, RS, false, H>(sV, vv, OA, pA0, pA1, SA, 0, c2, nmcA, d2, dpf, vk, RA);
     }
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
@@ -459,12 +510,34 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       pA[qh] = RS ? 0.25f * RA[qh][0] : accA[qh][0] + accA[qh][1];
       pB[qh] = RS ? 0.25f * RB[qh][0] : accB[qh][0] + accB[qh][1];
     }
+    if (H) {
+      // fp16 P must stay below 65504: a row sum past 2^15 (a quarter share past 2^13), or a
+      // non-finite O (a V value past the fp16 range), sends the block to the serial pass
+      float om = 0.f;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) om = fmaxf(om, fmaxf(fabsf(OA[db][qh][r]), fabsf(OB[db][qh][r])));
+      if (!(om <= 3.0e38f)) pA[0] = INFINITY;
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        if (!(pA[qh] <= 8192.f)) pA[qh] = INFINITY;
+        if (!(pB[qh] <= 8192.f)) pB[qh] = INFINITY;
+      }
+    }
   }
   if (CAUSAL) {
     // tail: this wave's share of the staging of the tiles the other waves still need
     for (int t = nbulk > 0 ? nbulk - 1 : 0; t + 1 < ntiles; ++t) {
       dma_k(sK + ((t + 2) & 3) * TILE, (t + 2) * ktile_b);
-      dma_v(sV + ((t + 1) & 1) * TILE, (t + 1) * vtile_b);
+      if (H) {  // and its share of the conversion of V(t + 1)
+        dma_v(sV + ((t + 2) & 3) * TILE, (t + 2) * vtile_b);
+        vcvt_write(sV + ((t + 1) & 3) * TILE, tid, vcvt_read(sV + ((t + 1) & 3) * TILE, tid));
+      } else {
+        dma_v(sV + ((t + 1) & 1) * TILE, (t + 1) * vtile_b);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -658,12 +731,13 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
-  const size_t smem = (size_t)(split || dual ? 2 : 1) * (kKSlots + kVSlots) * TILE * sizeof(bf16);
+  const size_t smem = (size_t)(split || dual ? 2 : 1) * (kKSlots + (var & 512 ? 4 : kVSlots)) * TILE * sizeof(bf16);
   void (*kern)(AttnArgs, int) = nullptr;
   switch (var) {  // product build: the defaults 66 / 18 / 98; the rest are A/B policies
     case 66: kern = fa_fwd_bf16_v6<66>; break;
     case 18: kern = fa_fwd_bf16_v6<18>; break;
     case 98: kern = fa_fwd_bf16_v6<98>; break;
+    case 610: kern = fa_fwd_bf16_v6<610>; break;  // 98 with fp16 PV (the fp32-output causal default)
 #ifdef MT_DIAGNOSTICS
     case 354: kern = fa_fwd_bf16_v6<354>; break;
     case 194: kern = fa_fwd_bf16_v6<194>; break;

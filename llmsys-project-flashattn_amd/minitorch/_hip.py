@@ -48,6 +48,8 @@ _PROTOS = {
                                  _i64, _i64, _i64, _i64, _i64p, _vp, _vp]),
     "mt_flash_attn_bwd_varlen": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                         _i64, _i64, _i64, _i64, _i64p, _vp, _vp, _vp]),
+    "mt_flash_attn_bwd_v3": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _i64, _i64, _i64, _i64, _i64p, _vp, _vp, _i64, _vp]),
     "mt_attn_softmax_fw": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64p, _int, _vp]),
     "mt_attn_softmax_bw": (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_layernorm_fw": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
@@ -272,11 +274,10 @@ def flash_bwd(q, k, v, o, do, m, l, causal: bool = False, dq=None, dk=None, dv=N
     args = (dtype_code(q), int(causal), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
             do.data_ptr(), m.data_ptr(), l.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
             B, H, N, d, strides)
-    if kv is None:
-        check(lib().mt_flash_attn_bwd(*args, workspace.data_ptr(), st), "mt_flash_attn_bwd")
-    else:
-        check(lib().mt_flash_attn_bwd_varlen(*args, kv.data_ptr(), workspace.data_ptr(), st),
-              "mt_flash_attn_bwd_varlen")
+    # the size-checked entry (ABI 3): a workspace the caller sized too small is an error
+    check(lib().mt_flash_attn_bwd_v3(*args, None if kv is None else kv.data_ptr(),
+                                     workspace.data_ptr(), workspace.numel() * workspace.element_size(),
+                                     st), "mt_flash_attn_bwd_v3")
     return dq, dk, dv
 
 

@@ -113,6 +113,38 @@ def chunk_rows(bh: int, world: int, rank: int, chunks: int, c: int) -> Tuple[int
     return lo, lo + rc
 
 
+def forward_workgroups_per_head(N: int, d: int, causal: bool = False) -> int:
+    """Workgroups one head contributes to the grid of the bf16 forward's default form
+    (capi_flash.hip fwd_bf16_dispatch): d = 64, 512-query 8-wave workgroups (v6; below one per
+    CU the dispatcher falls back to the slower split-keys form); d = 128, 256-query workgroups
+    (d128v2); causal, light / heavy pairs of 512-query blocks (v6 causal)."""
+    if causal:
+        return max(1, (-(-N // 512) + 1) // 2)
+    return max(1, -(-N // (512 if d == 64 else 256)))
+
+
+def occupancy_chunks(B: int, H: int, N: int, d: int, world: int, causal: bool = False,
+                     max_chunks: int = 4, cus: int = 256) -> int:
+    """Chunks for the overlapped all-gather (``sharded_flash_fwd(chunks=...)``, bench.py's
+    end-to-end leg): the largest power of two up to ``max_chunks`` such that each chunk's
+    forward still launches at least one workgroup per CU (``cus``, 256 on MI355X) and the
+    rank's rows divide evenly. A chunk whose grid leaves CUs idle, or drops the d = 64 forward
+    into its split-keys form, runs at a fraction of the kernel's rate, which costs more than
+    the overlap hides: C3 (8,16,4096,64) takes 2 chunks at 2 ranks (32 heads x 8 workgroups)
+    and none from 4 ranks up (at 8 ranks its 16 heads per rank are below one 8-wave workgroup
+    per CU even unchunked); C4 (64,16,16384,128) at 8 ranks (128 heads, 64 workgroups each)
+    takes 4."""
+    rows = (B * H) // world if world > 0 else 0
+    if world <= 0 or (B * H) % world:
+        return 1
+    per_head = forward_workgroups_per_head(N, d, causal)
+    c = 1
+    while (c * 2 <= max_chunks and rows % (c * 2) == 0
+           and (rows // (c * 2)) * per_head >= cus):
+        c *= 2
+    return c
+
+
 def _chunked_gather_fwd(q, k, v, causal, group, world, rank, chunks, fn):
     """The gathered forward with the all-gather of finished chunks overlapping the forward of
     the next: chunk c's three all-gathers are issued asynchronously right after its forward
@@ -152,8 +184,11 @@ def sharded_flash_fwd(q, k, v, causal: bool = False, group=None, gather: bool = 
     ``chunks`` > 1 (with ``gather``): the rank computes its rows in ``chunks`` pieces and
     all-gathers each piece while the next one computes ("chunk the shard
     and overlap"); the rows are dealt block-cyclically (``chunk_rows``) so every gather lands
-    in place. Needs B*H divisible by world*chunks, else the forward runs unchunked. The
-    gathered result is bit-identical to the unchunked one.
+    in place. Needs B*H divisible by world*chunks, else the forward runs unchunked;
+    ``occupancy_chunks`` picks a count that keeps every chunk's grid at one workgroup per CU.
+    Each chunk's forward runs on a smaller grid, where the bf16 dispatcher may pick another
+    kernel form (split keys): the gathered O is then within the forward's parity bound of the
+    unchunked one, not bit-identical (bit-identical with the CPU attention the tests inject).
 
     ``world``/``rank`` default to the process group's; giving them explicitly computes that
     rank's shard without any collective (with ``gather``, ``rank`` must be this process's

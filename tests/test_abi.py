@@ -42,16 +42,41 @@ def test_python_binding_covers_header():
         declared.update(_declared(h))
     lib = _hip.lib()  # also applies every argtypes declaration
     assert declared <= set(_hip.exported_symbols()), declared - set(_hip.exported_symbols())
-    assert lib.mt_abi_version() >= 1
-    # fp32 delta + log2-LSE per row, 256-B aligned; at d = 64 (N <= 8192) also the fused
-    # bf16 backward's dQ partial slab: B*H * ceil(N/64) * ceil(N/256) * 8 KiB
+    assert lib.mt_abi_version() == 3
+    # fp32 delta + log2-LSE per row, 256-B aligned; at d = 64 also the fused bf16 backward's
+    # arrival counters (u32 [B*H][ceil(N/64)], 256-B aligned) and the dQ partial slab of one
+    # group of heads: min(B*H, 2^30 // head) heads of ceil(N/64) * ceil(N/256) * 8 KiB each
+    def fused(B, H, N):
+        head = -(-N // 64) * -(-N // 256) * 8192
+        cnt = -(-(B * H * -(-N // 64) * 4) // 256) * 256
+        return cnt + min(B * H, 2 ** 30 // head) * head
     assert lib.mt_flash_attn_bwd_workspace_bytes(2, 3, 5, 7) == 256
-    assert lib.mt_flash_attn_bwd_workspace_bytes(8, 16, 4096, 64) == 2 * 128 * 4096 * 4 + 128 * 64 * 16 * 8192
-    assert lib.mt_flash_attn_bwd_workspace_bytes(1, 16, 16384, 64) == 2 * 16 * 16384 * 4
+    assert lib.mt_flash_attn_bwd_workspace_bytes(8, 16, 4096, 64) == 2 * 128 * 4096 * 4 + fused(8, 16, 4096)
+    assert fused(8, 16, 4096) == 128 * 64 * 4 + 2 ** 30  # C3: one launch, 1 GiB of partials
+    # longer sequences: head groups that reuse a slab of at most 1 GiB (N = 16384: 8 heads)
+    assert lib.mt_flash_attn_bwd_workspace_bytes(1, 16, 16384, 64) == 2 * 16 * 16384 * 4 + fused(1, 16, 16384)
+    # large batches no longer scale the slab (round 3: 32 GiB at (64,16,8192,64))
+    big = lib.mt_flash_attn_bwd_workspace_bytes(64, 16, 8192, 64)
+    assert big == 2 * 1024 * 8192 * 4 + fused(64, 16, 8192) and big < 2 ** 31
+    # past one head's slab within 1 GiB (N > 46336) the split backward needs the rows only
+    assert lib.mt_flash_attn_bwd_workspace_bytes(1, 1, 46336, 64) > 2 * 46336 * 4 + 255
+    assert lib.mt_flash_attn_bwd_workspace_bytes(1, 1, 46400, 64) == 2 * 46400 * 4
     # the fused form needs its lse2 | delta rows under 2^31 bytes (one LDS-DMA buffer)
     bh = 2 ** 31 // (2 * 8192 * 4)
     assert lib.mt_flash_attn_bwd_workspace_bytes(1, bh - 1, 8192, 64) > 2 * (bh - 1) * 8192 * 4 + 255
     assert lib.mt_flash_attn_bwd_workspace_bytes(1, bh, 8192, 64) == 2 * bh * 8192 * 4
+
+
+def test_bwd_v3_rejects_small_workspace():
+    """mt_flash_attn_bwd_v3 checks the caller's workspace size before touching any pointer
+    (host-only: the size check precedes every launch)."""
+    from minitorch import _hip
+    lib = _hip.lib()
+    need = lib.mt_flash_attn_bwd_workspace_bytes(8, 16, 4096, 64)
+    dummy = ctypes.c_void_p(16)
+    rc = lib.mt_flash_attn_bwd_v3(1, 0, *([dummy] * 10), 8, 16, 4096, 64, None, None, dummy,
+                                  need - 1, None)
+    assert rc != 0 and b"workspace" in lib.mt_last_error()
 
 
 def test_errors_are_reported_not_fatal():

@@ -92,7 +92,7 @@ def _run_world(world, argv):
 def test_bench_multi_rank_cpu(world, split, causal):
     shape = (2, 4, 48, 16)
     argv = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--split", split,
-            "--shape", *map(str, shape)] + (["--causal"] if causal else [])
+            "--chunks", "2", "--shape", *map(str, shape)] + (["--causal"] if causal else [])
     out = _run_world(world, argv)
     res, gathered = out[0]
     # the JSON contract fields
@@ -125,3 +125,35 @@ def test_gpus_must_match_world():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
                        capture_output=True, text=True, env={**os.environ, "WORLD_SIZE": "1"})
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_occupancy_chunks_rule():
+    """The end-to-end leg's default chunk count (minitorch/shard.py occupancy_chunks) for
+    BASELINE configs 3 and 4 at 1, 2, 4 and 8 ranks: a chunk keeps at least one workgroup per
+    CU of the forward's default (8-wave, non-split) form."""
+    from minitorch.shard import occupancy_chunks, forward_workgroups_per_head
+    c3, c4 = (8, 16, 4096, 64), (64, 16, 16384, 128)
+    assert [occupancy_chunks(*c3, w) for w in (1, 2, 4, 8)] == [4, 2, 1, 1]
+    assert [occupancy_chunks(*c4, w) for w in (1, 2, 4, 8)] == [4, 4, 4, 4]
+    for shape in (c3, c4):
+        for w in (1, 2, 4, 8):
+            c = occupancy_chunks(*shape, w)
+            rows = shape[0] * shape[1] // w
+            assert rows % c == 0
+            assert c == 1 or (rows // c) * forward_workgroups_per_head(shape[2], shape[3]) >= 256
+    assert occupancy_chunks(8, 16, 4096, 64, 3) == 1   # B*H not divisible by the world
+
+
+def test_bench_default_chunking_world4_bitwise():
+    """gloo world 4: bench.run with the chunk count the rule picks (on a model chip of 2 CUs
+    for this small shape) all-gathers an O bit-identical to the unchunked run's."""
+    from minitorch.shard import occupancy_chunks
+    shape = (4, 4, 48, 16)
+    chosen = occupancy_chunks(*shape, 4, cus=2)
+    assert chosen == 2
+    base = ["--gpus", "4", "--steps", "1", "--warmup", "1", "--shape", *map(str, shape)]
+    chunked = _run_world(4, base + ["--chunks", str(chosen)])
+    serial = _run_world(4, base + ["--chunks", "1"])
+    assert chunked[0][0]["end_to_end"]["chunks"] == chosen
+    for r in range(4):
+        np.testing.assert_array_equal(chunked[r][1], serial[r][1])
