@@ -174,11 +174,23 @@ void mt_set_gemm_backend(int backend);
  * copy a host mask per call. */
 int mt_rand_uniform(float* out, int64_t n, uint64_t seed, void* stream);
 
+/* Fused feed-forward pieces (reference minitorch/modules_transfomer.py FeedForward:
+ * dropout(linear_out(GELU(linear_in(x))))), fp32, x/dy/out rows of `cols` contiguous floats:
+ *   mt_bias_gelu_fw: out = GELU_tanh(x + bias[col])             (linear_in's bias + GELU)
+ *   mt_bias_gelu_bw: dx  = dy * GELU_tanh'(x + bias[col])         (dbias = column sums of dx)
+ *   mt_dropout:      out = u_i > p ? x * scale : 0, u_i the mt_rand_uniform draw of
+ *                    (seed, i), so a backward with the same seed applies the same mask. */
+int mt_bias_gelu_fw(float* out, const float* x, const float* bias, int64_t rows, int64_t cols, void* stream);
+int mt_bias_gelu_bw(float* dx, const float* dy, const float* x, const float* bias, int64_t rows, int64_t cols,
+                    void* stream);
+int mt_dropout(float* out, const float* x, int64_t n, float p, float scale, uint64_t seed, void* stream);
+
 /* Multi-tensor Adam step over n_tensors dense fp32 device tensors (parameters, their
  * gradients, first and second moments, numels[t] elements each), in place:
  *   m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2;  p -= step_size m / (sqrt(v) + eps)
  * step_size = lr sqrt(1 - b2^t) / (1 - b1^t) (host-computed bias correction); b1, b2,
- * 1 - b1, 1 - b2, eps and step_size are each rounded to fp32 once. Replaces the
+ * 1 - b1, 1 - b2, eps and step_size are each rounded to fp32 once; the update divides by
+ * (powf(v, 0.5) + eps) through its reciprocal, as the tensor ops do (bit-identical). Replaces the
  * reference's per-parameter tensor-op Adam (minitorch/optim.py:52-75), one launch per 24
  * tensors. */
 int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,

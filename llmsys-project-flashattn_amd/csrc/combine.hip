@@ -69,46 +69,106 @@ __device__ __forceinline__ float apply_fn(int fn, float x, float y) {
   }
 }
 
-// Position in `in` of the element broadcast to out-ordinal i (shapes right-aligned).
-__device__ __forceinline__ int64_t bcast_pos(int64_t i, const Layout& out, const Layout& in) {
-  int64_t pos = 0;
+// Position in `in` of the element broadcast to out-ordinal i (shapes right-aligned). I: the
+// index type, int32 whenever every ordinal and offset fits (host-checked): the 64-bit
+// division per dimension is a long software sequence on the GPU, and it made the strided
+// copies and broadcasts of the minitorch step several times slower than their bytes.
+template <typename I>
+__device__ __forceinline__ I bcast_pos(I i, const Layout& out, const Layout& in) {
+  I pos = 0;
   const int off = out.dims - in.dims;
   for (int d = out.dims - 1; d >= 0; --d) {
-    const int64_t idx = i % out.shape[d];
-    i /= out.shape[d];
+    const I sh = (I)out.shape[d];
+    const I q = i / sh;
+    const I idx = i - q * sh;
+    i = q;
     const int e = d - off;
-    if (e >= 0 && in.shape[e] != 1) pos += idx * in.strides[e];
+    if (e >= 0 && in.shape[e] != 1) pos += idx * (I)in.strides[e];
   }
   return pos;
 }
-__device__ __forceinline__ int64_t out_pos(int64_t i, const Layout& out) {
+template <typename I>
+__device__ __forceinline__ I out_pos(I i, const Layout& out) {
   if (out.contiguous) return i;
-  int64_t pos = 0;
+  I pos = 0;
   for (int d = out.dims - 1; d >= 0; --d) {
-    pos += (i % out.shape[d]) * out.strides[d];
-    i /= out.shape[d];
+    const I sh = (I)out.shape[d];
+    const I q = i / sh;
+    pos += (i - q * sh) * (I)out.strides[d];
+    i = q;
   }
   return pos;
 }
 
+template <typename I>
 __global__ __launch_bounds__(256) void map_kernel(int fn, float* out, Layout ol, int64_t n,
                                                   const float* in, Layout il, int same) {
-  const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
-    const float x = same ? in[i] : in[bcast_pos(i, ol, il)];
-    out[same ? i : out_pos(i, ol)] = apply_fn(fn, x, 0.f);
+  const I step = (I)gridDim.x * blockDim.x;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < (I)n; i += step) {
+    const float x = same ? in[i] : in[bcast_pos<I>(i, ol, il)];
+    out[same ? i : out_pos<I>(i, ol)] = apply_fn(fn, x, 0.f);
   }
 }
 
+template <typename I>
 __global__ __launch_bounds__(256) void zip_kernel(int fn, float* out, Layout ol, int64_t n,
                                                   const float* a, Layout al, const float* b,
                                                   Layout bl, int same) {
-  const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
-    const float x = same ? a[i] : a[bcast_pos(i, ol, al)];
-    const float y = same ? b[i] : b[bcast_pos(i, ol, bl)];
-    out[same ? i : out_pos(i, ol)] = apply_fn(fn, x, y);
+  const I step = (I)gridDim.x * blockDim.x;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < (I)n; i += step) {
+    const float x = same ? a[i] : a[bcast_pos<I>(i, ol, al)];
+    const float y = same ? b[i] : b[bcast_pos<I>(i, ol, bl)];
+    out[same ? i : out_pos<I>(i, ol)] = apply_fn(fn, x, y);
   }
+}
+
+// Dense fast paths (16 B per lane where the sizes allow): every operand contiguous in the
+// output's order, the second operand either the same shape (BMODE 0), one element (1), or a
+// contiguous block repeated along the leading dims (2: out[i] op b[i % nb], a bias row);
+// SWAP puts the repeated operand on the left.
+template <int BMODE, bool SWAP>
+__global__ __launch_bounds__(256) void zip_dense_kernel(int fn, float* __restrict__ out, int64_t n,
+                                                        const float* __restrict__ a,
+                                                        const float* __restrict__ b, int64_t nb) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  const float b0 = BMODE == 1 ? b[0] : 0.f;
+  if (n % 4 == 0 && (BMODE != 2 || nb % 4 == 0)) {
+    const float4* a4 = (const float4*)a;
+    float4* o4 = (float4*)out;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += step) {
+      const float4 x = a4[i];
+      float4 y;
+      if (BMODE == 0) y = ((const float4*)b)[i];
+      else if (BMODE == 1) y = make_float4(b0, b0, b0, b0);
+      else y = ((const float4*)b)[i % (nb / 4)];
+      float4 r;
+      r.x = SWAP ? apply_fn(fn, y.x, x.x) : apply_fn(fn, x.x, y.x);
+      r.y = SWAP ? apply_fn(fn, y.y, x.y) : apply_fn(fn, x.y, y.y);
+      r.z = SWAP ? apply_fn(fn, y.z, x.z) : apply_fn(fn, x.z, y.z);
+      r.w = SWAP ? apply_fn(fn, y.w, x.w) : apply_fn(fn, x.w, y.w);
+      o4[i] = r;
+    }
+    return;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    const float x = a[i];
+    const float y = BMODE == 0 ? b[i] : BMODE == 1 ? b0 : b[i % nb];
+    out[i] = SWAP ? apply_fn(fn, y, x) : apply_fn(fn, x, y);
+  }
+}
+__global__ __launch_bounds__(256) void map_dense_kernel(int fn, float* __restrict__ out, int64_t n,
+                                                        const float* __restrict__ a) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  if (n % 4 == 0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += step) {
+      const float4 x = ((const float4*)a)[i];
+      ((float4*)out)[i] = make_float4(apply_fn(fn, x.x, 0.f), apply_fn(fn, x.y, 0.f),
+                                      apply_fn(fn, x.z, 0.f), apply_fn(fn, x.w, 0.f));
+    }
+    return;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step)
+    out[i] = apply_fn(fn, a[i], 0.f);
 }
 
 // out has a's shape with shape[dim] = 1. One wave per output element (lanes stride the
@@ -120,7 +180,7 @@ __global__ __launch_bounds__(256) void reduce_wave_kernel(int fn, float* out, La
   const int64_t nw = (int64_t)gridDim.x * 4;
   const int64_t len = al.shape[dim], st = al.strides[dim];
   for (int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); o < n_out; o += nw) {
-    const int64_t base = bcast_pos(o, ol, al);  // out and a share shapes except dim (=1)
+    const int64_t base = bcast_pos<int64_t>(o, ol, al);  // out and a share shapes except dim (=1)
     float acc = 0.f;
     bool have = false;
     for (int64_t j = lane; j < len; j += 64) {
@@ -135,7 +195,7 @@ __global__ __launch_bounds__(256) void reduce_wave_kernel(int fn, float* out, La
       if (hy) acc = have ? apply_fn(fn, acc, y) : y;
       have = have || hy;
     }
-    if (lane == 0) out[out_pos(o, ol)] = have ? apply_fn(fn, start, acc) : start;
+    if (lane == 0) out[out_pos<int64_t>(o, ol)] = have ? apply_fn(fn, start, acc) : start;
   }
 }
 __global__ __launch_bounds__(256) void reduce_thread_kernel(int fn, float* out, Layout ol,
@@ -144,10 +204,10 @@ __global__ __launch_bounds__(256) void reduce_thread_kernel(int fn, float* out, 
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   const int64_t len = al.shape[dim], st = al.strides[dim];
   for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n_out; o += step) {
-    const int64_t base = bcast_pos(o, ol, al);
+    const int64_t base = bcast_pos<int64_t>(o, ol, al);
     float acc = start;
     for (int64_t j = 0; j < len; ++j) acc = apply_fn(fn, acc, a[base + j * st]);
-    out[out_pos(o, ol)] = acc;
+    out[out_pos<int64_t>(o, ol)] = acc;
   }
 }
 
@@ -218,6 +278,34 @@ static bool same_shape(const Layout& a, const Layout& b) {
     if (a.shape[d] != b.shape[d]) return false;
   return true;
 }
+// every ordinal below n and every element offset of the layouts below 2^31 (int32 indexing)
+static bool fits_i32(int64_t n, std::initializer_list<const Layout*> ls) {
+  if (n >= ((int64_t)1 << 31)) return false;
+  for (const Layout* l : ls) {
+    int64_t e = 0;
+    for (int d = 0; d < l->dims; ++d)
+      if (l->shape[d] > 1) e += (l->shape[d] - 1) * (l->strides[d] < 0 ? -l->strides[d] : l->strides[d]);
+    if (e >= ((int64_t)1 << 31)) return false;
+  }
+  return true;
+}
+static int64_t numel(const Layout& l) {
+  int64_t n = 1;
+  for (int d = 0; d < l.dims; ++d) n *= l.shape[d];
+  return n;
+}
+// b repeats along out's leading dims: contiguous, and its shape (leading 1s dropped) equals
+// out's trailing dims
+static bool trailing_block(const Layout& out, const Layout& b) {
+  if (!b.contiguous) return false;
+  int lead = 0;
+  while (lead < b.dims - 1 && b.shape[lead] == 1) ++lead;
+  const int k = b.dims - lead;
+  if (k > out.dims) return false;
+  for (int j = 0; j < k; ++j)
+    if (b.shape[lead + j] != out.shape[out.dims - k + j]) return false;
+  return true;
+}
 static unsigned grid_for(int64_t n, int per_block = 256) {
   int64_t g = (n + per_block - 1) / per_block;
   if (g > 256 * 16) g = 256 * 16;
@@ -249,6 +337,58 @@ __global__ void rand_uniform_kernel(float* out, int64_t n, uint64_t seed) {
   }
 }
 
+// Fused feed-forward pieces of the minitorch step (reference minitorch/modules_transfomer.py
+// FeedForward, :233-277: dropout(linear_out(GELU(linear_in(x))))): the bias add of linear_in
+// with the tanh-form GELU (minitorch/nn.py GELU, torch approximate='tanh'), forward and
+// backward in one pass each, and dropout with its keep mask drawn from the counter-based
+// uniform above (u > p keeps, as rand(shape) > p does) and redrawn in the backward from the
+// same seed, so no mask is stored. Rows of `cols` contiguous floats; 16 B per lane where the
+// row length allows.
+__device__ __forceinline__ float gelu_tanh(float u, float& t, float& dt) {
+  constexpr float k = 0.7978845608028654f;  // sqrt(2 / pi)
+  const float u2 = u * u;
+  t = tanhf(k * (u + 0.044715f * (u2 * u)));
+  dt = k * (1.f + 3.f * 0.044715f * u2);   // d(inner)/du
+  return 0.5f * u * (1.f + t);
+}
+template <bool BW>
+__global__ __launch_bounds__(256) void bias_gelu_kernel(float* __restrict__ out, const float* __restrict__ x,
+                                                        const float* __restrict__ bias,
+                                                        const float* __restrict__ dy, int64_t n, int64_t cols,
+                                                        int vec) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  auto one = [&](float xv, float bv, float g) -> float {
+    float t, dt;
+    const float u = xv + bv;
+    const float y = gelu_tanh(u, t, dt);
+    if (!BW) return y;
+    // d/du 0.5 u (1 + t) = 0.5 (1 + t) + 0.5 u (1 - t^2) dt
+    return g * (0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * dt);
+  };
+  if (vec) {  // cols % 4 == 0, 16-B aligned rows
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += step) {
+      const float4 xv = ((const float4*)x)[i];
+      const float4 bv = ((const float4*)bias)[i % (cols / 4)];
+      const float4 g = BW ? ((const float4*)dy)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      ((float4*)out)[i] = make_float4(one(xv.x, bv.x, g.x), one(xv.y, bv.y, g.y), one(xv.z, bv.z, g.z),
+                                      one(xv.w, bv.w, g.w));
+    }
+    return;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step)
+    out[i] = one(x[i], bias[i % cols], BW ? dy[i] : 0.f);
+}
+
+__global__ __launch_bounds__(256) void dropout_kernel(float* __restrict__ out, const float* __restrict__ x,
+                                                      int64_t n, float p, float scale, uint64_t seed) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    const uint64_t h = mix64(seed + 0x9e3779b97f4a7c15ull * (uint64_t)(i + 1));
+    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    out[i] = u > p ? x[i] * scale : 0.f;
+  }
+}
+
 // Multi-tensor Adam (minitorch/optim.py Adam.step, reference minitorch/optim.py:52-75 with
 // the second moment on (1 - beta2)): for every element of every listed tensor
 //   m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g g;  p = p - step_size m / (sqrt(v) + eps)
@@ -273,7 +413,9 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 #pragma clang fp contract(off)
   m = m * a.b1 + g * a.c1;
   v = v * a.b2 + (g * g) * a.c2;
-  p = p - (a.step * m) / (__fsqrt_rn(v) + a.eps);
+  // the tensor-op form divides as a product with the reciprocal (Tensor.__truediv__ =
+  // Mul(a, Inv(b))) and takes the square root as PowerScalar's powf(v, 0.5)
+  p = p - (a.step * m) * (1.f / (powf(v, 0.5f) + a.eps));
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
@@ -314,8 +456,13 @@ int mt_tensor_map(int fn, float* out, const int64_t* out_shape, const int64_t* o
   for (int d = 0; d < out_dims; ++d) n *= out_shape[d];
   if (n == 0) return 0;
   const int same = ol.contiguous && il.contiguous && same_shape(ol, il);
-  hipLaunchKernelGGL(map_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, fn, out,
-                     ol, n, in, il, same);
+  hipStream_t st = (hipStream_t)stream;
+  if (same && (((uintptr_t)out | (uintptr_t)in) & 15) == 0)
+    hipLaunchKernelGGL(map_dense_kernel, dim3(grid_for(n % 4 ? n : n / 4)), dim3(256), 0, st, fn, out, n, in);
+  else if (fits_i32(n, {&ol, &il}))
+    hipLaunchKernelGGL(map_kernel<int>, dim3(grid_for(n)), dim3(256), 0, st, fn, out, ol, n, in, il, same);
+  else
+    hipLaunchKernelGGL(map_kernel<int64_t>, dim3(grid_for(n)), dim3(256), 0, st, fn, out, ol, n, in, il, same);
   return check_hip(hipGetLastError(), "mt_tensor_map");
 }
 
@@ -332,8 +479,37 @@ int mt_tensor_zip(int fn, float* out, const int64_t* out_shape, const int64_t* o
   if (n == 0) return 0;
   const int same = ol.contiguous && al.contiguous && bl.contiguous && same_shape(ol, al) &&
                    same_shape(ol, bl);
-  hipLaunchKernelGGL(zip_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, fn, out,
-                     ol, n, a, al, b, bl, same);
+  hipStream_t st = (hipStream_t)stream;
+  // dense fast paths: one operand the output's shape and contiguous, the other the same, a
+  // single element, or a contiguous block repeated along the leading dims (16-B aligned)
+  const bool aligned = (((uintptr_t)out | (uintptr_t)a | (uintptr_t)b) & 15) == 0;
+  const bool a_full = al.contiguous && same_shape(ol, al), b_full = bl.contiguous && same_shape(ol, bl);
+  const unsigned g4 = grid_for(n % 4 ? n : n / 4);
+  if (ol.contiguous && aligned && (a_full || b_full)) {
+    const float* x = a_full ? a : b;  // the full operand
+    const float* y = a_full ? b : a;
+    const Layout& yl = a_full ? bl : al;
+    const bool swap = !a_full;
+    const int64_t ny = numel(yl);
+    if (same) {
+      hipLaunchKernelGGL((zip_dense_kernel<0, false>), dim3(g4), dim3(256), 0, st, fn, out, n, a, b, n);
+      return check_hip(hipGetLastError(), "mt_tensor_zip");
+    }
+    if (ny == 1) {
+      if (swap) hipLaunchKernelGGL((zip_dense_kernel<1, true>), dim3(g4), dim3(256), 0, st, fn, out, n, x, y, ny);
+      else hipLaunchKernelGGL((zip_dense_kernel<1, false>), dim3(g4), dim3(256), 0, st, fn, out, n, x, y, ny);
+      return check_hip(hipGetLastError(), "mt_tensor_zip");
+    }
+    if (trailing_block(ol, yl)) {
+      if (swap) hipLaunchKernelGGL((zip_dense_kernel<2, true>), dim3(g4), dim3(256), 0, st, fn, out, n, x, y, ny);
+      else hipLaunchKernelGGL((zip_dense_kernel<2, false>), dim3(g4), dim3(256), 0, st, fn, out, n, x, y, ny);
+      return check_hip(hipGetLastError(), "mt_tensor_zip");
+    }
+  }
+  if (fits_i32(n, {&ol, &al, &bl}))
+    hipLaunchKernelGGL(zip_kernel<int>, dim3(grid_for(n)), dim3(256), 0, st, fn, out, ol, n, a, al, b, bl, same);
+  else
+    hipLaunchKernelGGL(zip_kernel<int64_t>, dim3(grid_for(n)), dim3(256), 0, st, fn, out, ol, n, a, al, b, bl, same);
   return check_hip(hipGetLastError(), "mt_tensor_zip");
 }
 
@@ -442,6 +618,34 @@ int mt_rand_uniform(float* out, int64_t n, uint64_t seed, void* stream) {
   hipLaunchKernelGGL(rand_uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                      out, n, seed);
   return check_hip(hipGetLastError(), "mt_rand_uniform");
+}
+
+int mt_bias_gelu_fw(float* out, const float* x, const float* bias, int64_t rows, int64_t cols, void* stream) {
+  if (rows < 0 || cols <= 0) return set_error("mt_bias_gelu_fw: bad sizes %lld x %lld", (long long)rows, (long long)cols);
+  const int64_t n = rows * cols;
+  if (n == 0) return 0;
+  const bool v4 = cols % 4 == 0 && ((((uintptr_t)out | (uintptr_t)x | (uintptr_t)bias) & 15) == 0);
+  hipLaunchKernelGGL(bias_gelu_kernel<false>, dim3(grid_for(v4 ? n / 4 : n)), dim3(256), 0, (hipStream_t)stream,
+                     out, x, bias, nullptr, n, cols, (int)v4);
+  return check_hip(hipGetLastError(), "mt_bias_gelu_fw");
+}
+
+int mt_bias_gelu_bw(float* dx, const float* dy, const float* x, const float* bias, int64_t rows, int64_t cols,
+                    void* stream) {
+  if (rows < 0 || cols <= 0) return set_error("mt_bias_gelu_bw: bad sizes %lld x %lld", (long long)rows, (long long)cols);
+  const int64_t n = rows * cols;
+  if (n == 0) return 0;
+  const bool v4 = cols % 4 == 0 && ((((uintptr_t)dx | (uintptr_t)dy | (uintptr_t)x | (uintptr_t)bias) & 15) == 0);
+  hipLaunchKernelGGL(bias_gelu_kernel<true>, dim3(grid_for(v4 ? n / 4 : n)), dim3(256), 0, (hipStream_t)stream,
+                     dx, x, bias, dy, n, cols, (int)v4);
+  return check_hip(hipGetLastError(), "mt_bias_gelu_bw");
+}
+
+int mt_dropout(float* out, const float* x, int64_t n, float p, float scale, uint64_t seed, void* stream) {
+  if (n < 0) return set_error("mt_dropout: n = %lld", (long long)n);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, x, n, p, scale, seed);
+  return check_hip(hipGetLastError(), "mt_dropout");
 }
 
 int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,

@@ -239,9 +239,15 @@ __device__ __forceinline__ void dq_ksteps(const bf16* kimg, const bf16* si, int 
 // PAIR (causal): a workgroup owns key blocks nkb - 1 - u (light: the fewest query steps) and
 // then u (heavy) of one head, so every workgroup walks about nkb + 1 blocks' worth of steps
 // (the split kernels' pairing, fa_bwd_bf16.hip); the two blocks are two passes of one body.
-template <bool CAUSAL, bool PAIR = false>
+// VAR (A/B forms of the dQ hand-off; the product runs 0): 1 no in-kernel reduction, 2 no
+// arrivals (both: wrong dQ, timing only), 4 plain instead of sc1 partial stores, 8 the arrival
+// add as a global atomic (its return register is not its data register), 16 the round-3 form
+// (plain stores, no arrivals, fa_bwd_dq_reduce after the pass).
+template <bool CAUSAL, bool PAIR = false, int VAR = 0>
 __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb, int nsa, int bh0,
                                                              int slab_off, int ws_bytes) {
+  constexpr bool R3 = VAR & 16;
+  constexpr bool NORED = (VAR & 1) || R3, NOARR = (VAR & 2) || R3, PLAIN = (VAR & 4) || R3, GATOM = VAR & 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
@@ -350,7 +356,8 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     bf16x8 o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) { o[i] = (bf16)acc[0][i]; o[4 + i] = (bf16)acc[1][i]; }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rsl, slab_w + (step0 + tl) * slab_step, 0, kSc1);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rsl, slab_w + (step0 + tl) * slab_step, 0,
+                                           PLAIN ? 0 : kSc1);
   };
   // Arrivals (wave 0; the add by lane 0): arrive(s) first settles the previous add, whose
   // return value the caller has waited for (the next step's vmcnt, or settle's own wait at the
@@ -369,9 +376,16 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     }
   };
   auto arrive = [&](int s) __attribute__((always_inline)) {
+    if (NOARR) return;
     if (wave == 0) {
       settle();
-      if (lane == 0) pend_old = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rsl, (bh * nsa + s) * 4, 0, 0);
+      if (lane == 0) {
+        if (GATOM)
+          pend_old = (int)__hip_atomic_fetch_add(p.dq_cnt + (int64_t)bh * nsa + s, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        else
+          pend_old = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rsl, (bh * nsa + s) * 4, 0, 0);
+      }
       pend_s = s;
     }
   };
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   // round-3 reduce kernel's arithmetic), from sc1 loads, eight 16-B loads in flight per lane.
   // Lane l holds d = 32 (w >> 2) + 4 (l >> 4) + 0..3 (+ 16) of query 64 s + 16 (w & 3) + (l & 15).
   __syncthreads();  // red[] is written
-  const int nr = red[0];
+  const int nr = NORED ? 0 : red[0];
   bf16* const dQh = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + 32 * (wave >> 2) + 4 * (lane >> 4);
   const float sc = p.scale;
   for (int i = 0; i < nr; ++i) {
@@ -512,12 +526,58 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     }
   }
   // a head whose keys are all padding (kv_len = 0): nothing arrives, its dQ is zero
-  if (nkv == 0 && kb == 0) {
+  if (!R3 && nkv == 0 && kb == 0) {
     bf16* dQz = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1];
     for (int r = tid >> 3; r < N; r += 64) *(uint4*)(dQz + (int64_t)r * p.sdq[2] + 8 * (tid & 7)) = uint4{0, 0, 0, 0};
   }
   }  // pass
 }
+
+#ifdef MT_DIAGNOSTICS
+// The round-3 reduce (VAR 16): dQ = scale · Σ_kb slab[bh][step][kb] in key-block order, one wave
+// per (bh, step, strip w), after the pass; the slab of the launch's heads, offsets as above.
+__global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, int nkb, int nsa, int bh0, int ngrp,
+                                                        int slab_off, int ws_bytes, int causal) {
+  const int lane = threadIdx.x & 63;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit >= (int64_t)ngrp * nsa * 8) return;
+  const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(p.dq_cnt, (short)0, ws_bytes, 0x00020000);
+  const int w = (int)(unit & 7);
+  const int64_t bs = unit >> 3;
+  const int s = (int)(bs % nsa);
+  const int bhl = (int)(bs / nsa), bh = bh0 + bhl;
+  const int q = s * kStep + 16 * (w & 3) + (lane & 15);
+  const int nkv = (kv_keys(p, bh / p.H) + kKB - 1) / kKB;
+  const int nk = min(nkv, causal ? min(nkb, s / (kKB / kStep) + 1) : nkb);
+  const int src = slab_off + ((bhl * nsa + s) * nkb * 8 + w) * 1024 + lane * 16;
+  float a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.f;
+  int k = 0;
+  for (; k + 8 <= nk; k += 8) {
+    u32x4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rsl, src + (k + u) * 8192, 0, 2);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bf16x8 y = __builtin_bit_cast(bf16x8, x[u]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] += (float)y[i];
+    }
+  }
+  for (; k < nk; ++k) {
+    const bf16x8 y = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsl, src + k * 8192, 0, 2));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += (float)y[i];
+  }
+  if (q >= p.N) return;
+  const int b = bh / p.H, hh = bh % p.H;
+  bf16* dst = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)q * p.sdq[2] + 32 * (w >> 2) + 4 * (lane >> 4);
+  const float sc = p.scale;
+  store4(dst, a[0] * sc, a[1] * sc, a[2] * sc, a[3] * sc, true);
+  store4(dst + 16, a[4] * sc, a[5] * sc, a[6] * sc, a[7] * sc, true);
+}
+#endif
 
 // The fused backward's workspace beyond the prep rows: the arrival counters ([B·H][nsa] u32,
 // 256-B padded) and the slab of one head group (at most kSlabCap bytes); 0 when a single
@@ -551,7 +611,15 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
   const int64_t grp = fused_group_heads(B, H, N);
   // causal: light/heavy pairs while the paired grid still has a workgroup per CU
   const bool pair = causal && (int64_t)((nkb + 1) / 2) * grp >= 256;
-  auto kfn = pair ? fa_bwd_fused_bf16<true, true> : causal ? fa_bwd_fused_bf16<true> : fa_bwd_fused_bf16<false>;
+  void (*kfn)(AttnArgs, int, int, int, int, int) =
+      pair ? fa_bwd_fused_bf16<true, true> : causal ? fa_bwd_fused_bf16<true> : fa_bwd_fused_bf16<false>;
+#ifdef MT_DIAGNOSTICS
+  // A/B forms of the dQ hand-off (MT_KNOB, see the kernel's VAR)
+#define MT_FVAR(V) \
+  if (a.knob == V) kfn = pair ? fa_bwd_fused_bf16<true, true, V> : causal ? fa_bwd_fused_bf16<true, false, V> : fa_bwd_fused_bf16<false, false, V>;
+  MT_FVAR(1) MT_FVAR(2) MT_FVAR(3) MT_FVAR(4) MT_FVAR(7) MT_FVAR(8) MT_FVAR(16)
+#undef MT_FVAR
+#endif
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kSmemAll);
   if (e != hipSuccess) return e;
   for (int64_t bh0 = 0; bh0 < B * H; bh0 += grp) {
@@ -563,6 +631,16 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
                        (int)(fused_counter_bytes(B, H, N) + ng * fused_head_slab(N)));
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+#ifdef MT_DIAGNOSTICS
+    if (a.knob == 16) {
+      const int64_t nunit = ng * nsa * 8;
+      hipLaunchKernelGGL(fa_bwd_dq_reduce, dim3((unsigned)((nunit + 3) / 4)), dim3(256), 0, st, a, nkb, nsa,
+                         (int)bh0, (int)ng, (int)fused_counter_bytes(B, H, N),
+                         (int)(fused_counter_bytes(B, H, N) + ng * fused_head_slab(N)), causal ? 1 : 0);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+#endif
   }
   return hipSuccess;
 }

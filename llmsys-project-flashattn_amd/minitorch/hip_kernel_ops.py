@@ -213,6 +213,36 @@ class HipKernelOps(TensorOps):
 
     # ---- fused kernels -------------------------------------------------------------------
     @staticmethod
+    def bias_gelu_fw(x: Tensor, bias: Tensor) -> Tensor:
+        """GELU_tanh(x + bias) over the rows of a 2-D x (FeedForward's linear_in bias + GELU,
+        reference modules_transfomer.py FeedForward) in one pass."""
+        x, b = _dense(x), _dense(bias)
+        rows, cols = x.shape
+        out = _out(x, (rows, cols))
+        _hip.check(_hip.lib().mt_bias_gelu_fw(_ptr(out), _ptr(x), _ptr(b), rows, cols, _stream()),
+                   "bias_gelu_fw")
+        return out
+
+    @staticmethod
+    def bias_gelu_bw(grad: Tensor, x: Tensor, bias: Tensor) -> Tensor:
+        g, x, b = _dense(grad), _dense(x), _dense(bias)
+        rows, cols = x.shape
+        dx = _out(x, (rows, cols))
+        _hip.check(_hip.lib().mt_bias_gelu_bw(_ptr(dx), _ptr(g), _ptr(x), _ptr(b), rows, cols, _stream()),
+                   "bias_gelu_bw")
+        return dx
+
+    @staticmethod
+    def dropout_fw(x: Tensor, p: float, scale: float, seed: int) -> Tensor:
+        """x * (u > p) * scale with u the device uniform draw of (seed, index) (the mask of
+        rand(shape) > p, never stored: the backward redraws it from the seed)."""
+        x = _dense(x)
+        out = _out(x, x.shape)
+        _hip.check(_hip.lib().mt_dropout(_ptr(out), _ptr(x), x.size, ctypes.c_float(p), ctypes.c_float(scale),
+                                         seed & 0xFFFFFFFFFFFFFFFF, _stream()), "dropout")
+        return out
+
+    @staticmethod
     def softmax_xent_fw(logits: Tensor, target: Tensor):
         """(loss[rows], lse[rows]) of the reference's softmax_loss (nn.py) in one pass."""
         x = _dense(logits)
@@ -237,7 +267,7 @@ class HipKernelOps(TensorOps):
     def attn_softmax_fw(inp: Tensor, mask: Optional[Tensor], mask_future: bool = False) -> Tensor:
         B, nh, T_from, T_to = inp.shape
         x = inp if inp._tensor.is_dense() else inp.contiguous()
-        out = x.zeros(x.shape)
+        out = _out(x, x.shape)  # the kernel writes every element
         mptr, ms = None, None
         if mask is not None:
             mshape = (1,) * (4 - mask.dims) + tuple(mask.shape)
@@ -253,7 +283,7 @@ class HipKernelOps(TensorOps):
         g = out_grad if out_grad._tensor.is_dense() else out_grad.contiguous()
         y = soft_inp if soft_inp._tensor.is_dense() else soft_inp.contiguous()
         rows = int(np.prod(y.shape[:-1]))
-        dinp = g.zeros(g.shape)
+        dinp = _out(g, g.shape)
         _hip.check(_hip.lib().mt_attn_softmax_bw(_ptr(dinp), _ptr(g), _ptr(y), rows, y.shape[-1],
                                                  _stream()), "attn_softmax_bw")
         return dinp, soft_inp
@@ -263,9 +293,9 @@ class HipKernelOps(TensorOps):
         x = inp if inp._tensor.is_dense() else inp.contiguous()
         rows, H = x.shape
         gm, bt = _dense(gamma), _dense(beta)  # held: their device buffers must outlive the launch
-        ln = x.zeros(x.shape)
-        var = x.zeros((rows,))
-        mean = x.zeros((rows,))
+        ln = _out(x, x.shape)
+        var = _out(x, (rows,))
+        mean = _out(x, (rows,))
         _hip.check(_hip.lib().mt_layernorm_fw(_ptr(ln), _ptr(var), _ptr(mean), _ptr(x),
                                               _ptr(gm), _ptr(bt),
                                               rows, H, _stream()), "layernorm_fw")
@@ -279,9 +309,9 @@ class HipKernelOps(TensorOps):
         x = inp if inp._tensor.is_dense() else inp.contiguous()
         rows, H = x.shape
         gm, bt = _dense(gamma), _dense(beta)
-        dx = x.zeros(x.shape)
-        dgamma = x.zeros((1, H))
-        dbeta = x.zeros((1, H))
+        dx = _out(x, x.shape)
+        dgamma = _out(x, (1, H))
+        dbeta = _out(x, (1, H))
         ws = torch.empty(max(1, _hip.lib().mt_layernorm_bw_workspace_bytes(rows, H) // 4),
                          dtype=torch.float32, device="cuda")
         _hip.check(_hip.lib().mt_layernorm_bw(_ptr(dgamma), _ptr(dbeta), _ptr(dx), _ptr(g), _ptr(x),

@@ -36,7 +36,11 @@ class Dropout(Module):
             return x
         # keep with probability 1 - p, scale by 1 / (1 - p) (reference modules_basic.py
         # Dropout, which draws the mask with np.random.binomial on the host); here the
-        # uniform draw is on the device when the backend has one
+        # uniform draw is on the device when the backend has one, and a backend with the fused
+        # kernel draws, masks and scales in one pass each way (DropoutMask)
+        if getattr(x.backend, "dropout_fw", None) is not None and x._tensor.on_device:
+            from .tensor_functions import DropoutMask
+            return DropoutMask.apply(x, x._const(self.p_dropout))
         keep = rand(x.shape, backend=x.backend) > self.p_dropout
         return (x * keep) / (1 - self.p_dropout)
 

@@ -115,7 +115,15 @@ class FeedForward(Module):
 
     def forward(self, x):
         batch_size, seq_len, n_embd = x.shape
-        h = GELU(self.linear_in(x.view(batch_size * seq_len, n_embd)))
+        flat = x.view(batch_size * seq_len, n_embd)
+        be = x.backend
+        if (getattr(be, "bias_gelu_fw", None) is not None and self.linear_in.bias is not None
+                and x._tensor.on_device):
+            # linear_in's bias add and the GELU as one kernel each way (BiasGelu)
+            from .tensor_functions import BiasGelu
+            h = BiasGelu.apply(flat @ self.linear_in.weights.value, self.linear_in.bias.value)
+        else:
+            h = GELU(self.linear_in(flat))
         return self.dropout(self.linear_out(h)).view(batch_size, seq_len, n_embd)
 
 

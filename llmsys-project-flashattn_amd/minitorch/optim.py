@@ -2,9 +2,11 @@
 ``(1 - beta1)`` for the second moment (optim.py:68); this one uses ``(1 - beta2)``.
 
 On the HIP backend, Adam updates every parameter whose value, gradient and moments are
-dense fp32 device buffers in one multi-tensor kernel (``mt_adam_step``, in place, the same
-arithmetic and order as the tensor-op form below); anything else takes the tensor-op form,
-which is also the CPU backend's path."""
+dense fp32 device buffers in one multi-tensor kernel (``mt_adam_step``): the same arithmetic
+and order as the tensor-op form below, bit for bit (tests/test_optim_gpu.py), but in place:
+the parameter's storage is updated (the tensor-op form gives ``p.value`` a new tensor) and
+``p.value.grad`` is left as it is (neither path clears it; call ``zero_grad``). Anything else
+takes the tensor-op form, which is also the CPU backend's path."""
 from __future__ import annotations
 
 import math

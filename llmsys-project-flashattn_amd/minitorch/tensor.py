@@ -32,6 +32,7 @@ class History:
 
 
 _tensor_count = 0
+_DEV_SCALARS: dict = {}  # (value, backend id) -> shared device constant (Tensor._ensure_tensor)
 
 
 class Tensor:
@@ -75,10 +76,18 @@ class Tensor:
     def _ensure_tensor(self, b: TensorLike) -> "Tensor":
         if isinstance(b, (int, float, np.floating, np.integer)):
             if self.backend.cuda:
-                # filled on the device (no synchronous host-to-device copy per scalar)
-                import torch
-                st = torch.full((1,), float(b), dtype=torch.float32, device="cuda")
-                return Tensor(TensorData(st, (1,)), backend=self.backend)
+                # one device-resident constant per value, filled once and then shared (no
+                # host-to-device copy and no fill launch per scalar operand; no kernel writes
+                # into an operand, and gradients are always fresh tensors or copies)
+                key = (float(b), id(self.backend))
+                c = _DEV_SCALARS.get(key)
+                if c is None:
+                    import torch
+                    st = torch.full((1,), float(b), dtype=torch.float32, device="cuda")
+                    c = Tensor(TensorData(st, (1,)), backend=self.backend)
+                    if len(_DEV_SCALARS) < 4096:
+                        _DEV_SCALARS[key] = c
+                return c
             return Tensor.make([float(b)], (1,), backend=self.backend)
         b._type_(self.backend)
         return b

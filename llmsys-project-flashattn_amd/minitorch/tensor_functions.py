@@ -255,6 +255,45 @@ class SoftmaxXent(Function):
         return logits.f.softmax_xent_bw(grad_output, logits, target, lse), 0.0
 
 
+class BiasGelu(Function):
+    """GELU_tanh(x + bias) for a 2-D x and a [cols] bias: FeedForward's linear_in bias add and
+    GELU (reference modules_transfomer.py FeedForward, nn.py GELU) as one backend kernel each
+    way; the bias gradient is the column sum of dx."""
+
+    @staticmethod
+    def forward(ctx, x, bias):
+        ctx.save_for_backward(x, bias)
+        return x.f.bias_gelu_fw(x, bias)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        x, bias = ctx.saved_values
+        dx = x.f.bias_gelu_bw(grad_output, x, bias)
+        db = x.f.add_reduce(dx, 0)
+        from .tensor import Tensor
+        return dx, Tensor.make(db._tensor._storage, bias.shape, backend=db.backend)
+
+
+class DropoutMask(Function):
+    """Dropout with the keep mask drawn on the device from a seed (keep = u > p, then scaled by
+    1 / (1 - p), reference modules_basic.py Dropout) in one kernel, and redrawn from the same
+    seed in the backward; p is a host constant, the seed comes from NumPy's global generator
+    (np.random.seed reproduces a run, as with rand())."""
+
+    @staticmethod
+    def forward(ctx, x, p):
+        rate = float(p.item())
+        seed = int(np.random.randint(0, 2**63 - 1, dtype=np.int64))
+        scale = float(np.float32(1.0) / np.float32(1.0 - rate))
+        ctx.save_for_backward(rate, scale, seed)
+        return x.f.dropout_fw(x, rate, scale, seed)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        rate, scale, seed = ctx.saved_values
+        return grad_output.f.dropout_fw(grad_output, rate, scale, seed), 0.0
+
+
 class View(Function):
     @staticmethod
     def forward(ctx, a, shape):
@@ -419,7 +458,11 @@ def rand(shape: UserShape, backend=None, requires_grad: bool = False):
     if getattr(backend, "rand_uniform", None) is not None:
         # device draw; the seed comes from NumPy's global generator so np.random.seed()
         # still makes a run reproducible
-        t = zeros(shape, backend=backend)
+        import torch
+        from .tensor import Tensor
+        size = int(np.prod(shape)) if shape else 1  # every element is drawn: no zero fill
+        t = Tensor(TensorData(torch.empty(size, dtype=torch.float32, device="cuda"), tuple(shape)),
+                   backend=backend)
         backend.rand_uniform(t, int(np.random.randint(0, 2**63 - 1, dtype=np.int64)))
         t.requires_grad_(requires_grad)
         return t

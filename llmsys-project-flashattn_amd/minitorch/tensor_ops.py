@@ -113,6 +113,10 @@ class TensorBackend:
         # fused softmax cross-entropy (optional: a backend without it keeps the composition)
         self.softmax_xent_fw = getattr(ops, "softmax_xent_fw", None)
         self.softmax_xent_bw = getattr(ops, "softmax_xent_bw", None)
+        # fused FeedForward pieces (optional: a backend without them keeps the compositions)
+        self.bias_gelu_fw = getattr(ops, "bias_gelu_fw", None)
+        self.bias_gelu_bw = getattr(ops, "bias_gelu_bw", None)
+        self.dropout_fw = getattr(ops, "dropout_fw", None)
         # fused kernels
         self.attn_softmax_fw = ops.attn_softmax_fw
         self.attn_softmax_bw = ops.attn_softmax_bw

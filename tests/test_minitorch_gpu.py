@@ -49,6 +49,98 @@ def test_generic_ops(mt):
     np.testing.assert_allclose(p.contiguous().to_numpy(), x.transpose(2, 0, 1))
 
 
+@pytest.mark.parametrize("case", ["same", "same_odd", "scalar_right", "scalar_left", "row_right",
+                                  "row_left", "row_odd", "col_bcast", "permuted", "offset_view"])
+def test_zip_map_paths(mt, case):
+    """Every mt_tensor_zip / mt_tensor_map dispatch path against NumPy: the dense 16-B forms
+    (same shape, one-element operand on either side, a contiguous block repeated along the
+    leading dims), their scalar tails (sizes not a multiple of 4), and the int32 strided
+    kernel (a column broadcast, a permuted operand, a view at an unaligned offset)."""
+    minitorch, B = mt
+    from minitorch.tensor import Tensor
+    from minitorch.tensor_data import TensorData
+    import torch
+    rng = np.random.default_rng(abs(hash(case)) % 2**31)
+    shp = (6, 5, 7) if case.endswith("odd") else (6, 5, 8)
+    x = rng.standard_normal(shp).astype(np.float32)
+    ybase = {"same": shp, "same_odd": shp, "scalar_right": (1,), "scalar_left": (1,),
+             "row_right": (8,), "row_left": (5, 8), "row_odd": (7,), "col_bcast": (6, 5, 1),
+             "permuted": (8, 5, 6), "offset_view": shp}[case]
+    y = rng.standard_normal(ybase).astype(np.float32) + 2.0
+    a, b = minitorch.tensor_from_numpy(x, B), minitorch.tensor_from_numpy(y, B)
+    if case == "permuted":
+        b, y = b.permute(2, 1, 0), y.transpose(2, 1, 0)
+    if case == "offset_view":  # storage offset by one float: not 16-B aligned
+        st = torch.from_numpy(np.concatenate([[0.0], y.ravel()]).astype(np.float32)).cuda()[1:]
+        b = Tensor(TensorData(st, shp), backend=B)
+    left = case.endswith("left")
+    for op, ref in ((lambda u, v: u * v, np.multiply), (lambda u, v: u + v, np.add),
+                    (lambda u, v: u < v, lambda u, v: (u < v).astype(np.float32))):
+        got = (op(b, a) if left else op(a, b)).to_numpy()
+        want = ref(y, x) if left else ref(x, y)
+        np.testing.assert_allclose(got, want, rtol=1e-6, atol=0)
+    np.testing.assert_allclose(b.exp().to_numpy(), np.exp(y), rtol=1e-6)
+    np.testing.assert_allclose(b.contiguous().to_numpy(), y)
+
+
+def test_bias_gelu_fused(mt):
+    """BiasGelu (one kernel each way) against the nn.GELU composition on the same backend and
+    against torch's tanh GELU: GELU(x + b), dx and db."""
+    import torch
+    minitorch, B = mt
+    from minitorch.tensor_functions import BiasGelu
+    rng = np.random.default_rng(11)
+    for rows, cols in ((4992, 256), (33, 7)):  # config 5's FeedForward; a ragged shape
+        x = rng.standard_normal((rows, cols)).astype(np.float32) * 2
+        bias = rng.standard_normal((cols,)).astype(np.float32)
+        g = rng.standard_normal((rows, cols)).astype(np.float32)
+        outs = []
+        for fused in (True, False):
+            tx = minitorch.tensor_from_numpy(x, B, requires_grad=True)
+            tb = minitorch.tensor_from_numpy(bias, B, requires_grad=True)
+            y = BiasGelu.apply(tx, tb) if fused else minitorch.nn.GELU(tx + tb)
+            (y * minitorch.tensor_from_numpy(g, B)).sum().backward()
+            outs.append((y.to_numpy(), tx.grad.to_numpy(), tb.grad.to_numpy().reshape(cols)))
+        for f, c in zip(outs[0], outs[1]):
+            np.testing.assert_allclose(f, c, rtol=1e-5, atol=2e-5)
+        tt = torch.tensor(x, requires_grad=True)
+        tbb = torch.tensor(bias, requires_grad=True)
+        yt = torch.nn.functional.gelu(tt + tbb, approximate="tanh")
+        (yt * torch.tensor(g)).sum().backward()
+        np.testing.assert_allclose(outs[0][0], yt.detach().numpy(), rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(outs[0][1], tt.grad.numpy(), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(outs[0][2], tbb.grad.numpy(), rtol=1e-4, atol=1e-3)
+
+
+def test_dropout_fused(mt):
+    """DropoutMask: keeps ~(1 - p), scales by 1/(1 - p), the mask is mt_rand_uniform's draw of
+    the same seed (u > p), and the backward applies the same mask (redrawn, not stored)."""
+    minitorch, B = mt
+    from minitorch.tensor_functions import DropoutMask
+    rng = np.random.default_rng(12)
+    x = (rng.standard_normal((128, 39, 256)).astype(np.float32) + 3.0)
+    tx = minitorch.tensor_from_numpy(x, B, requires_grad=True)
+    np.random.seed(5)
+    y = DropoutMask.apply(tx, tx._const(0.1))
+    g = rng.standard_normal(x.shape).astype(np.float32)
+    (y * minitorch.tensor_from_numpy(g, B)).sum().backward()
+    yn, dx = y.to_numpy(), tx.grad.to_numpy()
+    kept = yn != 0
+    assert abs(kept.mean() - 0.9) < 0.005
+    scale = np.float32(1.0) / np.float32(0.9)
+    np.testing.assert_array_equal(yn[kept], x[kept] * scale)
+    np.testing.assert_array_equal(dx, np.where(kept, g * scale, 0.0).astype(np.float32))
+    # the same seed through the standalone uniform draw gives the same mask
+    np.random.seed(5)
+    seed = int(np.random.randint(0, 2**63 - 1, dtype=np.int64))
+    u = minitorch.zeros(x.shape, backend=B)
+    B.rand_uniform(u, seed)
+    np.testing.assert_array_equal(u.to_numpy() > 0.1, kept)
+    # the module uses it on the HIP backend
+    drop = minitorch.Dropout(0.25)
+    assert abs((drop(minitorch.tensor_from_numpy(x, B)).to_numpy() != 0).mean() - 0.75) < 0.005
+
+
 def test_one_hot_and_softmax_loss(mt):
     """nn.one_hot (device broadcast ==) equals the reference's np.eye(C)[idx]
     (minitorch/nn.py:212-222), and softmax_loss equals log-sum-exp minus the picked logit."""
