@@ -126,6 +126,9 @@ enum : int {
   // 143 = 142 with two 4-wave halves per workgroup, each walking its own light / heavy pair of
   // 256-query blocks (N % 1024 == 0)
   kPolV6CausalDual = 143,
+  // diagnostics: 140 with in-kernel s_memtime stamps per phase of the tile loop (the sums go to
+  // the mt_diag_set_debug_buffer buffer; timing-perturbing, read the shares only)
+  kPolV6Stamp = 144,
 };
 static const int kProductPolicies[] = {kPolDefault, kPolGeneric, kPolBwdFused, kPolBwdSplit};
 #ifdef MT_DIAGNOSTICS
@@ -137,9 +140,14 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal, kPolV6Wide, kPolV6SplitWide, kPolV6CausalWide, kPolV6CausalDual};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal, kPolV6Wide, kPolV6SplitWide, kPolV6CausalWide, kPolV6CausalDual, kPolV6Stamp};
 #endif
 static std::atomic<int> g_kernel_policy{kPolDefault};
+#ifdef MT_DIAGNOSTICS
+// the stamp buffer of the instrumented forward (policy 144), set by scripts/stamp_fwd.py
+static unsigned long long* g_dbg = nullptr;
+extern "C" void mt_diag_set_debug_buffer(void* p) { g_dbg = (unsigned long long*)p; }
+#endif
 
 static bool policy_valid(int p) {
   for (int v : kProductPolicies)
@@ -246,6 +254,12 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
     case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
     case kPolV6Wide: e = launch_fwd_v6(a, causal, 66, st, handled); break;
+    case kPolV6Stamp: {
+      AttnArgs as = a;
+      as.dbg = g_dbg;
+      if (g_dbg && !causal) e = launch_fwd_v6(as, false, 66 | 1024, st, handled);
+      break;
+    }
     case kPolV6SplitWide: e = launch_fwd_v6(a, causal, 82, st, handled); break;
     case kPolV6CausalWide:
       if (causal) e = launch_fwd_v6(a, true, 98, st, handled);

@@ -211,6 +211,44 @@ __global__ __launch_bounds__(256) void reduce_thread_kernel(int fn, float* out, 
   }
 }
 
+// Reduction over a non-innermost dim of a dense tensor viewed as [outer][len][inner] (the
+// bias gradients: column sums of [rows, cols] activations, e.g. the LM head's 4992 x 10000):
+// one 1024-thread workgroup per 64 consecutive inner indices, 16 row groups strided over len
+// (each wave reads 64 consecutive floats of a row: coalesced), then the 16 partial results
+// folded in row-group order through LDS. The wave-per-output kernel above read these columns
+// with a 4-byte access per lane at a stride of `inner` (300 µs for the LM head bias).
+__global__ __launch_bounds__(1024) void reduce_cols_kernel(int fn, float* __restrict__ out,
+                                                           const float* __restrict__ a, int64_t len,
+                                                           int64_t inner, float start) {
+  __shared__ float part[16][64];
+  __shared__ int have_s[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + tx;
+  const float* src = a + (int64_t)blockIdx.y * len * inner + i;
+  float acc = 0.f;
+  bool have = false;
+  if (i < inner) {
+    for (int64_t j = ty; j < len; j += 16) {
+      const float x = src[j * inner];
+      acc = have ? apply_fn(fn, acc, x) : x;
+      have = true;
+    }
+  }
+  part[ty][tx] = acc;
+  have_s[ty][tx] = have;
+  __syncthreads();
+  if (ty == 0 && i < inner) {
+    float r = 0.f;
+    bool hr = false;
+    for (int k = 0; k < 16; ++k) {
+      if (!have_s[k][tx]) continue;
+      r = hr ? apply_fn(fn, r, part[k][tx]) : part[k][tx];
+      hr = true;
+    }
+    out[(int64_t)blockIdx.y * inner + i] = hr ? apply_fn(fn, start, r) : start;
+  }
+}
+
 // Batched GEMM C[b] = A[b] @ B[b], fp32, exact fp32 MFMA. A: [M,K], B: [K,N], C: [M,N],
 // arbitrary element strides; batch stride 0 broadcasts. 64x64 output tile per 256-thread
 // workgroup (4 waves, 32x32 each), K staged 16 at a time through LDS.
@@ -523,7 +561,13 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   int64_t n = 1;
   for (int d = 0; d < dims; ++d) n *= out_shape[d];
   if (n == 0) return 0;
-  if (a_shape[reduce_dim] >= 64) {
+  int64_t inner = 1, outer = 1;
+  for (int d = reduce_dim + 1; d < dims; ++d) inner *= a_shape[d];
+  for (int d = 0; d < reduce_dim; ++d) outer *= a_shape[d];
+  if (al.contiguous && ol.contiguous && inner >= 16 && a_shape[reduce_dim] >= 16 && outer <= 65535) {
+    hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)((inner + 63) / 64), (unsigned)outer), dim3(1024), 0,
+                       (hipStream_t)stream, fn, out, a, a_shape[reduce_dim], inner, start);
+  } else if (a_shape[reduce_dim] >= 64) {
     hipLaunchKernelGGL(reduce_wave_kernel, dim3(grid_for(n, 4)), dim3(256), 0,
                        (hipStream_t)stream, fn, out, ol, n, a, al, reduce_dim, start);
   } else {

@@ -70,6 +70,8 @@ constexpr int kSmemAll = kSmemFused + (kMaxRed + 4) * 4;  // + the pass's list o
 static_assert(kSmemAll <= 160 * 1024, "LDS budget");
 constexpr int kSc1 = 16;                            // buffer cache policy bits: sc1
 constexpr int64_t kSlabCap = (int64_t)1 << 30;      // dQ partial bytes per launch (C3: exactly 1 GiB)
+// the product's dQ hand-off form (the kernel's VAR): 0 the in-kernel last-arriver reduce
+constexpr int kFusedForm = 0;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 static_assert(kSub % 16 == 0, "16-B aligned sub-tiles");
 
@@ -242,12 +244,16 @@ __device__ __forceinline__ void dq_ksteps(const bf16* kimg, const bf16* si, int 
 // VAR (A/B forms of the dQ hand-off; the product runs 0): 1 no in-kernel reduction, 2 no
 // arrivals (both: wrong dQ, timing only), 4 plain instead of sc1 partial stores, 8 the arrival
 // add as a global atomic (its return register is not its data register), 16 the round-3 form
-// (plain stores, no arrivals, fa_bwd_dq_reduce after the pass).
+// (plain stores, no arrivals, fa_bwd_dq_reduce after the pass), 32 rotated walks (non-causal,
+// no masked steps: key block kb starts its walk over the query steps at kb·nstep/nkb, so the
+// blocks of a head pass any given step at evenly spread times and each arrives last at about
+// nstep/nkb steps, instead of the head's slowest block arriving last almost everywhere).
 template <bool CAUSAL, bool PAIR = false, int VAR = 0>
 __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb, int nsa, int bh0,
                                                              int slab_off, int ws_bytes) {
   constexpr bool R3 = VAR & 16;
   constexpr bool NORED = (VAR & 1) || R3, NOARR = (VAR & 2) || R3, PLAIN = (VAR & 4) || R3, GATOM = VAR & 8;
+  constexpr bool ROT = (VAR & 32) && !CAUSAL;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
@@ -334,8 +340,15 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   const int step0 = qt0 / kStep;
   // a block of padding keys only (k0 >= Nk) stores zero dK / dV and no dQ partials
   const int nstep = N > qt0 && k0 < Nk ? (N - qt0 + kStep - 1) / kStep : 0;
+  // the walk: local step t covers query step step0 + sq(t); rotated only where every step is
+  // mask-free (N % 64 == 0, no padding keys in the head)
+  const int rot = ROT && N % kStep == 0 && Nk == N ? (kb * nstep) / nkb : 0;
+  auto sq = [&](int t) __attribute__((always_inline)) {
+    const int r = t + rot;
+    return r >= nstep ? r - nstep : r;
+  };
   auto stage = [&](int t, int slot) __attribute__((always_inline)) {
-    const int qs = qt0 + t * kStep + wu * kQT;
+    const int qs = qt0 + sq(t) * kStep + wu * kQT;
     const uint32_t img = lds0 + slot * 2 * kSub;
     dma_rows(img, rq, gq + qs * sqn * 2);
     dma_rows(img + kImg * 2, ro, go + qs * son * 2);
@@ -410,7 +423,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   const int nfull = min(nstep, max(nhead, (N - qt0) / kStep));
 #define FSUB(MASK_, SLOT_, T_, U_)                                                       \
   {                                                                                      \
-    const int qt_ = qt0 + (T_) * kStep + (U_) * kQT;                                     \
+    const int qt_ = qt0 + sq(T_) * kStep + (U_) * kQT;                                   \
     bf16* dsr_ = dsrow0 + (SLOT_) * (kKB * kStep);                                       \
     fdkv_tile<CAUSAL, MASK_, kPF && !(MASK_)>(smem + (2 * (SLOT_) + (U_)) * kSub, c, dK, dV, c2, qt_, N,  \
                              Nk, my_k, hf, dsr_, fk, U_);                                \
@@ -426,10 +439,10 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     FSUB(MASK_, SLOT_, t_, 0)                                                            \
     if (DQ_) dq_ksteps<4, 8, kPF && !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);             \
     FSUB(MASK_, SLOT_, t_, 1)                                                            \
-    if (DQ_) dq_store(qa_, t_ - 1);                                                      \
+    if (DQ_) dq_store(qa_, sq(t_ - 1));                                                  \
     if (more_ || (DQ_)) publish(DQ_);  /* DQ_: the store of step t - 2 has completed */  \
     __syncthreads();                                                                     \
-    if (t_ >= 2) arrive(step0 + t_ - 2);                                                 \
+    if (t_ >= 2) arrive(step0 + sq(t_ - 2));                                             \
   }
   if (nstep > 0) {
     if (nhead > 0 || nfull == 0) FSTEP(true, 0, 0, false) else FSTEP(false, 0, 0, false)
@@ -459,13 +472,13 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     f32x4 qa[2] = {f32x4{}, f32x4{}};
     dq_ksteps<0, 4, kPF>(kimg, dsimg + ((nstep - 1) & 1) * (kKB * kStep), oa0, oa1, ob, qa);
     dq_ksteps<4, 8, kPF>(kimg, dsimg + ((nstep - 1) & 1) * (kKB * kStep), oa0, oa1, ob, qa);
-    dq_store(qa, nstep - 1);
+    dq_store(qa, sq(nstep - 1));
   }
   // the last two steps' arrivals: every wave's stores complete, the barrier, the adds
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (nstep >= 2) arrive(step0 + nstep - 2);
-  if (nstep >= 1) arrive(step0 + nstep - 1);
+  if (nstep >= 2) arrive(step0 + sq(nstep - 2));
+  if (nstep >= 1) arrive(step0 + sq(nstep - 1));
   if (wave == 0) {
     settle();
     if (lane == 0) red[0] = nred;
@@ -533,7 +546,6 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   }  // pass
 }
 
-#ifdef MT_DIAGNOSTICS
 // The round-3 reduce (VAR 16): dQ = scale · Σ_kb slab[bh][step][kb] in key-block order, one wave
 // per (bh, step, strip w), after the pass; the slab of the launch's heads, offsets as above.
 __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, int nkb, int nsa, int bh0, int ngrp,
@@ -577,7 +589,6 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, int nkb, int
   store4(dst, a[0] * sc, a[1] * sc, a[2] * sc, a[3] * sc, true);
   store4(dst + 16, a[4] * sc, a[5] * sc, a[6] * sc, a[7] * sc, true);
 }
-#endif
 
 // The fused backward's workspace beyond the prep rows: the arrival counters ([B·H][nsa] u32,
 // 256-B padded) and the slab of one head group (at most kSlabCap bytes); 0 when a single
@@ -611,13 +622,17 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
   const int64_t grp = fused_group_heads(B, H, N);
   // causal: light/heavy pairs while the paired grid still has a workgroup per CU
   const bool pair = causal && (int64_t)((nkb + 1) / 2) * grp >= 256;
+  // the product form (kFusedForm, an A/B form of the kernel's VAR)
   void (*kfn)(AttnArgs, int, int, int, int, int) =
-      pair ? fa_bwd_fused_bf16<true, true> : causal ? fa_bwd_fused_bf16<true> : fa_bwd_fused_bf16<false>;
+      pair ? fa_bwd_fused_bf16<true, true, kFusedForm> : causal ? fa_bwd_fused_bf16<true, false, kFusedForm>
+           : fa_bwd_fused_bf16<false, false, kFusedForm>;
+  int form = kFusedForm;
 #ifdef MT_DIAGNOSTICS
   // A/B forms of the dQ hand-off (MT_KNOB, see the kernel's VAR)
 #define MT_FVAR(V) \
-  if (a.knob == V) kfn = pair ? fa_bwd_fused_bf16<true, true, V> : causal ? fa_bwd_fused_bf16<true, false, V> : fa_bwd_fused_bf16<false, false, V>;
-  MT_FVAR(1) MT_FVAR(2) MT_FVAR(3) MT_FVAR(4) MT_FVAR(7) MT_FVAR(8) MT_FVAR(16)
+  if (a.knob == V) { kfn = pair ? fa_bwd_fused_bf16<true, true, V> : causal ? fa_bwd_fused_bf16<true, false, V> : fa_bwd_fused_bf16<false, false, V>; form = V; }
+  MT_FVAR(1) MT_FVAR(2) MT_FVAR(3) MT_FVAR(4) MT_FVAR(7) MT_FVAR(8) MT_FVAR(16) MT_FVAR(32) MT_FVAR(40)
+  MT_FVAR(33)
 #undef MT_FVAR
 #endif
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kSmemAll);
@@ -631,8 +646,7 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
                        (int)(fused_counter_bytes(B, H, N) + ng * fused_head_slab(N)));
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-#ifdef MT_DIAGNOSTICS
-    if (a.knob == 16) {
+    if (form & 16) {
       const int64_t nunit = ng * nsa * 8;
       hipLaunchKernelGGL(fa_bwd_dq_reduce, dim3((unsigned)((nunit + 3) / 4)), dim3(256), 0, st, a, nkb, nsa,
                          (int)bh0, (int)ng, (int)fused_counter_bytes(B, H, N),
@@ -640,7 +654,6 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
       e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
-#endif
   }
   return hipSuccess;
 }

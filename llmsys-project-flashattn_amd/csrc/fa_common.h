@@ -197,6 +197,7 @@ struct AttnArgs {
   const int* kv_len;               // [B] valid keys per batch row (keys >= kv_len masked), or null
   int o_f32;                       // bf16 forward: O is fp32 (MT_BF16_F32OUT), else O has the input type
   int knob;                        // A/B schedule knob (diagnostics build: env MT_KNOB; product: 0)
+  unsigned long long* dbg;         // diagnostics build: in-kernel stamp sums (never an output)
   int64_t sq[3], sk[3], sv[3], so[3], sdo[3], sdq[3], sdk[3], sdv[3];  // (b, h, n)
   int B, H, N, d;
   float scale;       // 1/sqrt(d)

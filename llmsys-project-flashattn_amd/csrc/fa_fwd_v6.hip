@@ -266,6 +266,9 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // significant bits instead of 8) for the PV and row-sum MFMAs, which takes the rounding
   // of P, the error that dominates rows with few keys, down 8x
   constexpr bool H = VAR & 512;
+  // diagnostics (VAR 1024): s_memtime stamps at the phase boundaries of the bulk loop; per wave
+  // the cycle sums of [DMA issue, P1, P2, P3, P4, vmcnt(0), barrier] go to p.dbg
+  constexpr bool STAMP = VAR & 1024;
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   static_assert(!DUAL || CAUSAL, "dual halves: causal");
   static_assert(!H || (CAUSAL && !DUAL && !PS && RS && !EV), "fp16 PV: the causal default form");
@@ -455,8 +458,19 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     // stages K(t + 2) and V(t + 1). Unrolled by the K ring size (slot offsets immediate).
     // H: V(t + 2) is staged (4-slot V ring) and V(t + 1), landed by the previous tile's
     // barrier, is converted to fp16 beside P1 (read before it, written after it).
+    unsigned long long seg[7] = {0, 0, 0, 0, 0, 0, 0}, tprev = 0;
+    auto stamp = [&](int k) __attribute__((always_inline)) {
+      if (!STAMP) return;
+      unsigned long long tnow;
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tnow) :: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (k >= 0) seg[k] += tnow - tprev;
+      tprev = tnow;
+    };
     auto iter = [&](int t, int s0) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
+      stamp(-1);
       dma_k(sK + ((s0 + 2) & 3) * TILE, (t + 2) * ktile_b);
       if (H) dma_v(sV + ((s0 + 2) & 3) * TILE, (t + 2) * vtile_b);
       else dma_v(sV + ((s0 + 1) & 1) * TILE, (t + 1) * vtile_b);
@@ -471,13 +485,20 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       }
 #pragma unroll
       for (int db = 0; db < 4; ++db) vv[db] = vo[db] + vsl;
+      stamp(0);
       qk6<true, PS, RS, EV, H>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
       if (H) vcvt_write(sV + ((s0 + 1) & 3) * TILE, tid, vraw);
+      stamp(1);
       pv6<true, K1, PS, RS, EV, H>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
+      stamp(2);
       qk6<true, PS, RS, EV, H>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
+      stamp(3);
       pv6<true, K2, PS, RS, EV, H>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
+      stamp(4);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp(5);
       if (!NOBAR) __syncthreads();
+      stamp(6);
     };
     int t = 0;
     for (; t + 4 < nbulk; t += 4) {
@@ -502,6 +523,12 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       f32x2 d2[2];
       Pf6 dpf;
       pv6<false, K2, PS, RS, false, H>(sV, vv, OA, pA0, pA1, SA, 0, c2, nmcA, d2, dpf, vk, RA);
+    }
+    if (STAMP && lane == 0) {
+      unsigned long long* o = p.dbg + ((int64_t)blockIdx.x * kNW + wave) * 8;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) o[k] = seg[k];
+      o[7] = (unsigned long long)max(nbulk - 1, 0);
     }
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
@@ -740,6 +767,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 610: kern = fa_fwd_bf16_v6<610>; break;  // 98 with fp16 PV (the fp32-output causal default)
 #ifdef MT_DIAGNOSTICS
     case 354: kern = fa_fwd_bf16_v6<354>; break;
+    case 1090: kern = fa_fwd_bf16_v6<1090>; break;  // 66 with stamps
     case 194: kern = fa_fwd_bf16_v6<194>; break;
     case 2: kern = fa_fwd_bf16_v6<2>; break;
     case 34: kern = fa_fwd_bf16_v6<34>; break;

@@ -88,6 +88,20 @@ def _torch_view(t: Tensor):
     return torch.as_strided(st, t.shape, t._tensor.strides)
 
 
+def _layout_like(t: Tensor) -> tuple:
+    """Strides of a dense buffer of t's shape whose dims are laid out in t's stride order
+    (outermost = largest stride; ties keep the dim order): t's own layout when t is a
+    permutation of a dense tensor, row-major when t is dense."""
+    shape, st = t.shape, t._tensor.strides
+    order = sorted(range(len(shape)), key=lambda i: (-st[i], i))
+    out = [0] * len(shape)
+    acc = 1
+    for i in reversed(order):
+        out[i] = acc
+        acc *= shape[i]
+    return tuple(out)
+
+
 def _wrap(storage, shape, backend, strides=None) -> Tensor:
     return Tensor(TensorData(storage, tuple(shape), strides), backend=backend)
 
@@ -331,29 +345,36 @@ class HipKernelOps(TensorOps):
 
     @staticmethod
     def _flash_fw(Q: Tensor, K: Tensor, V: Tensor, causal: bool, kv_len=None):
+        """O is laid out like Q's storage: for MultiHeadAttention's permuted projection views
+        ([B,N,H,d] storage seen as [B,H,N,d]) O's storage is [B,N,H,d] too, so the block's
+        ``O.permute(0, 2, 1, 3).contiguous()`` is a view, not a copy (the kernels take strides)."""
         import torch
         B, H, N, d = Q.shape
         backend = Q.backend
+        so = _layout_like(Q)
         o = torch.empty(B * H * N * d, dtype=torch.float32, device="cuda")
         m = torch.empty(B * H * N, dtype=torch.float32, device="cuda")
         l = torch.empty(B * H * N, dtype=torch.float32, device="cuda")
         _hip.flash_fwd(_torch_view(Q), _torch_view(K), _torch_view(V), causal,
-                       out=o.view(B, H, N, d), m=m.view(B, H, N), l=l.view(B, H, N),
+                       out=torch.as_strided(o, (B, H, N, d), so), m=m.view(B, H, N), l=l.view(B, H, N),
                        kv_len=HipKernelOps._kv(kv_len))
-        return (_wrap(o, (B, H, N, d), backend), _wrap(m, (B, H, N), backend),
+        return (_wrap(o, (B, H, N, d), backend, so), _wrap(m, (B, H, N), backend),
                 _wrap(l, (B, H, N), backend))
 
     @staticmethod
     def _flash_bw(Q, K, V, O, dO, m, l, causal: bool, kv_len=None):
+        """dQ, dK, dV laid out like Q, K, V: the permuted projection views' gradients flow back
+        through Permute and View with no contiguous copy."""
         import torch
         B, H, N, d = Q.shape
         backend = Q.backend
+        lay = [_layout_like(t) for t in (Q, K, V)]
         bufs = [torch.empty(B * H * N * d, dtype=torch.float32, device="cuda") for _ in range(3)]
+        g = [torch.as_strided(b, (B, H, N, d), s) for b, s in zip(bufs, lay)]
         _hip.flash_bwd(_torch_view(Q), _torch_view(K), _torch_view(V), _torch_view(O),
                        _torch_view(dO), _torch_view(m), _torch_view(l), causal,
-                       dq=bufs[0].view(B, H, N, d), dk=bufs[1].view(B, H, N, d),
-                       dv=bufs[2].view(B, H, N, d), kv_len=HipKernelOps._kv(kv_len))
-        return tuple(_wrap(b, (B, H, N, d), backend) for b in bufs)
+                       dq=g[0], dk=g[1], dv=g[2], kv_len=HipKernelOps._kv(kv_len))
+        return tuple(_wrap(b, (B, H, N, d), backend, s) for b, s in zip(bufs, lay))
 
     # reference cuda_kernel_ops.py:605-892; kv_len (optional keyword, [B] valid key counts):
     # key padding through mt_flash_attn_*_varlen

@@ -196,6 +196,10 @@ class Tensor:
                                             backend=self.backend, device=False))
 
     def contiguous(self) -> "Tensor":
+        # already row-major: the tensor itself (a copy would change nothing but cost a launch
+        # and a buffer on the device backend)
+        if self._tensor.is_dense():
+            return self
         return Copy.apply(self)
 
     def __repr__(self) -> str:

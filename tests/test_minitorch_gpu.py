@@ -83,6 +83,20 @@ def test_zip_map_paths(mt, case):
     np.testing.assert_allclose(b.contiguous().to_numpy(), y)
 
 
+@pytest.mark.parametrize("shape,dim", [((4992, 256), 0), ((300, 10000), 0), ((3, 40, 70), 1),
+                                       ((17, 33), 0), ((50, 64, 1), 0)])
+def test_reduce_paths(mt, shape, dim):
+    """Sum and max over a non-innermost dim (the coalesced column kernel where the layout
+    allows: bias gradients) and the other reduce kernels, against NumPy."""
+    minitorch, B = mt
+    rng = np.random.default_rng(sum(shape) + dim)
+    x = rng.standard_normal(shape).astype(np.float32)
+    t = minitorch.tensor_from_numpy(x, B)
+    np.testing.assert_allclose(t.sum(dim).to_numpy(), x.sum(dim, keepdims=True), rtol=1e-4,
+                               atol=1e-4 * np.sqrt(shape[dim]))
+    np.testing.assert_array_equal(minitorch.max(t, dim).to_numpy(), x.max(dim, keepdims=True))
+
+
 def test_bias_gelu_fused(mt):
     """BiasGelu (one kernel each way) against the nn.GELU composition on the same backend and
     against torch's tanh GELU: GELU(x + b), dx and db."""
