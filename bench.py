@@ -420,6 +420,21 @@ def extra_legs(torch, _hip, time_fn):
     extra["bwd_causal_ms"] = round(bwdc_ms, 4)
     extra["bwd_causal_tflops"] = round(2.5 * fwd_flops(B, H, N, d, True) / (bwdc_ms * 1e-3) / 1e12, 2)
     del q, k, v, do, o, m, l, dq, dk, dv, ws
+    # the d = 128 bf16 backward (config 4's head dim) at (8,16,4096,128), FA-2 convention
+    s128 = (8, 16, 4096, 128)
+    q, k, v, do = (make_shard(torch, s128, 0, torch.bfloat16, s, "cuda") for s in (12, 13, 14, 15))
+    o = torch.empty_like(q)
+    m = torch.empty(s128[:3], dtype=torch.float32, device="cuda")
+    l = torch.empty_like(m)
+    ws = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(*s128) // 4 + 64, dtype=torch.float32,
+                     device="cuda")
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
+    for c_, tag in ((False, ""), (True, "_causal")):
+        _hip.flash_fwd(q, k, v, c_, out=o, m=m, l=l)
+        ms_ = time_fn(lambda: _hip.flash_bwd(q, k, v, o, do, m, l, c_, dq=dq, dk=dk, dv=dv, workspace=ws), 5, 2)
+        extra[f"bwd_d128{tag}_ms"] = round(ms_, 4)
+        extra[f"bwd_d128{tag}_tflops"] = round(2.5 * fwd_flops(*s128, c_) / (ms_ * 1e-3) / 1e12, 2)
+    del q, k, v, do, o, m, l, dq, dk, dv, ws
     # config 2: (8,16,1024,64) fp32 forward, and the fp32 backward minitorch's MHA runs
     # (the reference's own precision)
     c2 = (8, 16, 1024, 64)

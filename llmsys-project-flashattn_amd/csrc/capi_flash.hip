@@ -616,7 +616,8 @@ int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k
   // key padding (kv_len): the fused bf16 d = 64 kernel or the generic / ring kernels, which
   // mask keys >= kv_len[b] (the split bf16 kernels do not: policy 121 with kv_len runs the
   // generic kernels)
-  if (dtype == MT_BF16 && vec && pol != kPolGeneric && (!kv_len || (a.slab && pol != kPolBwdSplit))) {
+  if (dtype == MT_BF16 && vec && pol != kPolGeneric && (!kv_len || (a.slab && pol != kPolBwdSplit)) &&
+      (d == 64 || (d == 128 && !kv_len))) {
     bool handled = false;
     // 20: the fused backward (dQ in the dK/dV pass, fa_bwd_fused.hip), wherever it applies
     // (d = 64, N <= 46340) and kFusedBwdDefault says so; else the split forms.

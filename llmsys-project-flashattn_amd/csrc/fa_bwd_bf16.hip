@@ -30,17 +30,20 @@ using namespace bwdbf16;
 // rows per lane group (all loads issued first: with one row per 32-row workgroup the
 // C3 prep ran 16384 tiny workgroups at ≈2.2 TB/s).
 constexpr int kPrepRows = 4;
-// grid (ceil(N / (32 kPrepRows)), B·H): the head from blockIdx.y, no 64-bit division per row
-// (the 1-D form divided each row index by N and H)
+// grid (ceil(N / (RPP kPrepRows)), B·H): the head from blockIdx.y, no 64-bit division per row
+// (the 1-D form divided each row index by N and H). DH = 64 (8 lanes per row, RPP = 32 rows per
+// pass) or 128 (16 lanes, 16 rows: the d = 128 backward, fa_bwd_d128.hip).
+template <int DH = 64>
 __global__ __launch_bounds__(256) void fa_bwd_prep_bf16(AttnArgs p) {
+  constexpr int LPR = DH / 8, RPP = 256 / LPR;
   const int bh = blockIdx.y;
   const int b = bh / p.H, hh = bh % p.H;
   if (p.dq_cnt && blockIdx.x == 0) {  // the fused backward's arrival counters of this head
     const int nsa = (p.N + 63) / 64;
     for (int i = threadIdx.x; i < nsa; i += 256) p.dq_cnt[(int64_t)bh * nsa + i] = 0u;
   }
-  const int n0 = blockIdx.x * 32 * kPrepRows + (threadIdx.x >> 3);
-  const int sub = threadIdx.x & 7;
+  const int n0 = blockIdx.x * RPP * kPrepRows + threadIdx.x / LPR;
+  const int sub = threadIdx.x % LPR;
   const int64_t row0 = (int64_t)bh * p.N;
   const bf16* O = (const bf16*)p.o + b * p.so[0] + hh * p.so[1] + 8 * sub;
   const bf16* dO = (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1] + 8 * sub;
@@ -48,7 +51,7 @@ __global__ __launch_bounds__(256) void fa_bwd_prep_bf16(AttnArgs p) {
   float mm[kPrepRows], ll[kPrepRows];
 #pragma unroll
   for (int u = 0; u < kPrepRows; ++u) {
-    const int n = n0 + 32 * u;
+    const int n = n0 + RPP * u;
     o[u] = bf16x8{};
     g[u] = bf16x8{};
     mm[u] = 0.f;
@@ -70,7 +73,8 @@ __global__ __launch_bounds__(256) void fa_bwd_prep_bf16(AttnArgs p) {
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
     acc += __shfl_xor(acc, 4);
-    const int n = n0 + 32 * u;
+    if (LPR == 16) acc += __shfl_xor(acc, 8);
+    const int n = n0 + RPP * u;
     if (n < p.N && sub == 0) {
       p.delta[row0 + n] = -acc;
       p.lse2[row0 + n] = -(mm[u] * kLog2e + log2f(ll[u])) / p.scale_log2;
@@ -1096,7 +1100,7 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   // workspace (a.slab) starts with the arrival counters, which the prep kernel zeroes
   AttnArgs ap = a;
   ap.dq_cnt = variant == 20 ? (unsigned*)a.slab : nullptr;
-  hipLaunchKernelGGL(fa_bwd_prep_bf16, dim3((unsigned)((a.N + 32 * kPrepRows - 1) / (32 * kPrepRows)), (unsigned)(a.B * a.H)),
+  hipLaunchKernelGGL(fa_bwd_prep_bf16<64>, dim3((unsigned)((a.N + 32 * kPrepRows - 1) / (32 * kPrepRows)), (unsigned)(a.B * a.H)),
                      dim3(256), 0, st, ap);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1180,10 +1184,26 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   }
 }
 
-// bf16, d = 64, every per-head row offset of Q/K/V/dO (plus one tile past N) inside the
-// 31-bit buffer range; otherwise the caller falls back to the generic kernels.
+hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st);
+
+// bf16, d = 64 / 128, every per-head row offset of Q/K/V/dO (plus one tile past N) inside the
+// 31-bit buffer range; otherwise the caller falls back to the generic kernels. d = 128: the
+// split form on the 16x16x32 MFMA (fa_bwd_d128.hip; no key padding).
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled) {
   *handled = false;
+  if (a.d == 128 && !a.kv_len) {
+    const int64_t lim = (int64_t)1 << 31;
+    for (const int64_t s : {a.sq[2], a.sk[2], a.sv[2], a.sdo[2]})
+      if (((int64_t)a.N + 64) * s * 2 >= lim) return hipSuccess;
+    if ((int64_t)a.B * a.H > 65535 || (int64_t)a.B * a.H * a.N * 4 >= lim) return hipSuccess;
+    *handled = true;
+    constexpr int rpp = 256 / 16;
+    hipLaunchKernelGGL(fa_bwd_prep_bf16<128>, dim3((unsigned)((a.N + rpp * kPrepRows - 1) / (rpp * kPrepRows)), (unsigned)(a.B * a.H)),
+                       dim3(256), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_bwd_d128_passes(a, causal, st);
+  }
   if (a.d != 64) return hipSuccess;
   const int64_t lim = (int64_t)1 << 31;
   for (const int64_t s : {a.sq[2], a.sk[2], a.sv[2], a.sdo[2]})

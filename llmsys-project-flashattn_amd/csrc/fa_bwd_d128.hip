@@ -1,0 +1,328 @@
+// FlashAttention backward, bf16 I/O, head dim 128 (BASELINE config 4's head dim): the split
+// form (a dK/dV pass and a dQ pass) on the 16x16x32 MFMA, two waves per SIMD.
+//
+// Same mathematics as every backward here (reference backward_kernel,
+// src/flashattention_kernel.cu:115-255, with its dV term corrected):
+//     P = exp2(c2·S'),  dV = Pᵀ·dO,  dS = P ∘ dP',  dK = dSᵀ·Q / √d,  dQ = dS·K / √d
+// where S' = Q·Kᵀ − lse2/c2 and dP' = dO·Vᵀ − δ start from the prep kernel's pre-negated row
+// constants (C-init), as in fa_bwd_bf16.hip.
+//
+// Why this form at d = 128. The d = 64 kernels give each wave 32 keys (32x32x16 MFMA); at d =
+// 128 a wave's dKᵀ/dVᵀ for 32 keys is 128 accumulator registers and its K/V operands another
+// 64, past the two-waves-per-SIMD budget. With 16 keys per wave the accumulators are 64
+// registers, and the 16x16x32 MFMA has the lane dimension 16. The fused form (dQ inside the
+// dK/dV pass) would sum dQ over N/128 key blocks per query step: at (8,16,4096,128) 4.3 GB of
+// bf16 partials written and read back, ≈ 0.7 ms at HBM rate, as long as the extra dQ pass's
+// S and dP products, so the split (7 products, no slab, no cross-workgroup sum) is kept.
+//
+// One kernel body serves both passes (MODE): a workgroup of 8 waves owns 128 "stationary" rows
+// (16 per wave, in registers as MFMA B operands) and walks 64-row tiles of the "streamed"
+// operands through a two-slot LDS ring (LDS-DMA staging, one barrier per tile):
+//   MODE 0 (dK/dV): stationary K, V (keys); streamed Q, dO (+ the queries' row constants);
+//                   S[q][key] = Q·Kᵀ, dP[q][key] = dO·Vᵀ; dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS.
+//   MODE 1 (dQ):    stationary Q, dO (queries, row constants in registers); streamed K, V;
+//                   Sᵀ[key][q] = K·Qᵀ, dPᵀ[key][q] = V·dOᵀ; dQᵀ += Kᵀ·dSᵀ.
+// Layouts (16x16x32: lane l, g = l >> 4, i = l & 15; A lane holds row i, k = 8g .. 8g + 7; B
+// lane holds column i, k = 8g ..; C lane holds rows 4g + 0..3 of column i):
+//  * T = Y·Xᵀ per streamed 16-row tile rt: A = Y rows 16 rt + i (ds_read_b128 of the image),
+//    B = X row i of the wave (k-step ks: d 32 ks + 8 g ..), C: streamed rows 16 rt + 4 g + r
+//    of stationary row i. So the stationary row is the lane, and for a 32-row k-step kq the
+//    lane holds the streamed rows 32 kq + 4 g + r and 32 kq + 16 + 4 g + r: eight values of one
+//    stationary row, which are directly the B operand of the accumulate products in that k
+//    order (v6's P fragment, transposed roles).
+//  * The accumulate products take A = Yᵀ (d 16 dt + i, the same streamed rows in the same k
+//    order) by two ds_read_b64_tr_b16 of four rows each, as fa_fwd_d128v2.hip's Vᵀ.
+//  * One image per streamed tensor serves both reads: chunk c of row r at c ^ ((r & 7) << 1).
+//    A ds_read_b128 lane group ({0-3, 12-15 | 20-27} and its three siblings: rows i of two
+//    k-chunks) and a half-wave's transposed read (rows 4 g + 0..3, g = 0, 1, chunks 2 dt,
+//    2 dt + 1) both land on 16 distinct chunk slots (64 banks).
+// Each MFMA has one LDS operand and one register operand, so the LDS array delivers operands
+// at the MFMA's own rate (256 B per clock per CU against 1 KiB per 16-cycle MFMA per SIMD).
+// No masks for ragged N: rows past N read as zero through the buffer range check, and every
+// product they enter is zero (their Q / dO rows in the dK/dV pass, their K / V rows in the dQ
+// pass); causal masks on the diagonal tiles only.
+#include "fa_bwd_bf16.h"
+
+namespace mt {
+
+namespace {
+
+constexpr int D = 128;
+constexpr int kT = 64;                 // streamed rows per tile
+constexpr int kW = 16;                 // stationary rows per wave
+constexpr int kNW = 8;                 // waves per workgroup
+constexpr int kBR = kW * kNW;          // stationary rows per workgroup
+constexpr int kImgB = kT * D * 2;      // bytes of one streamed tile image (16 KiB)
+constexpr int kSlotB = 2 * kImgB + 2 * kT * 4;  // Y1, Y2 images + the row constants (MODE 0)
+constexpr int kSmem = 2 * kSlotB;
+static_assert(kSmem <= 160 * 1024, "LDS budget");
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ int swz(int r, int c) { return r * D + ((c ^ ((r & 7) << 1)) << 3); }
+
+__device__ __forceinline__ f32x4 mma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Yᵀ fragment (A operand of an accumulate product): d block dt, streamed rows 32 kq + 4 g + 0..3
+// and + 16, at the lane's transposed-read offset to[dt]
+__device__ __forceinline__ bf16x8 trread(const bf16* img, const int (&to)[8], int kq, int dt) {
+  const bf16* a = img + kq * 32 * D + to[dt];
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 16 * D));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// the eight values of k-step kq of a score tile set (tiles 2 kq, 2 kq + 1, rows r) as bf16
+__device__ __forceinline__ bf16x8 pack8(const f32x4 (&t)[4], int kq) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (bf16)t[2 * kq][j];
+    r[4 + j] = (bf16)t[2 * kq + 1][j];
+  }
+  return r;
+}
+
+__device__ __forceinline__ void dma16(uint32_t lds, __amdgpu_buffer_rsrc_t rs, int go) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(go), "s"(lds), "s"(rs)
+      : "memory");
+}
+__device__ __forceinline__ void dma4(uint32_t lds, __amdgpu_buffer_rsrc_t rs, int go) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dword %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(go), "s"(lds), "s"(rs)
+      : "memory");
+}
+
+}  // namespace
+
+// grid: ceil(N / 128) blocks of stationary rows x B·H, XCD-aware order (one head's blocks on
+// one XCD, where its streamed tiles stay in L2); 512 threads; kSmem bytes of LDS.
+template <int MODE, bool CAUSAL>
+__global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_head) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  const int N = p.N;
+  const int logical = bwdbf16::xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = logical / nblk_head, blk = logical % nblk_head;
+  const int b = bh / p.H, hh = bh % p.H;
+  const int r0 = blk * kBR;               // first stationary row of the workgroup
+  const int rw = r0 + wave * kW;          // first stationary row of this wave
+  const int my = rw + i16;                // this lane's stationary row
+  const float c2 = p.scale_log2;
+
+  // stationary operands (B fragments): X1, X2 row `my`, k-step ks = d 32 ks + 8 g ..
+  const bf16* X1 = MODE == 0 ? (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1]
+                             : (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* X2 = MODE == 0 ? (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1]
+                             : (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int64_t sx1 = MODE == 0 ? p.sk[2] : p.sq[2], sx2 = MODE == 0 ? p.sv[2] : p.sdo[2];
+  bf16x8 xf1[4], xf2[4];
+  {
+    const int rr = min(my, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      xf1[ks] = *(const bf16x8*)(X1 + (int64_t)rr * sx1 + 32 * ks + 8 * g);
+      xf2[ks] = *(const bf16x8*)(X2 + (int64_t)rr * sx2 + 32 * ks + 8 * g);
+    }
+  }
+  // MODE 1: the row constants of the lane's query (C-init of Sᵀ and dPᵀ)
+  float nl = 0.f, nd = 0.f;
+  if (MODE == 1 && my < N) {
+    nl = p.lse2[(int64_t)bh * N + my];
+    nd = p.delta[(int64_t)bh * N + my];
+  }
+
+  // streamed operands: images of 64-row tiles, staged by LDS-DMA: piece j of wave w fills rows
+  // 4 (2 w + j) .. + 3 in lane order, lane l fetching the source chunk the swizzle puts at
+  // chunk l % 16
+  const bf16* Y1 = MODE == 0 ? (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1]
+                             : (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const bf16* Y2 = MODE == 0 ? (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1]
+                             : (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const int sy1 = (int)(MODE == 0 ? p.sq[2] : p.sk[2]), sy2 = (int)(MODE == 0 ? p.sdo[2] : p.sv[2]);
+  const __amdgpu_buffer_rsrc_t ry1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Y1, (short)0, ((N - 1) * sy1 + D) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Y2, (short)0, ((N - 1) * sy2 + D) * 2, 0x00020000);
+  int yo1[2], yo2[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int dr = 4 * (2 * wave + j) + (lane >> 4), dc = lane & 15;
+    const int cs = dc ^ ((dr & 7) << 1);
+    yo1[j] = (dr * sy1 + cs * 8) * 2;
+    yo2[j] = (dr * sy2 + cs * 8) * 2;
+  }
+  const uint32_t lds0 = bwdbf16::lds_base(smem);
+  // MODE 0 row constants: waves 0 and 1 each move 64 dwords (−lse2/c2, then −δ) per tile;
+  // a query past N reads an out-of-range offset, i.e. 0
+  const __amdgpu_buffer_rsrc_t rcl = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.lse2 + (int64_t)bh * N), (short)0, N * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rcd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.delta + (int64_t)bh * N), (short)0, N * 4, 0x00020000);
+  auto stage = [&](int t, int slot) __attribute__((always_inline)) {
+    const uint32_t base = lds0 + slot * kSlotB;
+    const int row0 = t * kT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t off = (uint32_t)(4 * (2 * wave + j) * D * 2);
+      dma16(base + off, ry1, yo1[j] + row0 * sy1 * 2);
+      dma16(base + kImgB + off, ry2, yo2[j] + row0 * sy2 * 2);
+    }
+    if (MODE == 0 && wave < 2) {
+      const int q = row0 + lane;
+      dma4(base + 2 * kImgB + wave * kT * 4, wave ? rcd : rcl, q < N ? q * 4 : 0x7ffffff0);
+    }
+  };
+
+  // operand offsets: row reads (A of T = Y·Xᵀ): row i, chunk 4 ks + g; transposed reads (A of
+  // the accumulate products): rows 4 g + (i >> 2) (+ 16), chunk 2 dt + ((i & 3) >> 1), half i & 1
+  int ro[4], to[8];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) ro[ks] = swz(i16, 4 * ks + g);
+  {
+    const int q = i16 >> 2, pp = i16 & 3, row = 4 * g + q;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) to[dt] = swz(row, 2 * dt + (pp >> 1)) + 4 * (pp & 1);
+  }
+
+  // the tiles this workgroup walks: MODE 0 queries (causal: from the block's first key), MODE 1
+  // keys (causal: up to the block's last query)
+  const int ntile_all = (N + kT - 1) / kT;
+  const int t0 = (MODE == 0 && CAUSAL) ? r0 / kT : 0;
+  const int t1 = (MODE == 1 && CAUSAL) ? min(ntile_all, (min(r0 + kBR, N) + kT - 1) / kT) : ntile_all;
+
+  f32x4 acc1[8], acc2[8];  // MODE 0: dKᵀ, dVᵀ [d block]; MODE 1: dQᵀ in acc1
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) { acc1[dt] = f32x4{}; acc2[dt] = f32x4{}; }
+
+  if (t0 < t1) {
+    stage(t0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    const int slot = (t - t0) & 1;
+    if (t + 1 < t1) stage(t + 1, slot ^ 1);
+    const bf16* I1 = (const bf16*)(smem + slot * kSlotB);
+    const bf16* I2 = (const bf16*)(smem + slot * kSlotB + kImgB);
+    const float* cst = (const float*)(smem + slot * kSlotB + 2 * kImgB);
+    // T1 = Y1·X1ᵀ, T2 = Y2·X2ᵀ over the tile's four 16-row blocks, from the row constants
+    f32x4 T1[4], T2[4];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      if (MODE == 0) {
+        T1[rt] = *(const f32x4*)(cst + 16 * rt + 4 * g);
+        T2[rt] = *(const f32x4*)(cst + kT + 16 * rt + 4 * g);
+      } else {
+        T1[rt] = f32x4{nl, nl, nl, nl};
+        T2[rt] = f32x4{nd, nd, nd, nd};
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) {
+        T1[rt] = mma16(*(const bf16x8*)(I1 + 16 * rt * D + ro[ks]), xf1[ks], T1[rt]);
+        T2[rt] = mma16(*(const bf16x8*)(I2 + 16 * rt * D + ro[ks]), xf2[ks], T2[rt]);
+      }
+    // causal: the diagonal tiles (a streamed row on the wrong side of the lane's row)
+    const int y0 = t * kT;  // first streamed row of the tile
+    const bool diag = CAUSAL && (MODE == 0 ? y0 < rw + kW : y0 + kT - 1 > rw);
+    if (diag) {
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int y = y0 + 16 * rt + 4 * g + r;
+          // MODE 0: key my after query y; MODE 1: key y after query my
+          if (MODE == 0 ? my > y : y > my) T1[rt][r] = -INFINITY;
+        }
+    }
+    // P = exp2(c2·S'), dS = P ∘ dP'
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(T1[rt][r] * c2);
+        T1[rt][r] = pv;
+        T2[rt][r] = pv * T2[rt][r];
+      }
+    const bf16x8 sf0 = pack8(T2, 0), sf1 = pack8(T2, 1);
+    if (MODE == 0) {
+      const bf16x8 pf0 = pack8(T1, 0), pf1 = pack8(T1, 1);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        acc2[dt] = mma16(trread(I2, to, 0, dt), pf0, acc2[dt]);   // dVᵀ += dOᵀ·P
+        acc1[dt] = mma16(trread(I1, to, 0, dt), sf0, acc1[dt]);   // dKᵀ += Qᵀ·dS
+        acc2[dt] = mma16(trread(I2, to, 1, dt), pf1, acc2[dt]);
+        acc1[dt] = mma16(trread(I1, to, 1, dt), sf1, acc1[dt]);
+      }
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        acc1[dt] = mma16(trread(I1, to, 0, dt), sf0, acc1[dt]);   // dQᵀ += Kᵀ·dSᵀ
+        acc1[dt] = mma16(trread(I1, to, 1, dt), sf1, acc1[dt]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // outputs: lane (i, g) holds rows d = 16 dt + 4 g + r of stationary row `my`
+  if (my < N) {
+    const float sc = p.scale;
+    if (MODE == 0) {
+      bf16* dKg = (bf16*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my * p.sdk[2];
+      bf16* dVg = (bf16*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my * p.sdv[2];
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const int col = 16 * dt + 4 * g;
+        store4(dKg + col, acc1[dt][0] * sc, acc1[dt][1] * sc, acc1[dt][2] * sc, acc1[dt][3] * sc, true);
+        store4(dVg + col, acc2[dt][0], acc2[dt][1], acc2[dt][2], acc2[dt][3], true);
+      }
+    } else {
+      bf16* dQg = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)my * p.sdq[2];
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const int col = 16 * dt + 4 * g;
+        store4(dQg + col, acc1[dt][0] * sc, acc1[dt][1] * sc, acc1[dt][2] * sc, acc1[dt][3] * sc, true);
+      }
+    }
+  }
+}
+
+// The two passes after the d = 128 prep (fa_bwd_prep_bf16<128>). bf16, d = 128, 16-B rows,
+// every per-head row offset (plus one tile past N) inside the 31-bit buffer range.
+hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st) {
+  const int nbh = (a.N + kBR - 1) / kBR;
+  const int64_t nblk = (int64_t)nbh * a.B * a.H;
+  if (nblk > 0x7fffffff) return hipErrorInvalidValue;
+  void (*kd)(AttnArgs, int) = causal ? fa_bwd_d128_bf16<0, true> : fa_bwd_d128_bf16<0, false>;
+  void (*kq)(AttnArgs, int) = causal ? fa_bwd_d128_bf16<1, true> : fa_bwd_d128_bf16<1, false>;
+  for (auto k : {kd, kq}) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(512), kSmem, st, a, nbh);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace mt

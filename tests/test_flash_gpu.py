@@ -467,6 +467,46 @@ def test_bf16_bwd_fused_long_vs_oracle(torch_dev, N, causal, parity_record):
                       heads=2, max_abs=e, max_err_over_bound=r)
 
 
+@pytest.mark.parametrize("shape", [(1, 2, 128, 128), (1, 3, 200, 128), (2, 2, 1000, 128),
+                                   (1, 2, 2048, 128)])
+@pytest.mark.parametrize("causal", [False, True])
+def test_bf16_bwd_d128_vs_oracle(torch_dev, shape, causal, parity_record):
+    """The d = 128 split backward (fa_bwd_d128.hip: 16 keys / queries per wave on the
+    16x16x32 MFMA) against the C oracle under tests/bounds.py on whole heads: one block, a
+    ragged N (partial tiles and a partial block of 128), several blocks of both passes, and a
+    causal grid with blocks on both sides of the diagonal."""
+    from minitorch import _hip
+    torch = torch_dev
+    g = torch.Generator(device="cuda").manual_seed(sum(shape) + causal)
+    q, k, v, do = (torch.randn(shape, device="cuda", generator=g).to(torch.bfloat16) for _ in range(4))
+    o, m, l = _hip.flash_fwd(q, k, v, causal)
+    dq, dk, dv = _hip.flash_bwd(q, k, v, o, do, m, l, causal)
+    torch.cuda.synchronize()
+    heads = [(b, h) for b in range(shape[0]) for h in range(shape[1])]
+    res = _grad_check(q, k, v, do, (dq, dk, dv), causal, heads, f"{shape} causal={causal}")
+    for name, (e, r) in res.items():
+        parity_record("test_bf16_bwd_d128_vs_oracle", f"{shape} causal={causal} {name}",
+                      heads=len(heads), max_abs=e, max_err_over_bound=r)
+
+
+def test_bf16_bwd_d128_c4_heads(torch_dev):
+    """The d = 128 backward at a config-4-width grid, (8,16,2048,128): 8 heads (every batch row)
+    against the oracle, and a bitwise-equal rerun."""
+    from minitorch import _hip
+    torch = torch_dev
+    g = torch.Generator(device="cuda").manual_seed(128)
+    q, k, v, do = (torch.randn((8, 16, 2048, 128), device="cuda", generator=g).to(torch.bfloat16)
+                   for _ in range(4))
+    for causal in (False, True):
+        o, m, l = _hip.flash_fwd(q, k, v, causal)
+        g1 = _hip.flash_bwd(q, k, v, o, do, m, l, causal)
+        g2 = _hip.flash_bwd(q, k, v, o, do, m, l, causal)
+        torch.cuda.synchronize()
+        assert all(torch.equal(x, y) for x, y in zip(g1, g2))
+        _grad_check(q, k, v, do, g1, causal, [(b, (5 * b) % 16) for b in range(8)],
+                    f"(8,16,2048,128) causal={causal}")
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_bf16_bwd_fused_head_groups(torch_dev, causal):
     """More heads than one 1-GiB slab holds at N = 4096 (128): (2,72,4096,64) runs the fused
