@@ -147,6 +147,13 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
     nl = p.lse2[(int64_t)bh * N + my];
     nd = p.delta[(int64_t)bh * N + my];
   }
+  // Wait for these loads here: left to itself hipcc waits for them at their first use, inside
+  // the tile loop, with vmcnt counts that also cover the staging issued from inline asm at the
+  // top of every tile (which it does not count), and so stalls each tile mid-way for the next
+  // tile's staging.
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(xf1[ks]), "v"(xf2[ks]));
+  asm volatile("" ::"v"(nl), "v"(nd));
 
   // streamed operands: images of 64-row tiles, staged by LDS-DMA: piece j of wave w fills rows
   // 4 (2 w + j) .. + 3 in lane order, lane l fetching the source chunk the swizzle puts at
@@ -234,51 +241,88 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
         T2[rt] = f32x4{nd, nd, nd, nd};
       }
     }
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int rt = 0; rt < 4; ++rt) {
-        T1[rt] = mma16(*(const bf16x8*)(I1 + 16 * rt * D + ro[ks]), xf1[ks], T1[rt]);
-        T2[rt] = mma16(*(const bf16x8*)(I2 + 16 * rt * D + ro[ks]), xf2[ks], T2[rt]);
-      }
     // causal: the diagonal tiles (a streamed row on the wrong side of the lane's row)
     const int y0 = t * kT;  // first streamed row of the tile
     const bool diag = CAUSAL && (MODE == 0 ? y0 < rw + kW : y0 + kT - 1 > rw);
-    if (diag) {
+    bf16x8 pf[2], sf[2];  // P and dS of k-steps 0, 1 (B operands of the accumulate products)
+    // The tile as one unrolled stream of MFMA slots (sched_barrier after each, so the source
+    // order is the issue order): [0, 32) the T products, rows 0-31 (k-step 0) first; then
+    // the accumulate products of k-step 0 and of k-step 1 (16 + 16 in MODE 0: dVᵀ and dKᵀ
+    // alternating; 8 + 8 in MODE 1). Every MFMA's LDS operand is read kAhead slots before it
+    // (a ring of register fragments; hipcc's own order read each operand right before its
+    // MFMA and waited lgkmcnt(0) there, exposing the LDS latency in every slot). The softmax
+    // of k-step 0 runs beside the T products of k-step 1, that of k-step 1 beside the
+    // accumulate products of k-step 0.
+    constexpr int kNA = MODE == 0 ? 16 : 8;  // accumulate products per k-step
+    constexpr int kL = 32 + 2 * kNA;
+    constexpr int kAhead = 3;
+    auto operand = [&](int m) __attribute__((always_inline)) -> bf16x8 {
+      if (m < 32) {  // T slot: tensor m & 1, 16-row block rt, k-step ks (chains alternate)
+        const int idx = m >> 1, rt = 2 * (idx >> 3) + (idx & 1), ks = (idx >> 1) & 3;
+        return *(const bf16x8*)(((m & 1) ? I2 : I1) + 16 * rt * D + ro[ks]);
+      }
+      const int j = m - 32, kq = j / kNA, jj = j % kNA;
+      if (MODE == 0) return trread((jj & 1) ? I1 : I2, to, kq, jj >> 1);  // dVᵀ (I2), dKᵀ (I1)
+      return trread(I1, to, kq, jj);
+    };
+    // softmax item it (0..7) of k-step kq: score (rt = 2 kq + (it >> 2), r = it & 3)
+    auto item = [&](int kq, int it) __attribute__((always_inline)) {
+      const int rt = 2 * kq + (it >> 2), r = it & 3;
+      float x = T1[rt][r];
+      if (diag) {
+        const int y = y0 + 16 * rt + 4 * g + r;
+        if (MODE == 0 ? my > y : y > my) x = -INFINITY;  // MODE 0: key after query; 1: the reverse
+      }
+      const float pv = __builtin_amdgcn_exp2f(x * c2);
+      T1[rt][r] = pv;
+      T2[rt][r] = pv * T2[rt][r];
+    };
+    // pack piece k (0..3) of k-step kq: elements 2k, 2k + 1 of P (MODE 0) and dS
+    auto piece = [&](int kq, int k) __attribute__((always_inline)) {
+      const int rt = 2 * kq + (k >> 1), r = 2 * (k & 1);
+      if (MODE == 0) {
+        pf[kq][2 * k] = (bf16)T1[rt][r];
+        pf[kq][2 * k + 1] = (bf16)T1[rt][r + 1];
+      }
+      sf[kq][2 * k] = (bf16)T2[rt][r];
+      sf[kq][2 * k + 1] = (bf16)T2[rt][r + 1];
+    };
+    bf16x8 ring[kAhead + 1];
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt)
+    for (int m = 0; m < kAhead; ++m) ring[m] = operand(m);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int y = y0 + 16 * rt + 4 * g + r;
-          // MODE 0: key my after query y; MODE 1: key y after query my
-          if (MODE == 0 ? my > y : y > my) T1[rt][r] = -INFINITY;
+    for (int m = 0; m < kL; ++m) {
+      if (m + kAhead < kL) ring[(m + kAhead) % (kAhead + 1)] = operand(m + kAhead);
+      const bf16x8 a = ring[m % (kAhead + 1)];
+      if (m < 32) {
+        const int idx = m >> 1, rt = 2 * (idx >> 3) + (idx & 1), ks = (idx >> 1) & 3;
+        if (m & 1) T2[rt] = mma16(a, xf2[ks], T2[rt]);
+        else T1[rt] = mma16(a, xf1[ks], T1[rt]);
+      } else {
+        const int j = m - 32, kq = j / kNA, jj = j % kNA;
+        if (MODE == 0) {
+          if (jj & 1) acc1[jj >> 1] = mma16(a, sf[kq], acc1[jj >> 1]);  // dKᵀ += Qᵀ·dS
+          else acc2[jj >> 1] = mma16(a, pf[kq], acc2[jj >> 1]);        // dVᵀ += dOᵀ·P
+        } else {
+          acc1[jj] = mma16(a, sf[kq], acc1[jj]);  // dQᵀ += Kᵀ·dSᵀ
         }
-    }
-    // P = exp2(c2·S'), dS = P ∘ dP'
-#pragma unroll
-    for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(T1[rt][r] * c2);
-        T1[rt][r] = pv;
-        T2[rt][r] = pv * T2[rt][r];
       }
-    const bf16x8 sf0 = pack8(T2, 0), sf1 = pack8(T2, 1);
-    if (MODE == 0) {
-      const bf16x8 pf0 = pack8(T1, 0), pf1 = pack8(T1, 1);
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        acc2[dt] = mma16(trread(I2, to, 0, dt), pf0, acc2[dt]);   // dVᵀ += dOᵀ·P
-        acc1[dt] = mma16(trread(I1, to, 0, dt), sf0, acc1[dt]);   // dKᵀ += Qᵀ·dS
-        acc2[dt] = mma16(trread(I2, to, 1, dt), pf1, acc2[dt]);
-        acc1[dt] = mma16(trread(I1, to, 1, dt), sf1, acc1[dt]);
+      // the softmax beside the MFMAs: k-step 0 in slots [16, 32), k-step 1 in [32, 32 + kNA)
+      const int kq = m < 32 ? 0 : 1, w = m < 32 ? m - 16 : m - 32;
+      const int wl = kq == 0 ? 16 : kNA;  // window length
+      if (w >= 0 && w < wl) {
+        if (wl == 16) {
+          if (w < 8) item(kq, w);
+          else if (w < 12) piece(kq, w - 8);
+        } else {
+          item(kq, w);
+        }
       }
-    } else {
+      if (m == 32 + kNA - 1 && kNA == 8) {  // MODE 1: k-step 1's packs after its window
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        acc1[dt] = mma16(trread(I1, to, 0, dt), sf0, acc1[dt]);   // dQᵀ += Kᵀ·dSᵀ
-        acc1[dt] = mma16(trread(I1, to, 1, dt), sf1, acc1[dt]);
+        for (int k = 0; k < 4; ++k) piece(1, k);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -32,7 +32,13 @@
 //    waits for another (no spin, so no co-residency assumption). The adds are issued a step
 //    late and their return values read a step later still, by when they have long returned;
 //    a workgroup that turns out last for some steps reduces them after its pass (their
-//    partials are then fresh in the Infinity Cache).
+//    partials are then fresh in the Infinity Cache). The key blocks of a head walk the query
+//    steps in rotated orders (VAR 32), so each is last for about nstep / nkb steps: walked in
+//    one order, the head's slowest block was last almost everywhere and reduced the whole
+//    head alone after its pass (1.77 ms at C3 against 1.48 rotated).
+//    That form is the non-causal default; causal and masked heads (ragged N, kv_len) keep
+//    the round-3 hand-off (plain partial stores, fa_bwd_dq_reduce after the pass), which the
+//    in-kernel forms did not beat there (profiles/r4_ab_fused_forms.txt).
 // Why slabs and not float atomics: at 256 keys per workgroup dQ is summed over N/256
 // workgroups, 2.1 GB of f32 adds at C3, whose floor at the chip's ≈1.3 TB/s atomic rate
 // (MI355X_MICROARCH.md, Global float atomics) is 1.65 ms, longer than the whole split
@@ -70,8 +76,11 @@ constexpr int kSmemAll = kSmemFused + (kMaxRed + 4) * 4;  // + the pass's list o
 static_assert(kSmemAll <= 160 * 1024, "LDS budget");
 constexpr int kSc1 = 16;                            // buffer cache policy bits: sc1
 constexpr int64_t kSlabCap = (int64_t)1 << 30;      // dQ partial bytes per launch (C3: exactly 1 GiB)
-// the product's dQ hand-off form (the kernel's VAR): 0 the in-kernel last-arriver reduce
-constexpr int kFusedForm = 0;
+// the product's dQ hand-off forms (the kernel's VAR; same-box A/B of every form at C3,
+// profiles/r4_ab_fused_forms.txt): non-causal with mask-free heads (N % 64 == 0, no kv_len) the
+// rotated walks with the in-kernel reduce (32), everything else the round-3 form (16: plain
+// partial stores and the ordered reduce kernel after the pass)
+constexpr int kFormRot = 32, kFormR3 = 16;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 static_assert(kSub % 16 == 0, "16-B aligned sub-tiles");
 
@@ -241,7 +250,7 @@ __device__ __forceinline__ void dq_ksteps(const bf16* kimg, const bf16* si, int 
 // PAIR (causal): a workgroup owns key blocks nkb - 1 - u (light: the fewest query steps) and
 // then u (heavy) of one head, so every workgroup walks about nkb + 1 blocks' worth of steps
 // (the split kernels' pairing, fa_bwd_bf16.hip); the two blocks are two passes of one body.
-// VAR (A/B forms of the dQ hand-off; the product runs 0): 1 no in-kernel reduction, 2 no
+// VAR (A/B forms of the dQ hand-off; the product runs 32 or 16, kFormRot): 1 no in-kernel reduction, 2 no
 // arrivals (both: wrong dQ, timing only), 4 plain instead of sc1 partial stores, 8 the arrival
 // add as a global atomic (its return register is not its data register), 16 the round-3 form
 // (plain stores, no arrivals, fa_bwd_dq_reduce after the pass), 32 rotated walks (non-causal,
@@ -622,11 +631,12 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
   const int64_t grp = fused_group_heads(B, H, N);
   // causal: light/heavy pairs while the paired grid still has a workgroup per CU
   const bool pair = causal && (int64_t)((nkb + 1) / 2) * grp >= 256;
-  // the product form (kFusedForm, an A/B form of the kernel's VAR)
+  // the product form (an A/B form of the kernel's VAR, see kFormRot)
+  const bool rot = !causal && N % kStep == 0 && !a.kv_len;
   void (*kfn)(AttnArgs, int, int, int, int, int) =
-      pair ? fa_bwd_fused_bf16<true, true, kFusedForm> : causal ? fa_bwd_fused_bf16<true, false, kFusedForm>
-           : fa_bwd_fused_bf16<false, false, kFusedForm>;
-  int form = kFusedForm;
+      pair ? fa_bwd_fused_bf16<true, true, kFormR3> : causal ? fa_bwd_fused_bf16<true, false, kFormR3>
+      : rot ? fa_bwd_fused_bf16<false, false, kFormRot> : fa_bwd_fused_bf16<false, false, kFormR3>;
+  int form = rot ? kFormRot : kFormR3;
 #ifdef MT_DIAGNOSTICS
   // A/B forms of the dQ hand-off (MT_KNOB, see the kernel's VAR)
 #define MT_FVAR(V) \
@@ -634,6 +644,10 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
   MT_FVAR(1) MT_FVAR(2) MT_FVAR(3) MT_FVAR(4) MT_FVAR(7) MT_FVAR(8) MT_FVAR(16) MT_FVAR(32) MT_FVAR(40)
   MT_FVAR(33)
 #undef MT_FVAR
+  if (a.knob == 64) {  // the round-4 first form: in-kernel reduce, unrotated walks
+    kfn = pair ? fa_bwd_fused_bf16<true, true, 0> : causal ? fa_bwd_fused_bf16<true, false, 0> : fa_bwd_fused_bf16<false, false, 0>;
+    form = 0;
+  }
 #endif
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kSmemAll);
   if (e != hipSuccess) return e;
