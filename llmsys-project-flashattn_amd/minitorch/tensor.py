@@ -266,10 +266,16 @@ class Tensor:
     def accumulate_derivative(self, x: Any) -> None:
         assert self.is_leaf(), "Only leaf variables can have derivatives."
         if self.grad is None:
-            # the first gradient is copied (0 + x without the zero fill and the add); the copy
-            # keeps the gradient's storage its own, as the optimizer and the bucketed
-            # all-reduce update it in place
-            self.grad = Tensor(self.backend.id_map(x)._tensor, backend=self.backend)
+            # the first gradient is 0 + x without the zero fill and the add. A dense device
+            # gradient that spans its whole storage is taken as it is (nothing updates a
+            # gradient in place: the fused Adam reads it, the data-parallel all-reduce gives
+            # .grad a new tensor, the next accumulation adds into a new one); anything else
+            # (a strided view, host storage) is copied into a dense tensor of its own
+            td = x._tensor
+            if td.on_device and td.is_dense() and int(td._storage.numel()) == td.size:
+                self.grad = Tensor(td, backend=self.backend)
+            else:
+                self.grad = Tensor(self.backend.id_map(x)._tensor, backend=self.backend)
             return
         self.grad = Tensor(self.backend.add_zip(self.grad, x)._tensor, backend=self.backend)
 

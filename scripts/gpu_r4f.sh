@@ -8,3 +8,6 @@ rc=$?; grep -E "FAILED|ERROR|passed|failed|Error|assert" gpurun_out/tests_bwd_$T
 SHAPE=8,16,4096,128 timeout -k 10 300 python scripts/ablate_bwd.py 0 > gpurun_out/ab_d128_$TAG.txt 2>&1 && SHAPE=8,16,4096,128 timeout -k 10 300 python scripts/ablate_bwd.py 0 causal >> gpurun_out/ab_d128_$TAG.txt 2>&1 \
  && timeout -k 10 300 python scripts/ablate_bwd.py 0 >> gpurun_out/ab_d128_$TAG.txt 2>&1 && timeout -k 10 300 python scripts/ablate_bwd.py 0 causal >> gpurun_out/ab_d128_$TAG.txt 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/ab_d128_$TAG.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_minitorch_gpu.py tests/test_transformer_gpu.py tests/test_optim_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/tests_mt_$TAG.log 2>&1; rc=$?; tail -3 gpurun_out/tests_mt_$TAG.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/c5_op_census.py > gpurun_out/c5_census_$TAG.txt 2>&1 && head -40 gpurun_out/c5_census_$TAG.txt
+timeout -k 10 300 python scripts/mt_step_bench.py 20 > gpurun_out/c5_$TAG.json 2>&1 && cat gpurun_out/c5_$TAG.json
