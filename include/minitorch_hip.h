@@ -185,6 +185,16 @@ int mt_bias_gelu_bw(float* dx, const float* dy, const float* x, const float* bia
                     void* stream);
 int mt_dropout(float* out, const float* x, int64_t n, float p, float scale, uint64_t seed, void* stream);
 
+/* Embedding rows (reference minitorch/modules_basic.py Embedding.forward: one_hot(ids, V) @ W),
+ * fp32, ids[ntok] the float token ids, W [V x E] and out / dout [ntok x E] contiguous:
+ *   mt_embedding_fw: out[t] = W[ids[t]]            (a zero row for an id outside [0, V))
+ *   mt_embedding_bw: dW[v]  = sum over t with ids[t] == v of dout[t] in a fixed order
+ *                    (deterministic); every row of dW is written (zero for ids that do not occur) */
+int mt_embedding_fw(float* out, const float* ids, const float* weight, int64_t ntok, int64_t V, int64_t E,
+                    void* stream);
+int mt_embedding_bw(float* dweight, const float* dout, const float* ids, int64_t ntok, int64_t V, int64_t E,
+                    void* stream);
+
 /* Multi-tensor Adam step over n_tensors dense fp32 device tensors (parameters, their
  * gradients, first and second moments, numels[t] elements each), in place:
  *   m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2;  p -= step_size m / (sqrt(v) + eps)

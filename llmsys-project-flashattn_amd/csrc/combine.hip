@@ -211,24 +211,32 @@ __global__ __launch_bounds__(256) void reduce_thread_kernel(int fn, float* out, 
   }
 }
 
-// Reduction over a non-innermost dim of a dense tensor viewed as [outer][len][inner] (the
-// bias gradients: column sums of [rows, cols] activations, e.g. the LM head's 4992 x 10000):
-// one 1024-thread workgroup per 64 consecutive inner indices, 16 row groups strided over len
-// (each wave reads 64 consecutive floats of a row: coalesced), then the 16 partial results
-// folded in row-group order through LDS. The wave-per-output kernel above read these columns
-// with a 4-byte access per lane at a stride of `inner` (300 µs for the LM head bias).
+// Column reductions (a contiguous [outer][len][inner] tensor reduced over len with inner >= 16:
+// the bias gradients, column sums of [rows, cols] activations such as the LM head's 4992 x
+// 10000). The columns are split into 64-wide blocks and the rows into R chunks, so the grid
+// fills the chip even for 256 columns (one workgroup per column block ran 4 workgroups
+// there: 100 µs per 4992 x 256 sum). Workgroup (column block, chunk): 16 waves over the
+// chunk's rows (a wave reads 64 consecutive floats of a row: coalesced), folded in wave order
+// through LDS into the chunk's partial; reduce_cols_fold then folds the R <= 16 partials of
+// each column in chunk order (fixed order: deterministic). R = 1 writes the result directly.
+constexpr int kColRMax = 16;
 __global__ __launch_bounds__(1024) void reduce_cols_kernel(int fn, float* __restrict__ out,
+                                                           float* __restrict__ part_out,
+                                                           int* __restrict__ have_out,
                                                            const float* __restrict__ a, int64_t len,
-                                                           int64_t inner, float start) {
+                                                           int64_t inner, int64_t chunk, float start) {
   __shared__ float part[16][64];
   __shared__ int have_s[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + tx;
-  const float* src = a + (int64_t)blockIdx.y * len * inner + i;
+  const int r = blockIdx.y, R = gridDim.y, o = blockIdx.z;
+  const float* src = a + (int64_t)o * len * inner + i;
+  const int64_t j0 = (int64_t)r * chunk, j1 = min(len, j0 + chunk);
   float acc = 0.f;
   bool have = false;
   if (i < inner) {
-    for (int64_t j = ty; j < len; j += 16) {
+#pragma unroll 4
+    for (int64_t j = j0 + ty; j < j1; j += 16) {
       const float x = src[j * inner];
       acc = have ? apply_fn(fn, acc, x) : x;
       have = true;
@@ -238,15 +246,70 @@ __global__ __launch_bounds__(1024) void reduce_cols_kernel(int fn, float* __rest
   have_s[ty][tx] = have;
   __syncthreads();
   if (ty == 0 && i < inner) {
-    float r = 0.f;
-    bool hr = false;
+    float v = 0.f;
+    bool hv = false;
+#pragma unroll
     for (int k = 0; k < 16; ++k) {
       if (!have_s[k][tx]) continue;
-      r = hr ? apply_fn(fn, r, part[k][tx]) : part[k][tx];
-      hr = true;
+      v = hv ? apply_fn(fn, v, part[k][tx]) : part[k][tx];
+      hv = true;
     }
-    out[(int64_t)blockIdx.y * inner + i] = hr ? apply_fn(fn, start, r) : start;
+    if (R == 1) {
+      out[(int64_t)o * inner + i] = hv ? apply_fn(fn, start, v) : start;
+    } else {
+      const int64_t w = ((int64_t)o * R + r) * inner + i;
+      part_out[w] = v;
+      have_out[w] = hv;
+    }
   }
+}
+__global__ __launch_bounds__(256) void reduce_cols_fold(int fn, float* __restrict__ out,
+                                                        const float* __restrict__ part,
+                                                        const int* __restrict__ have, int64_t inner,
+                                                        int R, int64_t n, float start) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const int64_t o = t / inner, i = t % inner;
+  const float* p = part + o * R * inner + i;
+  const int* h = have + o * R * inner + i;
+  float x[kColRMax];
+  int hx[kColRMax];
+#pragma unroll
+  for (int r = 0; r < kColRMax; ++r) {  // every load first, then the ordered fold
+    x[r] = r < R ? p[(int64_t)r * inner] : 0.f;
+    hx[r] = r < R ? h[(int64_t)r * inner] : 0;
+  }
+  float v = 0.f;
+  bool hv = false;
+#pragma unroll
+  for (int r = 0; r < kColRMax; ++r) {
+    if (!hx[r]) continue;
+    v = hv ? apply_fn(fn, v, x[r]) : x[r];
+    hv = true;
+  }
+  out[t] = hv ? apply_fn(fn, start, v) : start;
+}
+
+// The partial buffer of the column reductions (per device, grown on demand, kept: the
+// reductions of one step reuse it in stream order).
+static void* reduce_scratch(size_t bytes) {
+  static std::mutex mu;
+  static void* buf[64] = {};
+  static size_t cap[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (cap[dev] < bytes) {
+    if (buf[dev]) {
+      if (hipDeviceSynchronize() != hipSuccess) return nullptr;  // in-flight users of the old buffer
+      (void)hipFree(buf[dev]);
+    }
+    buf[dev] = nullptr;
+    cap[dev] = 0;
+    if (hipMalloc(&buf[dev], bytes) != hipSuccess) { buf[dev] = nullptr; return nullptr; }
+    cap[dev] = bytes;
+  }
+  return buf[dev];
 }
 
 // Batched GEMM C[b] = A[b] @ B[b], fp32, exact fp32 MFMA. A: [M,K], B: [K,N], C: [M,N],
@@ -427,6 +490,105 @@ __global__ __launch_bounds__(256) void dropout_kernel(float* __restrict__ out, c
   }
 }
 
+// Embedding rows (reference modules_basic.py Embedding: one_hot(ids) @ W, a [tokens x V] x
+// [V x E] product): the forward gathers W[id] (zero for an id outside [0, V), the one-hot
+// row of such an id being zero); the backward sums dY rows into dW rows. ids are the float
+// token ids of the minitorch tensor.
+__global__ __launch_bounds__(256) void embed_fw_kernel(float* __restrict__ out, const float* __restrict__ ids,
+                                                       const float* __restrict__ w, int64_t ntok, int64_t V,
+                                                       int64_t E) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntok * E; i += step) {
+    const int64_t t = i / E, c = i - t * E;
+    const float f = ids[t];
+    const int64_t id = (int64_t)f;
+    out[i] = (f >= 0.f && id < V) ? w[id * E + c] : 0.f;
+  }
+}
+// dW[v] = sum of dY[t] over the tokens t with id v (deterministic: fixed order; every row of
+// dW written). One 1024-thread workgroup per kEmbVB vocabulary rows. Per pass over kEmbChunk
+// tokens each of the 16 waves compacts its 128 tokens' matches (ballot, token order) into an
+// LDS list of (token, row) entries; thread (group q, column c) then adds, in list order, the
+// dY rows of the matches of waves 4q .. 4q + 3 (a quarter of the chunk), eight loads in
+// flight; the four groups' sums are folded in group order at the end. (An id that repeats
+// thousands of times, the padding id of a padded batch, is spread over the four groups.)
+constexpr int kEmbVB = 8, kEmbChunk = 2048;
+__global__ __launch_bounds__(1024) void embed_bw_kernel(float* __restrict__ dw, const float* __restrict__ dy,
+                                                        const float* __restrict__ ids, int64_t ntok, int64_t V,
+                                                        int64_t E) {
+  __shared__ int list[kEmbChunk];
+  __shared__ int wcount[16];
+  __shared__ float fold[3][kEmbVB][256];
+  constexpr int kW = kEmbChunk / 16;  // tokens per wave per pass
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = tid >> 8, cl = tid & 255;
+  const int64_t v0 = (int64_t)blockIdx.x * kEmbVB;
+  for (int64_t c0 = 0; c0 < E; c0 += 256) {
+    const int64_t col = c0 + cl;
+    float acc[kEmbVB];
+#pragma unroll
+    for (int k = 0; k < kEmbVB; ++k) acc[k] = 0.f;
+    for (int64_t t0 = 0; t0 < ntok; t0 += kEmbChunk) {
+      int* my = list + w * kW;
+      int n = 0;
+#pragma unroll
+      for (int k = 0; k < kW; k += 64) {
+        const int64_t t = t0 + w * kW + k + lane;
+        int rel = -1;
+        if (t < ntok) {
+          const float f = ids[t];
+          const int64_t id = (int64_t)f;
+          if (f >= 0.f && id >= v0 && id < v0 + kEmbVB) rel = (int)(id - v0);
+        }
+        const unsigned long long m = __ballot(rel >= 0);
+        if (rel >= 0) my[n + __popcll(m & ((1ull << lane) - 1))] = (w * kW + k + lane) | (rel << 12);
+        n += __popcll(m);
+      }
+      if (lane == 0) wcount[w] = n;
+      __syncthreads();
+      if (col < E) {
+        const float* g = dy + t0 * E + col;
+        for (int ww = 4 * q; ww < 4 * q + 4; ++ww) {
+          const int* l = list + ww * kW;
+          const int nw = wcount[ww];
+          int j = 0;
+          for (; j + 8 <= nw; j += 8) {
+            int e[8];
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) e[u] = l[j + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = g[(int64_t)(e[u] & 4095) * E];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+              for (int k = 0; k < kEmbVB; ++k)
+                if (k == (e[u] >> 12)) acc[k] += x[u];
+          }
+          for (; j < nw; ++j) {
+            const int e = l[j];
+            const float x = g[(int64_t)(e & 4095) * E];
+#pragma unroll
+            for (int k = 0; k < kEmbVB; ++k)
+              if (k == (e >> 12)) acc[k] += x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (q > 0) {
+#pragma unroll
+      for (int k = 0; k < kEmbVB; ++k) fold[q - 1][k][cl] = acc[k];
+    }
+    __syncthreads();
+    if (q == 0 && col < E) {
+#pragma unroll
+      for (int k = 0; k < kEmbVB; ++k)
+        if (v0 + k < V) dw[(v0 + k) * E + col] = ((acc[k] + fold[0][k][cl]) + fold[1][k][cl]) + fold[2][k][cl];
+    }
+    __syncthreads();
+  }
+}
+
 // Multi-tensor Adam (minitorch/optim.py Adam.step, reference minitorch/optim.py:52-75 with
 // the second moment on (1 - beta2)): for every element of every listed tensor
 //   m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g g;  p = p - step_size m / (sqrt(v) + eps)
@@ -564,9 +726,26 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   int64_t inner = 1, outer = 1;
   for (int d = reduce_dim + 1; d < dims; ++d) inner *= a_shape[d];
   for (int d = 0; d < reduce_dim; ++d) outer *= a_shape[d];
-  if (al.contiguous && ol.contiguous && inner >= 16 && a_shape[reduce_dim] >= 16 && outer <= 65535) {
-    hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)((inner + 63) / 64), (unsigned)outer), dim3(1024), 0,
-                       (hipStream_t)stream, fn, out, a, a_shape[reduce_dim], inner, start);
+  const int64_t len = a_shape[reduce_dim];
+  if (al.contiguous && ol.contiguous && inner >= 16 && len >= 16 && outer <= 65535) {
+    // R row chunks: about 256 workgroups over the column blocks, at least 64 rows a chunk
+    const int64_t cb = (inner + 63) / 64;
+    int64_t R = std::min<int64_t>(std::min<int64_t>(kColRMax, (256 + cb * outer - 1) / (cb * outer)), len / 64);
+    if (R < 1) R = 1;
+    float* part = nullptr;
+    if (R > 1) {
+      part = (float*)reduce_scratch((size_t)(outer * R * inner) * 8);
+      if (!part) R = 1;
+    }
+    const int64_t chunk = (len + R - 1) / R;
+    hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cb, (unsigned)R, (unsigned)outer), dim3(1024), 0,
+                       (hipStream_t)stream, fn, out, part, (int*)(part + outer * R * inner), a, len, inner,
+                       chunk, start);
+    if (R > 1) {
+      const int64_t no = outer * inner;
+      hipLaunchKernelGGL(reduce_cols_fold, dim3((unsigned)((no + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                         fn, out, part, (const int*)(part + outer * R * inner), inner, (int)R, no, start);
+    }
   } else if (a_shape[reduce_dim] >= 64) {
     hipLaunchKernelGGL(reduce_wave_kernel, dim3(grid_for(n, 4)), dim3(256), 0,
                        (hipStream_t)stream, fn, out, ol, n, a, al, reduce_dim, start);
@@ -690,6 +869,27 @@ int mt_dropout(float* out, const float* x, int64_t n, float p, float scale, uint
   if (n == 0) return 0;
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, x, n, p, scale, seed);
   return check_hip(hipGetLastError(), "mt_dropout");
+}
+
+int mt_embedding_fw(float* out, const float* ids, const float* weight, int64_t ntok, int64_t V, int64_t E,
+                    void* stream) {
+  if (ntok < 0 || V <= 0 || E <= 0)
+    return set_error("mt_embedding_fw: bad sizes %lld %lld %lld", (long long)ntok, (long long)V, (long long)E);
+  if (ntok == 0) return 0;
+  hipLaunchKernelGGL(embed_fw_kernel, dim3(grid_for(ntok * E)), dim3(256), 0, (hipStream_t)stream, out, ids, weight,
+                     ntok, V, E);
+  return check_hip(hipGetLastError(), "mt_embedding_fw");
+}
+
+int mt_embedding_bw(float* dweight, const float* dout, const float* ids, int64_t ntok, int64_t V, int64_t E,
+                    void* stream) {
+  if (ntok < 0 || V <= 0 || E <= 0)
+    return set_error("mt_embedding_bw: bad sizes %lld %lld %lld", (long long)ntok, (long long)V, (long long)E);
+  const int64_t nb = (V + kEmbVB - 1) / kEmbVB;
+  if (nb > 0x7fffffff) return set_error("mt_embedding_bw: V = %lld", (long long)V);
+  hipLaunchKernelGGL(embed_bw_kernel, dim3((unsigned)nb), dim3(1024), 0, (hipStream_t)stream, dweight, dout, ids, ntok,
+                     V, E);
+  return check_hip(hipGetLastError(), "mt_embedding_bw");
 }
 
 int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,

@@ -269,13 +269,17 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // diagnostics (VAR 1024): s_memtime stamps at the phase boundaries of the bulk loop; per wave
   // the cycle sums of [DMA issue, P1, P2, P3, P4, vmcnt(0), barrier] go to p.dbg
   constexpr bool STAMP = VAR & 1024;
+  // diagnostics (VAR 2048): the older half of the workgroup (waves 0-3, which win the SIMDs'
+  // issue arbitration and then wait at the tile barrier) issues all of the tile's LDS-DMA, two
+  // pieces each, and the younger half (the pole) none
+  constexpr bool ODMA = (VAR & 2048) && !SPLIT && !DUAL;
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   static_assert(!DUAL || CAUSAL, "dual halves: causal");
   static_assert(!H || (CAUSAL && !DUAL && !PS && RS && !EV), "fp16 PV: the causal default form");
   constexpr int VS = H ? 4 : kVSlots;  // V ring slots
   constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
   constexpr int NWQ = (SPLIT || DUAL) ? 4 : kNW;  // waves sharing one query block and its key tiles
-  constexpr int LPT = kNW / NWQ;        // LDS-DMA instructions per wave per tile
+  constexpr int LPT = ODMA ? 2 : kNW / NWQ;  // LDS-DMA instructions per (issuing) wave per tile
   constexpr int BQ = 64 * NWQ;          // queries per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
 
@@ -337,10 +341,12 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     return lds0 + (uint32_t)((sl - (const bf16*)smem_raw) + 8 * (LPT * wq + i) * D) * 2;
   };
   auto dma_k = [&](bf16* sl, int step) __attribute__((always_inline)) {
+    if (ODMA && wave >= 4) return;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rk, kdo[i], step);
   };
   auto dma_v = [&](bf16* sl, int step) __attribute__((always_inline)) {
+    if (ODMA && wave >= 4) return;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rv, vdo[i], step);
   };
@@ -768,6 +774,8 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
 #ifdef MT_DIAGNOSTICS
     case 354: kern = fa_fwd_bf16_v6<354>; break;
     case 1090: kern = fa_fwd_bf16_v6<1090>; break;  // 66 with stamps
+    case 2114: kern = fa_fwd_bf16_v6<2114>; break;  // 66 with the tile's DMA by waves 0-3
+    case 3138: kern = fa_fwd_bf16_v6<3138>; break;  // 2114 with stamps
     case 194: kern = fa_fwd_bf16_v6<194>; break;
     case 2: kern = fa_fwd_bf16_v6<2>; break;
     case 34: kern = fa_fwd_bf16_v6<34>; break;

@@ -56,6 +56,8 @@ _PROTOS = {
     "mt_bias_gelu_fw": (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_bias_gelu_bw": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_dropout": (_int, [_vp, _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_uint64, _vp]),
+    "mt_embedding_fw": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
+    "mt_embedding_bw": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
     "mt_softmax_xent_fw": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_softmax_xent_bw": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_layernorm_bw_workspace_bytes": (_i64, [_i64, _i64]),

@@ -172,18 +172,33 @@ class HipKernelOps(TensorOps):
         flattens to 3-D the same way)."""
         both_2d = a.dims == 2 and b.dims == 2
 
-        def lift(t: Tensor) -> Tensor:
+        Mo, No = a.shape[-2], b.shape[-1]
+
+        def gemm_ready(t: Tensor, left: bool) -> bool:
+            # a layout the GEMM takes as it is: row-major (with a row pitch), or, for the left
+            # operand of a product with a small output, the transpose of a row-major matrix
+            # (MatMul.backward's dW = xᵀ·dy: rocBLAS op T with split-K, 12 µs against 28 µs +
+            # the transposing copy at config 5). Otherwise the copy: rocBLAS's op-T kernels
+            # measured slower on the other shapes (LM-head dW 2.3 ms against 0.25 ms, dX = dy·Wᵀ
+            # 16.6 against 11.4 µs + copy; profiles/r4_c5_gemm_layouts.txt)
+            r, c = t.shape[-2], t.shape[-1]
+            sr, sc = t._tensor.strides[-2], t._tensor.strides[-1]
+            if t._tensor.is_dense() or (sc == 1 and sr >= c):
+                return True
+            return left and Mo <= 1024 and No <= 1024 and sr == 1 and sc >= r
+
+        def lift(t: Tensor, left: bool) -> Tensor:
             # a 2-D operand as a batch of one over the same storage (a backend op: no autodiff
             # View, whose shape tensor and Function record cost host time on every matmul)
-            if not t._tensor.is_dense():
+            if not gemm_ready(t, left):
                 t = t.contiguous()
             st = t._tensor.strides
             return _wrap(t._tensor._storage, (1,) + tuple(t.shape), t.backend, (t.size,) + tuple(st))
 
         if a.dims == 2:
-            a = lift(a)
+            a = lift(a, True)
         if b.dims == 2:
-            b = lift(b)
+            b = lift(b, False)
         lead = tuple(shape_broadcast(a.shape[:-2], b.shape[:-2]))
         M, K = a.shape[-2], a.shape[-1]
         K2, N = b.shape[-2], b.shape[-1]
@@ -200,7 +215,7 @@ class HipKernelOps(TensorOps):
                 return t, (0, t._tensor.strides[-2], t._tensor.strides[-1])
             if tuple(tl) != lead:
                 raise NotImplementedError(f"partial batch broadcast {t.shape} vs {lead}")
-            if not t._tensor.is_dense():
+            if not t._tensor.is_dense() and not (t.dims == 3 and gemm_ready(t, t is a)):
                 t = t.contiguous()
             s = t._tensor.strides
             return t, (s[-3], s[-2], s[-1])
@@ -255,6 +270,27 @@ class HipKernelOps(TensorOps):
         _hip.check(_hip.lib().mt_dropout(_ptr(out), _ptr(x), x.size, ctypes.c_float(p), ctypes.c_float(scale),
                                          seed & 0xFFFFFFFFFFFFFFFF, _stream()), "dropout")
         return out
+
+    @staticmethod
+    def embedding_fw(ids: Tensor, weight: Tensor) -> Tensor:
+        """W[ids] for float token ids of any shape: rows of the [V, E] weight (reference
+        modules_basic.py Embedding: one_hot(ids) @ W, a 25.6 GFLOP product at config 5)."""
+        ids, w = _dense(ids), _dense(weight)
+        V, E = w.shape
+        out = _out(w, tuple(ids.shape) + (E,))
+        _hip.check(_hip.lib().mt_embedding_fw(_ptr(out), _ptr(ids), _ptr(w), ids.size, V, E, _stream()),
+                   "embedding_fw")
+        return out
+
+    @staticmethod
+    def embedding_bw(grad: Tensor, ids: Tensor, num_embeddings: int) -> Tensor:
+        """dW [V, E]: the rows of grad summed per token id (fixed order: deterministic)."""
+        g, ids = _dense(grad), _dense(ids)
+        E = g.shape[-1]
+        dw = _out(g, (num_embeddings, E))
+        _hip.check(_hip.lib().mt_embedding_bw(_ptr(dw), _ptr(g), _ptr(ids), ids.size, num_embeddings, E,
+                                              _stream()), "embedding_bw")
+        return dw
 
     @staticmethod
     def softmax_xent_fw(logits: Tensor, target: Tensor):

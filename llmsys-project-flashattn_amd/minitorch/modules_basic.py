@@ -22,6 +22,11 @@ class Embedding(Module):
 
     def forward(self, x: Tensor) -> Tensor:
         bs, seq_len = x.shape
+        if getattr(x.backend, "embedding_fw", None) is not None:
+            # the device backend gathers the rows (and sums dW per id) instead of the one-hot
+            # product: the same values without the [tokens x V] one-hot matrix and its GEMMs
+            from .tensor_functions import EmbeddingGather
+            return EmbeddingGather.apply(x, self.weights.value)
         oh = one_hot(x, self.num_embeddings).view(bs * seq_len, self.num_embeddings)
         return (oh @ self.weights.value).view(bs, seq_len, self.embedding_dim)
 

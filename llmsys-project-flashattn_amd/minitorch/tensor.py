@@ -247,7 +247,12 @@ class Tensor:
         for dim, s in enumerate(out.shape):
             if orig_shape[dim] == 1 and s != 1:
                 out = self.backend.add_reduce(out, dim)
-        if out is other:  # no reduction ran (only leading size-1 dims differ): a dense copy
+        if out is other:  # no reduction ran (only leading size-1 dims differ)
+            td = other._tensor
+            if td.on_device and td.is_dense() and int(td._storage.numel()) == td.size:
+                # the same values in this tensor's shape: a view (gradients are never updated in
+                # place, see accumulate_derivative)
+                return Tensor.make(td._storage, self.shape, backend=self.backend)
             out = self.backend.id_map(other)
         assert out.size == self.size, f"{out.shape} {self.shape}"
         return Tensor.make(out._tensor._storage, self.shape, backend=self.backend)

@@ -274,6 +274,22 @@ class BiasGelu(Function):
         return dx, Tensor.make(db._tensor._storage, bias.shape, backend=db.backend)
 
 
+class EmbeddingGather(Function):
+    """Embedding lookup W[ids] as one backend kernel each way (the reference forms
+    one_hot(ids, V) @ W, modules_basic.py Embedding): same values (a row of W is the one-hot
+    product's exact result), dW the per-id sums of the output gradient; the ids get none."""
+
+    @staticmethod
+    def forward(ctx, ids, weight):
+        ctx.save_for_backward(ids, weight.shape[0])
+        return ids.f.embedding_fw(ids, weight)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        ids, V = ctx.saved_values
+        return 0.0, grad_output.f.embedding_bw(grad_output, ids, V)
+
+
 class DropoutMask(Function):
     """Dropout with the keep mask drawn on the device from a seed (keep = u > p, then scaled by
     1 / (1 - p), reference modules_basic.py Dropout) in one kernel, and redrawn from the same

@@ -117,6 +117,8 @@ class TensorBackend:
         self.bias_gelu_fw = getattr(ops, "bias_gelu_fw", None)
         self.bias_gelu_bw = getattr(ops, "bias_gelu_bw", None)
         self.dropout_fw = getattr(ops, "dropout_fw", None)
+        self.embedding_fw = getattr(ops, "embedding_fw", None)
+        self.embedding_bw = getattr(ops, "embedding_bw", None)
         # fused kernels
         self.attn_softmax_fw = ops.attn_softmax_fw
         self.attn_softmax_bw = ops.attn_softmax_bw

@@ -84,7 +84,8 @@ def test_zip_map_paths(mt, case):
 
 
 @pytest.mark.parametrize("shape,dim", [((4992, 256), 0), ((300, 10000), 0), ((3, 40, 70), 1),
-                                       ((17, 33), 0), ((50, 64, 1), 0)])
+                                       ((17, 33), 0), ((50, 64, 1), 0), ((4992, 10000), 0),
+                                       ((16, 20), 0), ((3, 4096, 80), 1), ((2000, 17), 0)])
 def test_reduce_paths(mt, shape, dim):
     """Sum and max over a non-innermost dim (the coalesced column kernel where the layout
     allows: bias gradients) and the other reduce kernels, against NumPy."""
@@ -153,6 +154,43 @@ def test_dropout_fused(mt):
     # the module uses it on the HIP backend
     drop = minitorch.Dropout(0.25)
     assert abs((drop(minitorch.tensor_from_numpy(x, B)).to_numpy() != 0).mean() - 0.75) < 0.005
+
+
+@pytest.mark.parametrize("V,E,shape", [(10000, 256, (128, 39)), (37, 300, (6, 5)), (5, 16, (3000, 3))])
+def test_embedding_gather(mt, V, E, shape):
+    """EmbeddingGather (the HIP backend's Embedding): rows of W, equal to the reference's
+    one_hot(ids) @ W; dW = per-id sums of dY (fixed order), against a float64 np.add.at (the
+    one-hot product's transpose) within fp32 summation error, and exactly for ids seen once.
+    Repeated ids (every id of V = 5 thousands of times), an id >= V and a negative id (zero rows,
+    as their one-hot rows are zero)."""
+    minitorch, B = mt
+    from minitorch.tensor_functions import EmbeddingGather
+    rng = np.random.default_rng(V)
+    ids = rng.integers(0, V, shape)
+    ids.flat[0] = V + 3
+    ids.flat[-1] = -2
+    W = rng.standard_normal((V, E)).astype(np.float32)
+    g = rng.standard_normal(tuple(shape) + (E,)).astype(np.float32)
+    tw = minitorch.tensor_from_numpy(W, B, requires_grad=True)
+    tid = minitorch.tensor_from_numpy(ids.astype(np.float32), B)
+    y = EmbeddingGather.apply(tid, tw)
+    assert y.shape == tuple(shape) + (E,)
+    valid = (ids >= 0) & (ids < V)
+    ref = np.where(valid[..., None], W[np.clip(ids, 0, V - 1)], 0.0).astype(np.float32)
+    np.testing.assert_array_equal(y.to_numpy(), ref)
+    (y * minitorch.tensor_from_numpy(g, B)).sum().backward()
+    dw = tw.grad.to_numpy()
+    exp = np.zeros((V, E))
+    np.add.at(exp, ids[valid], g[valid].astype(np.float64))
+    cnt = np.bincount(ids[valid], minlength=V)
+    np.testing.assert_allclose(dw, exp, rtol=1e-5, atol=1e-5 * np.sqrt(cnt.max()))
+    once = cnt == 1
+    np.testing.assert_array_equal(dw[once], exp[once].astype(np.float32))
+    # the module takes this path on the HIP backend and matches the one-hot form
+    emb = minitorch.Embedding(V, E, B)
+    emb.weights.value = tw
+    oh = minitorch.nn.one_hot(tid, V).view(int(np.prod(shape)), V) @ tw
+    np.testing.assert_array_equal(emb(tid).to_numpy().reshape(-1, E), oh.to_numpy())
 
 
 def test_one_hot_and_softmax_loss(mt):
