@@ -111,7 +111,10 @@ __device__ __forceinline__ void dma4(uint32_t lds, __amdgpu_buffer_rsrc_t rs, in
 
 // grid: ceil(N / 128) blocks of stationary rows x B·H, XCD-aware order (one head's blocks on
 // one XCD, where its streamed tiles stay in L2); 512 threads; kSmem bytes of LDS.
-template <int MODE, bool CAUSAL>
+// PAIR (causal): a workgroup runs a light and a heavy block of one head as two passes (MODE 0:
+// key blocks nblk - 1 - u, then u; MODE 1: query blocks u, then nblk - 1 - u), so every
+// workgroup walks about nblk + 1 blocks' worth of tiles (the d = 64 kernels' pairing).
+template <int MODE, bool CAUSAL, bool PAIR = false>
 __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_head) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -119,41 +122,9 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
   const int g = lane >> 4, i16 = lane & 15;
   const int N = p.N;
   const int logical = bwdbf16::xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = logical / nblk_head, blk = logical % nblk_head;
+  const int nslot = PAIR ? (nblk_head + 1) / 2 : nblk_head;
+  const int bh = logical / nslot, u_ = logical % nslot;
   const int b = bh / p.H, hh = bh % p.H;
-  const int r0 = blk * kBR;               // first stationary row of the workgroup
-  const int rw = r0 + wave * kW;          // first stationary row of this wave
-  const int my = rw + i16;                // this lane's stationary row
-  const float c2 = p.scale_log2;
-
-  // stationary operands (B fragments): X1, X2 row `my`, k-step ks = d 32 ks + 8 g ..
-  const bf16* X1 = MODE == 0 ? (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1]
-                             : (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
-  const bf16* X2 = MODE == 0 ? (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1]
-                             : (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
-  const int64_t sx1 = MODE == 0 ? p.sk[2] : p.sq[2], sx2 = MODE == 0 ? p.sv[2] : p.sdo[2];
-  bf16x8 xf1[4], xf2[4];
-  {
-    const int rr = min(my, N - 1);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      xf1[ks] = *(const bf16x8*)(X1 + (int64_t)rr * sx1 + 32 * ks + 8 * g);
-      xf2[ks] = *(const bf16x8*)(X2 + (int64_t)rr * sx2 + 32 * ks + 8 * g);
-    }
-  }
-  // MODE 1: the row constants of the lane's query (C-init of Sᵀ and dPᵀ)
-  float nl = 0.f, nd = 0.f;
-  if (MODE == 1 && my < N) {
-    nl = p.lse2[(int64_t)bh * N + my];
-    nd = p.delta[(int64_t)bh * N + my];
-  }
-  // Wait for these loads here: left to itself hipcc waits for them at their first use, inside
-  // the tile loop, with vmcnt counts that also cover the staging issued from inline asm at the
-  // top of every tile (which it does not count), and so stalls each tile mid-way for the next
-  // tile's staging.
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(xf1[ks]), "v"(xf2[ks]));
-  asm volatile("" ::"v"(nl), "v"(nd));
 
   // streamed operands: images of 64-row tiles, staged by LDS-DMA: piece j of wave w fills rows
   // 4 (2 w + j) .. + 3 in lane order, lane l fetching the source chunk the swizzle puts at
@@ -207,6 +178,45 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) to[dt] = swz(row, 2 * dt + (pp >> 1)) + 4 * (pp & 1);
   }
+
+#pragma nounroll
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+  const int light = MODE == 0 ? nblk_head - 1 - u_ : u_, heavy = nblk_head - 1 - light;
+  const int blk = PAIR ? (pass == 0 ? light : heavy) : u_;
+  if (PAIR && pass == 1 && heavy == light) break;  // odd block count: the middle block alone
+  const int r0 = blk * kBR;               // first stationary row of the workgroup
+  const int rw = r0 + wave * kW;          // first stationary row of this wave
+  const int my = rw + i16;                // this lane's stationary row
+  const float c2 = p.scale_log2;
+
+  // stationary operands (B fragments): X1, X2 row `my`, k-step ks = d 32 ks + 8 g ..
+  const bf16* X1 = MODE == 0 ? (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1]
+                             : (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* X2 = MODE == 0 ? (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1]
+                             : (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int64_t sx1 = MODE == 0 ? p.sk[2] : p.sq[2], sx2 = MODE == 0 ? p.sv[2] : p.sdo[2];
+  bf16x8 xf1[4], xf2[4];
+  {
+    const int rr = min(my, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      xf1[ks] = *(const bf16x8*)(X1 + (int64_t)rr * sx1 + 32 * ks + 8 * g);
+      xf2[ks] = *(const bf16x8*)(X2 + (int64_t)rr * sx2 + 32 * ks + 8 * g);
+    }
+  }
+  // MODE 1: the row constants of the lane's query (C-init of Sᵀ and dPᵀ)
+  float nl = 0.f, nd = 0.f;
+  if (MODE == 1 && my < N) {
+    nl = p.lse2[(int64_t)bh * N + my];
+    nd = p.delta[(int64_t)bh * N + my];
+  }
+  // Wait for these loads here: left to itself hipcc waits for them at their first use, inside
+  // the tile loop, with vmcnt counts that also cover the staging issued from inline asm at the
+  // top of every tile (which it does not count), and so stalls each tile mid-way for the next
+  // tile's staging.
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(xf1[ks]), "v"(xf2[ks]));
+  asm volatile("" ::"v"(nl), "v"(nd));
 
   // the tiles this workgroup walks: MODE 0 queries (causal: from the block's first key), MODE 1
   // keys (causal: up to the block's last query)
@@ -349,16 +359,24 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
       }
     }
   }
+  }  // pass
 }
 
 // The two passes after the d = 128 prep (fa_bwd_prep_bf16<128>). bf16, d = 128, 16-B rows,
 // every per-head row offset (plus one tile past N) inside the 31-bit buffer range.
 hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st) {
   const int nbh = (a.N + kBR - 1) / kBR;
-  const int64_t nblk = (int64_t)nbh * a.B * a.H;
+  // causal: light / heavy pairs while the paired grid keeps a workgroup per CU
+  bool pair = causal && (int64_t)((nbh + 1) / 2) * a.B * a.H >= 256;
+#ifdef MT_DIAGNOSTICS
+  if (a.knob == 1) pair = false;
+#endif
+  const int64_t nblk = (int64_t)(pair ? (nbh + 1) / 2 : nbh) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  void (*kd)(AttnArgs, int) = causal ? fa_bwd_d128_bf16<0, true> : fa_bwd_d128_bf16<0, false>;
-  void (*kq)(AttnArgs, int) = causal ? fa_bwd_d128_bf16<1, true> : fa_bwd_d128_bf16<1, false>;
+  void (*kd)(AttnArgs, int) = pair ? fa_bwd_d128_bf16<0, true, true>
+                              : causal ? fa_bwd_d128_bf16<0, true> : fa_bwd_d128_bf16<0, false>;
+  void (*kq)(AttnArgs, int) = pair ? fa_bwd_d128_bf16<1, true, true>
+                              : causal ? fa_bwd_d128_bf16<1, true> : fa_bwd_d128_bf16<1, false>;
   for (auto k : {kd, kq}) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
     if (e != hipSuccess) return e;

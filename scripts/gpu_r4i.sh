@@ -1,0 +1,11 @@
+# round 4: C5 (column reductions, embedding gather, GEMM layouts) + the paired causal d = 128
+# backward (tests, A/B against the unpaired form = MT_KNOB 1)
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${TAG:-r4i}
+timeout -k 10 600 python -u -m pytest tests/test_minitorch_gpu.py tests/test_transformer_gpu.py tests/test_optim_gpu.py tests/test_varlen_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/tests_mt_$TAG.log 2>&1; rc=$?; grep -E "FAILED|Error|passed|failed" gpurun_out/tests_mt_$TAG.log | tail -15; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_flash_gpu.py -k "d128" -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/tests_d128_$TAG.log 2>&1; rc=$?; grep -E "FAILED|Error|passed|failed" gpurun_out/tests_d128_$TAG.log | tail -15; [ $rc -eq 0 ] || exit $rc
+MT_DIAG=1 SHAPE=8,16,4096,128 ENVAB=MT_KNOB:0,1 timeout -k 10 300 python scripts/ablate_bwd.py 0 causal > gpurun_out/ab_d128pair_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_d128pair_$TAG.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/c5_op_census.py > gpurun_out/c5_census_$TAG.txt 2>&1 && head -8 gpurun_out/c5_census_$TAG.txt
+timeout -k 10 300 python scripts/mt_step_bench.py 20 > gpurun_out/c5_$TAG.json 2>&1 && cat gpurun_out/c5_$TAG.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c5prof_$TAG -o c5 -- python3 scripts/mt_step_bench.py 10 > gpurun_out/c5prof_$TAG.log 2>&1; echo rocprof rc=$?

@@ -507,6 +507,21 @@ def test_bf16_bwd_d128_c4_heads(torch_dev):
                     f"(8,16,2048,128) causal={causal}")
 
 
+def test_bf16_bwd_d128_paired_odd(torch_dev):
+    """The causal d = 128 backward with light / heavy block pairs on an odd block count,
+    (4,16,1100,128): 9 blocks of 128 per head (the middle block alone, a ragged last block),
+    a grid large enough to pair; heads against the oracle."""
+    from minitorch import _hip
+    torch = torch_dev
+    g = torch.Generator(device="cuda").manual_seed(1100)
+    q, k, v, do = (torch.randn((4, 16, 1100, 128), device="cuda", generator=g).to(torch.bfloat16)
+                   for _ in range(4))
+    o, m, l = _hip.flash_fwd(q, k, v, True)
+    grads = _hip.flash_bwd(q, k, v, o, do, m, l, True)
+    torch.cuda.synchronize()
+    _grad_check(q, k, v, do, grads, True, [(0, 0), (2, 7), (3, 15)], "(4,16,1100,128) causal")
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_bf16_bwd_fused_head_groups(torch_dev, causal):
     """More heads than one 1-GiB slab holds at N = 4096 (128): (2,72,4096,64) runs the fused
