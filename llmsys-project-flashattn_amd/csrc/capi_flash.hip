@@ -253,11 +253,14 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     case kPolV6RowSumNoKeep: e = launch_fwd_v6(a, causal, 6, st, handled); break;
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
     case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
-    case kPolV6Wide: e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : 0), st, handled); break;
+    case kPolV6Wide:  // diagnostics knobs: 1 the older half's DMA, 2 / 3 priority flips
+      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : 0), st, handled);
+      break;
     case kPolV6Stamp: {
       AttnArgs as = a;
       as.dbg = g_dbg;
-      if (g_dbg && !causal) e = launch_fwd_v6(as, false, 66 | 1024 | (a.knob == 1 ? 2048 : 0), st, handled);
+      if (g_dbg && !causal)
+        e = launch_fwd_v6(as, false, 66 | 1024 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : 0), st, handled);
       break;
     }
     case kPolV6SplitWide: e = launch_fwd_v6(a, causal, 82, st, handled); break;

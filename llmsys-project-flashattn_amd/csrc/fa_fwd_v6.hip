@@ -273,6 +273,10 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // issue arbitration and then wait at the tile barrier) issues all of the tile's LDS-DMA, two
   // pieces each, and the younger half (the pole) none
   constexpr bool ODMA = (VAR & 2048) && !SPLIT && !DUAL;
+  // diagnostics (VAR 4096 / 8192): the younger half (waves 4-7) at issue priority 1 from the
+  // tile's start to P3 (4096) or to P2 (8192), priority 0 for the rest of the tile (the older
+  // half wins the arbitration of P1-P2 otherwise and then waits at the barrier)
+  constexpr int PFLIP = (VAR & 4096) ? 3 : (VAR & 8192) ? 2 : 0;
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   static_assert(!DUAL || CAUSAL, "dual halves: causal");
   static_assert(!H || (CAUSAL && !DUAL && !PS && RS && !EV), "fp16 PV: the causal default form");
@@ -476,6 +480,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     };
     auto iter = [&](int t, int s0) __attribute__((always_inline)) {
       __builtin_amdgcn_sched_barrier(0);
+      if (PFLIP && wave >= 4) __builtin_amdgcn_s_setprio(1);
       stamp(-1);
       dma_k(sK + ((s0 + 2) & 3) * TILE, (t + 2) * ktile_b);
       if (H) dma_v(sV + ((s0 + 2) & 3) * TILE, (t + 2) * vtile_b);
@@ -495,8 +500,10 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       qk6<true, PS, RS, EV, H>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
       if (H) vcvt_write(sV + ((s0 + 1) & 3) * TILE, tid, vraw);
       stamp(1);
+      if (PFLIP == 2 && wave >= 4) __builtin_amdgcn_s_setprio(0);
       pv6<true, K1, PS, RS, EV, H>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
       stamp(2);
+      if (PFLIP == 3 && wave >= 4) __builtin_amdgcn_s_setprio(0);
       qk6<true, PS, RS, EV, H>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
       stamp(3);
       pv6<true, K2, PS, RS, EV, H>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
@@ -776,6 +783,9 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 1090: kern = fa_fwd_bf16_v6<1090>; break;  // 66 with stamps
     case 2114: kern = fa_fwd_bf16_v6<2114>; break;  // 66 with the tile's DMA by waves 0-3
     case 3138: kern = fa_fwd_bf16_v6<3138>; break;  // 2114 with stamps
+    case 4162: kern = fa_fwd_bf16_v6<4162>; break;  // 66, waves 4-7 at priority 1 for P1-P2
+    case 8258: kern = fa_fwd_bf16_v6<8258>; break;  // 66, waves 4-7 at priority 1 for P1
+    case 5186: kern = fa_fwd_bf16_v6<5186>; break;  // 4162 with stamps
     case 194: kern = fa_fwd_bf16_v6<194>; break;
     case 2: kern = fa_fwd_bf16_v6<2>; break;
     case 34: kern = fa_fwd_bf16_v6<34>; break;

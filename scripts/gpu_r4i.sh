@@ -9,3 +9,6 @@ MT_DIAG=1 SHAPE=8,16,4096,128 ENVAB=MT_KNOB:0,1 timeout -k 10 300 python scripts
 timeout -k 10 300 python scripts/c5_op_census.py > gpurun_out/c5_census_$TAG.txt 2>&1 && head -8 gpurun_out/c5_census_$TAG.txt
 timeout -k 10 300 python scripts/mt_step_bench.py 20 > gpurun_out/c5_$TAG.json 2>&1 && cat gpurun_out/c5_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c5prof_$TAG -o c5 -- python3 scripts/mt_step_bench.py 10 > gpurun_out/c5prof_$TAG.log 2>&1; echo rocprof rc=$?
+timeout -k 10 300 python scripts/mt_step_bench.py 10 --prof gpurun_out/c5_host_$TAG.txt > /dev/null 2>&1; echo hostprof rc=$?
+MT_DIAG=1 ENVAB=MT_KNOB:0,2,3 timeout -k 10 300 python scripts/ablate.py 140 > gpurun_out/ab_pflip_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_pflip_$TAG.txt; [ $rc -eq 0 ] || exit $rc
+MT_DIAG=1 MT_KNOB=2 timeout -k 10 120 python scripts/stamp_fwd.py --json gpurun_out/stamp_pflip_$TAG.json > gpurun_out/stamp_pflip_$TAG.txt 2>&1; grep -v amdgpu.ids gpurun_out/stamp_pflip_$TAG.txt
