@@ -217,9 +217,12 @@ __global__ __launch_bounds__(256) void reduce_thread_kernel(int fn, float* out, 
 // fills the chip even for 256 columns (one workgroup per column block ran 4 workgroups
 // there: 100 µs per 4992 x 256 sum). Workgroup (column block, chunk): 16 waves over the
 // chunk's rows (a wave reads 64 consecutive floats of a row: coalesced), folded in wave order
-// through LDS into the chunk's partial; reduce_cols_fold then folds the R <= 16 partials of
+// through LDS into the chunk's partial; reduce_cols_fold then folds the R <= 64 partials of
 // each column in chunk order (fixed order: deterministic). R = 1 writes the result directly.
-constexpr int kColRMax = 16;
+// Both kernels are latency-bound at these sizes (5 MB for a 4992 x 256 sum): chunks of at most
+// 128 rows (8 independent loads per thread), and the fold issues all its loads unconditionally
+// (clamped indices) before it folds.
+constexpr int kColRMax = 64;
 __global__ __launch_bounds__(1024) void reduce_cols_kernel(int fn, float* __restrict__ out,
                                                            float* __restrict__ part_out,
                                                            int* __restrict__ have_out,
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(1024) void reduce_cols_kernel(int fn, float* __rest
   float acc = 0.f;
   bool have = false;
   if (i < inner) {
-#pragma unroll 4
+#pragma unroll 8
     for (int64_t j = j0 + ty; j < j1; j += 16) {
       const float x = src[j * inner];
       acc = have ? apply_fn(fn, acc, x) : x;
@@ -272,20 +275,25 @@ __global__ __launch_bounds__(256) void reduce_cols_fold(int fn, float* __restric
   const int64_t o = t / inner, i = t % inner;
   const float* p = part + o * R * inner + i;
   const int* h = have + o * R * inner + i;
-  float x[kColRMax];
-  int hx[kColRMax];
-#pragma unroll
-  for (int r = 0; r < kColRMax; ++r) {  // every load first, then the ordered fold
-    x[r] = r < R ? p[(int64_t)r * inner] : 0.f;
-    hx[r] = r < R ? h[(int64_t)r * inner] : 0;
-  }
   float v = 0.f;
   bool hv = false;
 #pragma unroll
-  for (int r = 0; r < kColRMax; ++r) {
-    if (!hx[r]) continue;
-    v = hv ? apply_fn(fn, v, x[r]) : x[r];
-    hv = true;
+  for (int r0 = 0; r0 < kColRMax; r0 += 16) {
+    if (r0 >= R) break;
+    float x[16];
+    int hx[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {  // 16 loads in flight, then the ordered fold
+      const int64_t rr = min(r0 + r, R - 1);
+      x[r] = p[rr * inner];
+      hx[r] = h[rr * inner];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (r0 + r >= R || !hx[r]) continue;
+      v = hv ? apply_fn(fn, v, x[r]) : x[r];
+      hv = true;
+    }
   }
   out[t] = hv ? apply_fn(fn, start, v) : start;
 }
@@ -728,9 +736,12 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   for (int d = 0; d < reduce_dim; ++d) outer *= a_shape[d];
   const int64_t len = a_shape[reduce_dim];
   if (al.contiguous && ol.contiguous && inner >= 16 && len >= 16 && outer <= 65535) {
-    // R row chunks: about 256 workgroups over the column blocks, at least 64 rows a chunk
+    // R row chunks: at most 128 rows a chunk (8 per thread), at least 64, and no more chunks
+    // than it takes to give the grid about 512 workgroups
     const int64_t cb = (inner + 63) / 64;
-    int64_t R = std::min<int64_t>(std::min<int64_t>(kColRMax, (256 + cb * outer - 1) / (cb * outer)), len / 64);
+    int64_t R = std::min<int64_t>(std::min<int64_t>(kColRMax, (len + 127) / 128),
+                                  std::max<int64_t>((512 + cb * outer - 1) / (cb * outer), len / 1024));
+    R = std::min<int64_t>(R, len / 64);
     if (R < 1) R = 1;
     float* part = nullptr;
     if (R > 1) {

@@ -20,6 +20,33 @@ from .modules_basic import Dropout, Embedding, FusedLayerNorm, LayerNorm1d, Line
 from .nn import GELU, softmax
 from .tensor_functions import tensor, tensor_from_numpy
 
+# Small host-built index tensors the model makes on every forward (the [B] key-padding lengths
+# of the flash path, the [1, T] position ids): cached by value, so a training loop that feeds
+# the same shapes does not copy host memory to the device in every layer (each synchronous
+# host-to-device copy also waits for the work already queued on the stream)
+_INDEX_CACHE: dict = {}
+
+
+def _kv_tensor(kv_len, batch_size: int, backend):
+    a = np.ascontiguousarray(np.asarray(kv_len, dtype=datatype).reshape(batch_size))
+    key = ("kv", id(backend), a.tobytes())
+    t = _INDEX_CACHE.get(key)
+    if t is None:
+        if len(_INDEX_CACHE) > 64:
+            _INDEX_CACHE.clear()
+        t = _INDEX_CACHE[key] = tensor_from_numpy(a, backend=backend)
+    return t
+
+
+def _positions(seq_len: int, backend):
+    key = ("pos", id(backend), seq_len)
+    t = _INDEX_CACHE.get(key)
+    if t is None:
+        if len(_INDEX_CACHE) > 64:
+            _INDEX_CACHE.clear()
+        t = _INDEX_CACHE[key] = tensor([[float(i) for i in range(seq_len)]], backend=backend)
+    return t
+
 datatype = np.float32
 
 
@@ -72,10 +99,7 @@ class MultiHeadAttention(Module):
         batch_size, num_head, queries_len, q_dim = q.shape
         scale = self.attn_hidden_dim ** 0.5
         if self.use_flash_attention:
-            kv = None
-            if kv_len is not None:
-                kv = tensor_from_numpy(np.asarray(kv_len, dtype=datatype).reshape(batch_size),
-                                       backend=self.backend)
+            kv = None if kv_len is None else _kv_tensor(kv_len, batch_size, self.backend)
             result = (q.flash_attention_causal(kT, v, kv_len=kv) if self.causal
                       else q.flash_attention(kT, v, kv_len=kv))
         elif self.use_fused_kernel:
@@ -182,7 +206,7 @@ class DecoderLM(Module):
         it are masked in every layer's self-attention; with the causal mask and right padding
         this changes only the outputs at padding positions)."""
         batch_size, seq_len = idx.shape
-        pos = tensor([[float(i) for i in range(seq_len)]], backend=self.backend)
+        pos = _positions(seq_len, self.backend)
         h = self.token_embeddings(idx) + self.position_embeddings(pos).view(1, seq_len, self.n_embd)
         h = self.dropout(h)
         for i in range(self.n_layer):

@@ -73,6 +73,21 @@ for nm in sorted(n for n in dir(lib) if n.startswith("mt_")):
             or "error" in nm or "workspace" in nm or "policy" in nm or "set_" in nm or not callable(getattr(lib, nm)):
         continue
     wrap(nm, lambda a: ())
+# host-to-device copies of host-built tensors (each a synchronous copy on the stream)
+from minitorch.tensor_data import TensorData
+_to_cuda = TensorData.to_cuda_
+
+
+def _counted_to_cuda(self):
+    if not self.on_device:
+        st = [f for f in traceback.extract_stack()[:-1] if "minitorch" in f.filename or "scripts" in f.filename]
+        key = ("to_cuda_", tuple(self.shape))
+        counts[key] += 1
+        where.setdefault(key, " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}" for f in st[-6:]))
+    return _to_cuda(self)
+
+
+TensorData.to_cuda_ = _counted_to_cuda
 step()
 torch.cuda.synchronize()
 tot = sum(counts.values())
