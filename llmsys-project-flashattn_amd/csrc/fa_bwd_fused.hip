@@ -524,6 +524,17 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] = 0.f;
     int k = 0;
+    for (; k + 16 <= nk; k += 16) {  // sixteen 16-B loads in flight per lane (the pass's registers are free here)
+      u32x4 x[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rsl, src + (k + u) * 8192, 0, kSc1);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const bf16x8 y = __builtin_bit_cast(bf16x8, x[u]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += (float)y[j];
+      }
+    }
     for (; k + 8 <= nk; k += 8) {
       u32x4 x[8];
 #pragma unroll
@@ -575,6 +586,17 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_reduce(AttnArgs p, int nkb, int
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i] = 0.f;
   int k = 0;
+  for (; k + 16 <= nk; k += 16) {
+    u32x4 x[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rsl, src + (k + u) * 8192, 0, 2);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const bf16x8 y = __builtin_bit_cast(bf16x8, x[u]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] += (float)y[i];
+    }
+  }
   for (; k + 8 <= nk; k += 8) {
     u32x4 x[8];
 #pragma unroll
