@@ -217,12 +217,12 @@ __global__ __launch_bounds__(256) void reduce_thread_kernel(int fn, float* out, 
 // fills the chip even for 256 columns (one workgroup per column block ran 4 workgroups
 // there: 100 µs per 4992 x 256 sum). Workgroup (column block, chunk): 16 waves over the
 // chunk's rows (a wave reads 64 consecutive floats of a row: coalesced), folded in wave order
-// through LDS into the chunk's partial; reduce_cols_fold then folds the R <= 64 partials of
+// through LDS into the chunk's partial; reduce_cols_fold then folds the R <= 16 partials of
 // each column in chunk order (fixed order: deterministic). R = 1 writes the result directly.
-// Both kernels are latency-bound at these sizes (5 MB for a 4992 x 256 sum): chunks of at most
-// 128 rows (8 independent loads per thread), and the fold issues all its loads unconditionally
-// (clamped indices) before it folds.
-constexpr int kColRMax = 64;
+// Both kernels are latency-bound at these sizes (5 MB for a 4992 x 256 sum; 14 + 12 µs at
+// C5): the fold issues all its loads unconditionally (clamped indices) before it folds, and
+// each extra round of 16 partial loads cost it ≈ 5 µs (R = 39 chunks of 128 rows: 22 µs).
+constexpr int kColRMax = 16;
 __global__ __launch_bounds__(1024) void reduce_cols_kernel(int fn, float* __restrict__ out,
                                                            float* __restrict__ part_out,
                                                            int* __restrict__ have_out,
@@ -736,8 +736,8 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   for (int d = 0; d < reduce_dim; ++d) outer *= a_shape[d];
   const int64_t len = a_shape[reduce_dim];
   if (al.contiguous && ol.contiguous && inner >= 16 && len >= 16 && outer <= 65535) {
-    // R row chunks: at most 128 rows a chunk (8 per thread), at least 64, and no more chunks
-    // than it takes to give the grid about 512 workgroups
+    // R row chunks: as many as give the grid about 512 workgroups, at most kColRMax, chunks of
+    // at least 64 rows (128 where the rows allow)
     const int64_t cb = (inner + 63) / 64;
     int64_t R = std::min<int64_t>(std::min<int64_t>(kColRMax, (len + 127) / 128),
                                   std::max<int64_t>((512 + cb * outer - 1) / (cb * outer), len / 1024));
