@@ -7,3 +7,4 @@ timeout -k 10 300 python scripts/c5_op_census.py > gpurun_out/c5_census_$TAG.txt
 timeout -k 10 300 python scripts/mt_step_bench.py 20 > gpurun_out/c5_$TAG.json 2>&1 && cat gpurun_out/c5_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c5prof_$TAG -o c5 -- python3 scripts/mt_step_bench.py 10 > gpurun_out/c5prof_$TAG.log 2>&1; echo rocprof rc=$?
 timeout -k 10 300 python scripts/mt_step_bench.py 10 --prof gpurun_out/c5_host_$TAG.txt > /dev/null 2>&1; echo hostprof rc=$?
+timeout -k 10 300 python scripts/ablate_bwd.py 0 > gpurun_out/ab_bwd_$TAG.txt 2>&1 && timeout -k 10 300 python scripts/ablate_bwd.py 0 causal >> gpurun_out/ab_bwd_$TAG.txt 2>&1; grep -v amdgpu.ids gpurun_out/ab_bwd_$TAG.txt
