@@ -277,12 +277,17 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // tile's start to P3 (4096) or to P2 (8192), priority 0 for the rest of the tile (the older
   // half wins the arbitration of P1-P2 otherwise and then waits at the barrier)
   constexpr int PFLIP = (VAR & 4096) ? 3 : (VAR & 8192) ? 2 : 0;
+  // diagnostics (VAR 16384, non-causal): 4-wave workgroups (256 queries), two per CU, so the two
+  // waves of a SIMD belong to different workgroups and share no barrier (the 8-wave form's
+  // older half waits at every tile barrier for the younger half, which loses the SIMDs' issue
+  // arbitration); each workgroup stages its own K/V tiles (two LDS-DMA pieces per wave)
+  constexpr bool W4 = (VAR & 16384) && !SPLIT && !DUAL && !CAUSAL;
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   static_assert(!DUAL || CAUSAL, "dual halves: causal");
   static_assert(!H || (CAUSAL && !DUAL && !PS && RS && !EV), "fp16 PV: the causal default form");
   constexpr int VS = H ? 4 : kVSlots;  // V ring slots
   constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
-  constexpr int NWQ = (SPLIT || DUAL) ? 4 : kNW;  // waves sharing one query block and its key tiles
+  constexpr int NWQ = (SPLIT || DUAL || W4) ? 4 : kNW;  // waves sharing one query block and its key tiles
   constexpr int LPT = ODMA ? 2 : kNW / NWQ;  // LDS-DMA instructions per (issuing) wave per tile
   constexpr int BQ = 64 * NWQ;          // queries per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -329,10 +334,14 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // LDS-DMA: instruction i of wave w fills rows 8 (LPT w + i) .. + 7 of a tile in lane
   // order, so lane l fetches the source chunk the swizzle puts at chunk l % 8 of row
   // 8 (LPT w + i) + l / 8
-  int kdo[LPT], vdo[LPT];
+  // W4: piece i of wave w fills rows 8 (w + 4 i) ..: rows 32 apart take the same swizzle, so
+  // piece 1's source offset is piece 0's plus a scalar (one address VGPR per tensor)
+  auto prow = [&](int i) __attribute__((always_inline)) { return W4 ? 8 * (wq + 4 * i) : 8 * (LPT * wq + i); };
+  constexpr int NDO = W4 ? 1 : LPT;
+  int kdo[NDO], vdo[NDO];
 #pragma unroll
-  for (int i = 0; i < LPT; ++i) {
-    const int dr = 8 * (LPT * wq + i) + (lane >> 3), dc = lane & 7;
+  for (int i = 0; i < NDO; ++i) {
+    const int dr = prow(i) + (lane >> 3), dc = lane & 7;
     kdo[i] = (dr * skn + (dc ^ ((dr >> 1) & 7)) * 8) * 2;
     vdo[i] = (dr * svn + (dc ^ (((dr >> 1) & 3) << 1)) * 8) * 2;
   }
@@ -342,17 +351,17 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem_raw);
   auto lds_of = [&](const bf16* sl, int i) __attribute__((always_inline)) {
-    return lds0 + (uint32_t)((sl - (const bf16*)smem_raw) + 8 * (LPT * wq + i) * D) * 2;
+    return lds0 + (uint32_t)((sl - (const bf16*)smem_raw) + prow(i) * D) * 2;
   };
   auto dma_k = [&](bf16* sl, int step) __attribute__((always_inline)) {
     if (ODMA && wave >= 4) return;
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rk, kdo[i], step);
+    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rk, kdo[W4 ? 0 : i], step + (W4 ? i * 64 * skn : 0));
   };
   auto dma_v = [&](bf16* sl, int step) __attribute__((always_inline)) {
     if (ODMA && wave >= 4) return;
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rv, vdo[i], step);
+    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rv, vdo[W4 ? 0 : i], step + (W4 ? i * 64 * svn : 0));
   };
   const float c2 = p.scale_log2;
 
@@ -786,6 +795,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 4162: kern = fa_fwd_bf16_v6<4162>; break;  // 66, waves 4-7 at priority 1 for P1-P2
     case 8258: kern = fa_fwd_bf16_v6<8258>; break;  // 66, waves 4-7 at priority 1 for P1
     case 5186: kern = fa_fwd_bf16_v6<5186>; break;  // 4162 with stamps
+    case 16450: kern = fa_fwd_bf16_v6<16450>; break;  // 66 with 4-wave workgroups, two per CU
     case 194: kern = fa_fwd_bf16_v6<194>; break;
     case 2: kern = fa_fwd_bf16_v6<2>; break;
     case 34: kern = fa_fwd_bf16_v6<34>; break;
@@ -799,11 +809,12 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   }
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
-  const int bq = split || dual ? kBQ / 2 : kBQ;
+  const bool w4 = (var & 16384) != 0 && !causal;
+  const int bq = split || dual || w4 ? kBQ / 2 : kBQ;
   const int nqb = (a.N + bq - 1) / bq;
   const int64_t nblk = (int64_t)(dual ? nqb / 4 : causal ? (nqb + 1) / 2 : nqb) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(64 * kNW), smem, st, a, nqb);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(w4 ? 32 * kNW : 64 * kNW), smem, st, a, nqb);
   return hipGetLastError();
 }
 
