@@ -796,6 +796,8 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 8258: kern = fa_fwd_bf16_v6<8258>; break;  // 66, waves 4-7 at priority 1 for P1
     case 5186: kern = fa_fwd_bf16_v6<5186>; break;  // 4162 with stamps
     case 16450: kern = fa_fwd_bf16_v6<16450>; break;  // 66 with 4-wave workgroups, two per CU
+    case 102: kern = fa_fwd_bf16_v6<102>; break;  // 98 without the Vᵀ reuse (32 VGPRs fewer)
+    case 614: kern = fa_fwd_bf16_v6<614>; break;  // 610 without the Vᵀ reuse
     case 194: kern = fa_fwd_bf16_v6<194>; break;
     case 2: kern = fa_fwd_bf16_v6<2>; break;
     case 34: kern = fa_fwd_bf16_v6<34>; break;
