@@ -236,6 +236,18 @@ __device__ __forceinline__ void dma6(uint32_t lds, __amdgpu_buffer_rsrc_t rs, in
       : "memory");
 }
 
+// dma6 with a scalar byte offset on top of the per-lane one (soffset): the W4 form's second
+// piece reuses the first piece's address VGPR
+__device__ __forceinline__ void dma6s(uint32_t lds, __amdgpu_buffer_rsrc_t rs, int go, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(go), "s"(lds), "s"(rs), "s"(soff)
+      : "memory");
+}
+
 }  // namespace
 
 // PS (policy 101): Q pre-scaled by c2 = log2(e) / sqrt(d) (rounded to bf16 once, in
@@ -355,13 +367,25 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   };
   auto dma_k = [&](bf16* sl, int step) __attribute__((always_inline)) {
     if (ODMA && wave >= 4) return;
+    if (W4) {
+      const int go = kdo[0] + step;
+      dma6s(lds_of(sl, 0), rk, go, 0);
+      dma6s(lds_of(sl, 1), rk, go, 64 * skn);
+      return;
+    }
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rk, kdo[W4 ? 0 : i], step + (W4 ? i * 64 * skn : 0));
+    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rk, kdo[i], step);
   };
   auto dma_v = [&](bf16* sl, int step) __attribute__((always_inline)) {
     if (ODMA && wave >= 4) return;
+    if (W4) {
+      const int go = vdo[0] + step;
+      dma6s(lds_of(sl, 0), rv, go, 0);
+      dma6s(lds_of(sl, 1), rv, go, 64 * svn);
+      return;
+    }
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rv, vdo[W4 ? 0 : i], step + (W4 ? i * 64 * svn : 0));
+    for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rv, vdo[i], step);
   };
   const float c2 = p.scale_log2;
 

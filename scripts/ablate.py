@@ -17,13 +17,13 @@ if os.environ.get("ENVAB"):
     env_vals = vals.split(",")
 arms = env_vals if env_vals else pols
 causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
-B, H, N, d = 8, 16, 4096, 64
+B, H, N, d = (int(x) for x in os.environ.get("SHAPE", "8,16,4096,64").split(","))
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
 o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
 res = {p: [] for p in arms}
 flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
-for rnd in range(5):
+for rnd in range(int(os.environ.get("ROUNDS", "5"))):
     for p in arms:
         if env_name:
             os.environ[env_name] = p
