@@ -265,7 +265,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     }
     case kPolV6SplitWide: e = launch_fwd_v6(a, causal, 82, st, handled); break;
     case kPolV6CausalWide:  // diagnostics knob 5: without the Vᵀ reuse (no spills)
-      if (causal) e = launch_fwd_v6(a, true, (a.o_f32 ? 610 : 98) | (a.knob == 5 ? 4 : 0), st, handled);
+      if (causal) e = launch_fwd_v6(a, true, (a.o_f32 ? 610 : 98) | (a.knob == 5 ? 4 : a.knob == 4 ? 16384 : a.knob == 6 ? 16388 : 0), st, handled);
       break;
     case kPolV6CausalDual:
       if (causal) e = launch_fwd_v6(a, true, 354, st, handled);

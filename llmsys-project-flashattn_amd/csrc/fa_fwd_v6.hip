@@ -293,7 +293,9 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // waves of a SIMD belong to different workgroups and share no barrier (the 8-wave form's
   // older half waits at every tile barrier for the younger half, which loses the SIMDs' issue
   // arbitration); each workgroup stages its own K/V tiles (two LDS-DMA pieces per wave)
-  constexpr bool W4 = (VAR & 16384) && !SPLIT && !DUAL && !CAUSAL;
+  constexpr bool W4 = (VAR & 16384) && !SPLIT && !DUAL;
+  // H with W4: 256 threads convert a V tile (8 KiB) in two 16-B chunks each
+  constexpr int NCV = W4 ? 2 : 1;
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   static_assert(!DUAL || CAUSAL, "dual halves: causal");
   static_assert(!H || (CAUSAL && !DUAL && !PS && RS && !EV), "fp16 PV: the causal default form");
@@ -457,7 +459,8 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (H) {  // V(0) to fp16 (V(1) is converted in iteration 0)
-    vcvt_write(sV, tid, vcvt_read(sV, tid));
+#pragma unroll
+    for (int c = 0; c < NCV; ++c) vcvt_write(sV, tid + 256 * c, vcvt_read(sV, tid + 256 * c));
     __syncthreads();
   }
   if (nbulk >= 1) {  // non-causal: the launcher guarantees N >= 128
@@ -518,8 +521,10 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       dma_k(sK + ((s0 + 2) & 3) * TILE, (t + 2) * ktile_b);
       if (H) dma_v(sV + ((s0 + 2) & 3) * TILE, (t + 2) * vtile_b);
       else dma_v(sV + ((s0 + 1) & 1) * TILE, (t + 1) * vtile_b);
-      u32x4 vraw;
-      if (H) vraw = vcvt_read(sV + ((s0 + 1) & 3) * TILE, tid);
+      u32x4 vraw[NCV];
+#pragma unroll
+      for (int c = 0; c < NCV; ++c)
+        if (H) vraw[c] = vcvt_read(sV + ((s0 + 1) & 3) * TILE, tid + 256 * c);
       int koA[2], koB[2], vv[4];
       const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & (VS - 1)) * TILE;
 #pragma unroll
@@ -531,7 +536,9 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       for (int db = 0; db < 4; ++db) vv[db] = vo[db] + vsl;
       stamp(0);
       qk6<true, PS, RS, EV, H>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
-      if (H) vcvt_write(sV + ((s0 + 1) & 3) * TILE, tid, vraw);
+#pragma unroll
+      for (int c = 0; c < NCV; ++c)
+        if (H) vcvt_write(sV + ((s0 + 1) & 3) * TILE, tid + 256 * c, vraw[c]);
       stamp(1);
       if (PFLIP == 2 && wave >= 4) __builtin_amdgcn_s_setprio(0);
       pv6<true, K1, PS, RS, EV, H>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
@@ -607,7 +614,9 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       dma_k(sK + ((t + 2) & 3) * TILE, (t + 2) * ktile_b);
       if (H) {  // and its share of the conversion of V(t + 1)
         dma_v(sV + ((t + 2) & 3) * TILE, (t + 2) * vtile_b);
-        vcvt_write(sV + ((t + 1) & 3) * TILE, tid, vcvt_read(sV + ((t + 1) & 3) * TILE, tid));
+#pragma unroll
+        for (int c = 0; c < NCV; ++c)
+          vcvt_write(sV + ((t + 1) & 3) * TILE, tid + 256 * c, vcvt_read(sV + ((t + 1) & 3) * TILE, tid + 256 * c));
       } else {
         dma_v(sV + ((t + 1) & 1) * TILE, (t + 1) * vtile_b);
       }
@@ -821,6 +830,10 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 5186: kern = fa_fwd_bf16_v6<5186>; break;  // 4162 with stamps
     case 16450: kern = fa_fwd_bf16_v6<16450>; break;  // 66 with 4-wave workgroups, two per CU
     case 102: kern = fa_fwd_bf16_v6<102>; break;  // 98 without the Vᵀ reuse (32 VGPRs fewer)
+    case 16482: kern = fa_fwd_bf16_v6<16482>; break;  // 98 with 4-wave workgroups
+    case 16994: kern = fa_fwd_bf16_v6<16994>; break;  // 610 with 4-wave workgroups
+    case 16486: kern = fa_fwd_bf16_v6<16486>; break;  // 16482 without the Vᵀ reuse
+    case 16998: kern = fa_fwd_bf16_v6<16998>; break;  // 16994 without the Vᵀ reuse
     case 614: kern = fa_fwd_bf16_v6<614>; break;  // 610 without the Vᵀ reuse
     case 194: kern = fa_fwd_bf16_v6<194>; break;
     case 2: kern = fa_fwd_bf16_v6<2>; break;
@@ -835,7 +848,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   }
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
-  const bool w4 = (var & 16384) != 0 && !causal;
+  const bool w4 = (var & 16384) != 0;
   const int bq = split || dual || w4 ? kBQ / 2 : kBQ;
   const int nqb = (a.N + bq - 1) / bq;
   const int64_t nblk = (int64_t)(dual ? nqb / 4 : causal ? (nqb + 1) / 2 : nqb) * a.B * a.H;
