@@ -378,7 +378,15 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     // policy 106): 1137 vs 1084 TF/s at (1,16,16384,64), even at C3 causal (980 vs 981,
     // profiles/r2_ab_v6.txt); v5 stays for the shapes v6 does not take.
   {
-    e = launch_fwd_v6(a, true, a.o_f32 ? 610 : 98, st, handled);
+    // Round 4: bf16 output with 4-wave workgroups (256 queries, light / heavy pairs, two
+    // workgroups per CU) where that grid still has two per CU: the two waves of a SIMD then
+    // belong to different workgroups and wait at no common barrier (in the 8-wave form the
+    // older half, which wins the SIMDs' issue arbitration, waits at every tile barrier for the
+    // younger one), and the diagonal imbalance within a workgroup is 4 waves deep instead of
+    // 8: 0.2544 vs 0.2598 ms at C3 causal, interleaved (profiles/r4_ab_fwd_w4.txt). Neutral
+    // non-causal (±1.3 % over four grids), so the non-causal default stays 8-wave.
+    const bool w4 = !a.o_f32 && (int64_t)((a.N + 255) / 256 + 1) / 2 * a.B * a.H >= 512;
+    e = launch_fwd_v6(a, true, a.o_f32 ? 610 : w4 ? (98 | 16384) : 98, st, handled);
     if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
   }
   if (!*handled && pol == kPolDefault && a.d == 64)

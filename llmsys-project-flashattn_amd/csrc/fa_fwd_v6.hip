@@ -289,10 +289,11 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // tile's start to P3 (4096) or to P2 (8192), priority 0 for the rest of the tile (the older
   // half wins the arbitration of P1-P2 otherwise and then waits at the barrier)
   constexpr int PFLIP = (VAR & 4096) ? 3 : (VAR & 8192) ? 2 : 0;
-  // diagnostics (VAR 16384, non-causal): 4-wave workgroups (256 queries), two per CU, so the two
-  // waves of a SIMD belong to different workgroups and share no barrier (the 8-wave form's
-  // older half waits at every tile barrier for the younger half, which loses the SIMDs' issue
-  // arbitration); each workgroup stages its own K/V tiles (two LDS-DMA pieces per wave)
+  // W4 (VAR 16384; the bf16-output causal default since round 4): 4-wave workgroups (256
+  // queries), two per CU, so the two waves of a SIMD belong to different workgroups and share
+  // no barrier (the 8-wave form's older half waits at every tile barrier for the younger half,
+  // which loses the SIMDs' issue arbitration); each workgroup stages its own K/V tiles (two
+  // LDS-DMA pieces per wave)
   constexpr bool W4 = (VAR & 16384) && !SPLIT && !DUAL;
   // H with W4: 256 threads convert a V tile (8 KiB) in two 16-B chunks each
   constexpr int NCV = W4 ? 2 : 1;
@@ -815,11 +816,12 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   *handled = true;
   const size_t smem = (size_t)(split || dual ? 2 : 1) * (kKSlots + (var & 512 ? 4 : kVSlots)) * TILE * sizeof(bf16);
   void (*kern)(AttnArgs, int) = nullptr;
-  switch (var) {  // product build: the defaults 66 / 18 / 98; the rest are A/B policies
+  switch (var) {  // product build: the defaults 66 / 18 / 98 / 610 / 16482; the rest are A/B policies
     case 66: kern = fa_fwd_bf16_v6<66>; break;
     case 18: kern = fa_fwd_bf16_v6<18>; break;
     case 98: kern = fa_fwd_bf16_v6<98>; break;
     case 610: kern = fa_fwd_bf16_v6<610>; break;  // 98 with fp16 PV (the fp32-output causal default)
+    case 16482: kern = fa_fwd_bf16_v6<16482>; break;  // 98 with 4-wave workgroups (the causal default)
 #ifdef MT_DIAGNOSTICS
     case 354: kern = fa_fwd_bf16_v6<354>; break;
     case 1090: kern = fa_fwd_bf16_v6<1090>; break;  // 66 with stamps
@@ -830,7 +832,6 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 5186: kern = fa_fwd_bf16_v6<5186>; break;  // 4162 with stamps
     case 16450: kern = fa_fwd_bf16_v6<16450>; break;  // 66 with 4-wave workgroups, two per CU
     case 102: kern = fa_fwd_bf16_v6<102>; break;  // 98 without the Vᵀ reuse (32 VGPRs fewer)
-    case 16482: kern = fa_fwd_bf16_v6<16482>; break;  // 98 with 4-wave workgroups
     case 16994: kern = fa_fwd_bf16_v6<16994>; break;  // 610 with 4-wave workgroups
     case 16486: kern = fa_fwd_bf16_v6<16486>; break;  // 16482 without the Vᵀ reuse
     case 16998: kern = fa_fwd_bf16_v6<16998>; break;  // 16994 without the Vᵀ reuse
