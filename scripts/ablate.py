@@ -20,7 +20,8 @@ causal = len(sys.argv) > 2 and sys.argv[2] == "causal"
 B, H, N, d = (int(x) for x in os.environ.get("SHAPE", "8,16,4096,64").split(","))
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
-o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
+o = torch.empty_like(q, dtype=torch.float32 if os.environ.get("OUT") == "f32" else q.dtype)  # OUT=f32: fp32 output
+m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
 res = {p: [] for p in arms}
 flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
 for rnd in range(int(os.environ.get("ROUNDS", "5"))):
