@@ -99,11 +99,15 @@ __device__ __forceinline__ bf16x8 vread6(const bf16* sv, const int (&vo)[4], int
 // (i >> 1) & 1, rows 2(i & 1), 2(i & 1) + 1. Exponentials in one MFMA slot, the row-sum add
 // and bf16 pack in the next (no transcendental-to-use stall). PS: the scores already are
 // c2 s - reference (Q pre-scaled, the shift in the MFMA's C operand): no scale-and-shift.
-template <bool PS>
+template <bool PS, bool PK = false>
 __device__ __forceinline__ f32x2 sm6_exp(const Blk6& s, int kk, int i, float c2, const float (&nmc)[2]) {
   const int kbl = i >> 2, qh = (i >> 1) & 1, r0 = 2 * (i & 1);
   const f32x4& v = s.s[2 * kk + kbl][qh];
   if (PS) return f32x2{__builtin_amdgcn_exp2f(v[r0]), __builtin_amdgcn_exp2f(v[r0 + 1])};
+  if (PK) {  // diagnostics (VAR 32768): the pair's scale-and-shift as one v_pk_fma_f32
+    const f32x2 x = __builtin_elementwise_fma(f32x2{v[r0], v[r0 + 1]}, f32x2{c2, c2}, f32x2{nmc[qh], nmc[qh]});
+    return f32x2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+  }
   // scalar f32 arithmetic: packed v_pk_fma_f32 / v_pk_add_f32 beside the MFMAs cost issue
   // cycles the scalar forms do not (MI355X_MICROARCH.md, 'price of one filler')
   const float x0 = __builtin_fmaf(v[r0], c2, nmc[qh]), x1 = __builtin_fmaf(v[r0 + 1], c2, nmc[qh]);
@@ -132,12 +136,12 @@ __device__ __forceinline__ void sm6_fin(const f32x2& e, int i, f32x2 (&acc)[2], 
 // m / 2 in the even slot, its row-sum adds and bf16 pack in the odd one. EV (with RS only):
 // one exponential per slot, and in odd slots the pack of the previous pair (the last pair is
 // packed after the phase's last MFMA): 12 / 16 cycles of issue per slot instead of 24 / 4.
-template <bool PS, bool RS, bool EV, bool H = false>
+template <bool PS, bool RS, bool EV, bool H = false, bool PK = false>
 __device__ __forceinline__ void sm6_slot(int m, const Blk6& s_in, int kk, float c2, const float (&nmc)[2],
                                          f32x2 (&acc)[2], Pf6& pf, f32x2& ep, f32x2& ec) {
   if (!EV) {
     if (m & 1) sm6_fin<RS, H>(ep, m >> 1, acc, pf);
-    else ep = sm6_exp<PS>(s_in, kk, m >> 1, c2, nmc);
+    else ep = sm6_exp<PS, PK>(s_in, kk, m >> 1, c2, nmc);
     return;
   }
   const int i = m >> 1, j = m & 1, kbl = i >> 2, qh = (i >> 1) & 1, r = 2 * (i & 1) + j;
@@ -152,7 +156,7 @@ __device__ __forceinline__ void sm6_slot(int m, const Blk6& s_in, int kk, float 
 // QKᵀ phase: 16 MFMAs into S (16-key blocks in order, so keys 0-31 finish first), beside the
 // softmax of half kk of s_in. MFMA m: fragment f = m >> 1 (block f >> 1, k-step f & 1),
 // query half m & 1. The chains start from ci[qh] (zero, or the PS shift).
-template <bool SOFT, bool PS, bool RS = false, bool EV = false, bool H = false>
+template <bool SOFT, bool PS, bool RS = false, bool EV = false, bool H = false, bool PK = false>
 __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf16x8 (&qf)[2][2], Blk6& S,
                                     const f32x4 (&ci)[2], const Blk6& s_in, int kk, float c2,
                                     const float (&nmc)[2], f32x2 (&acc)[2], Pf6& pf) {
@@ -165,7 +169,7 @@ __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf
     const int f = m >> 1, kb = f >> 1, ks = f & 1, qh = m & 1;
     if (!(m & 1) && f + 2 < 8) kf[f + 2] = kread6(sk, ko, f + 2);
     S.s[kb][qh] = mma16(kf[f], qf[qh][ks], ks ? S.s[kb][qh] : ci[qh]);
-    if (SOFT) sm6_slot<PS, RS, EV, H>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
+    if (SOFT) sm6_slot<PS, RS, EV, H, PK>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (SOFT && EV) sm6_fin<true, H>(ep, 7, acc, pf);
@@ -176,7 +180,7 @@ __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf
 // query half m & 1. KEEP: 1 = read the Vᵀ fragments and leave them in vk, 2 = take them
 // from vk (P2 and P4 multiply the same V(t)). RS: R[qh] += ones·Pᵀ right after each P
 // operand's first MFMA (every element of R[qh] is then the running row sum of its query).
-template <bool SOFT, int KEEP, bool PS, bool RS = false, bool EV = false, bool H = false>
+template <bool SOFT, int KEEP, bool PS, bool RS = false, bool EV = false, bool H = false, bool PK = false>
 __device__ __forceinline__ void pv6(const bf16* sv, const int (&vo)[4], f32x4 (&O)[4][2], const Pf6& plo,
                                     const Pf6& phi, const Blk6& s_in, int kk, float c2,
                                     const float (&nmc)[2], f32x2 (&acc)[2], Pf6& pf, bf16x8 (&vk)[8],
@@ -196,7 +200,7 @@ __device__ __forceinline__ void pv6(const bf16* sv, const int (&vo)[4], f32x4 (&
     if (KEEP != 2 && !(m & 1) && f + 2 < 8) vf[f + 2] = vread6(sv, vo, f + 2);
     O[db][qh] = mma_pv<H>(vf[f], (hv ? phi : plo).p[qh], O[db][qh]);
     if (RS && db == 0) R[qh] = mma_pv<H>(ones, (hv ? phi : plo).p[qh], R[qh]);
-    if (SOFT) sm6_slot<PS, RS, EV, H>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
+    if (SOFT) sm6_slot<PS, RS, EV, H, PK>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (SOFT && EV) sm6_fin<true, H>(ep, 7, acc, pf);
@@ -295,6 +299,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // which loses the SIMDs' issue arbitration); each workgroup stages its own K/V tiles (two
   // LDS-DMA pieces per wave)
   constexpr bool W4 = (VAR & 16384) && !SPLIT && !DUAL;
+  constexpr bool PK = (VAR & 32768) && !PS;  // diagnostics: packed scale-and-shift (sm6_exp)
   // H with W4: 256 threads convert a V tile (8 KiB) in two 16-B chunks each
   constexpr int NCV = W4 ? 2 : 1;
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
@@ -536,18 +541,18 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
 #pragma unroll
       for (int db = 0; db < 4; ++db) vv[db] = vo[db] + vsl;
       stamp(0);
-      qk6<true, PS, RS, EV, H>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
+      qk6<true, PS, RS, EV, H, PK>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
 #pragma unroll
       for (int c = 0; c < NCV; ++c)
         if (H) vcvt_write(sV + ((s0 + 1) & 3) * TILE, tid + 256 * c, vraw[c]);
       stamp(1);
       if (PFLIP == 2 && wave >= 4) __builtin_amdgcn_s_setprio(0);
-      pv6<true, K1, PS, RS, EV, H>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
+      pv6<true, K1, PS, RS, EV, H, PK>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
       stamp(2);
       if (PFLIP == 3 && wave >= 4) __builtin_amdgcn_s_setprio(0);
-      qk6<true, PS, RS, EV, H>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
+      qk6<true, PS, RS, EV, H, PK>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
       stamp(3);
-      pv6<true, K2, PS, RS, EV, H>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
+      pv6<true, K2, PS, RS, EV, H, PK>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
       stamp(4);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(5);
@@ -569,9 +574,9 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
 #pragma unroll
       for (int db = 0; db < 4; ++db) vv[db] = vo[db] + (t & (VS - 1)) * TILE;
       if (CAUSAL) mask_diag(SB, 32);  // S_B(tD): keys 32-63 are block B's diagonal
-      qk6<true, PS, RS, EV, H>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
+      qk6<true, PS, RS, EV, H, PK>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
       if (CAUSAL) mask_diag(SA, 0);  // S_A(tD): keys 0-31 its diagonal, 32-63 above it
-      pv6<true, K1, PS, RS, EV, H>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);
+      pv6<true, K1, PS, RS, EV, H, PK>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);
 #pragma unroll
       for (int i = 0; i < 8; ++i) sm6_fin<RS, H>(sm6_exp<PS>(SA, 1, i, c2, nmcA), i, accA, pA1);
       f32x2 d2[2];
@@ -831,6 +836,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 8258: kern = fa_fwd_bf16_v6<8258>; break;  // 66, waves 4-7 at priority 1 for P1
     case 5186: kern = fa_fwd_bf16_v6<5186>; break;  // 4162 with stamps
     case 16450: kern = fa_fwd_bf16_v6<16450>; break;  // 66 with 4-wave workgroups, two per CU
+    case 32834: kern = fa_fwd_bf16_v6<32834>; break;  // 66 with packed scale-and-shift
     case 102: kern = fa_fwd_bf16_v6<102>; break;  // 98 without the Vᵀ reuse (32 VGPRs fewer)
     case 16994: kern = fa_fwd_bf16_v6<16994>; break;  // 610 with 4-wave workgroups
     case 16486: kern = fa_fwd_bf16_v6<16486>; break;  // 16482 without the Vᵀ reuse

@@ -1,0 +1,5 @@
+# round 4: v6 with the packed scale-and-shift (knob 7) vs the default, 10 rounds, C3
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${TAG:-r4o}
+ROUNDS=10 MT_DIAG=1 ENVAB=MT_KNOB:0,7 timeout -k 10 300 python scripts/ablate.py 140 > gpurun_out/ab_pk_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_pk_$TAG.txt; exit $rc
