@@ -114,7 +114,7 @@ __device__ __forceinline__ void dma4(uint32_t lds, __amdgpu_buffer_rsrc_t rs, in
 // PAIR (causal): a workgroup runs a light and a heavy block of one head as two passes (MODE 0:
 // key blocks nblk - 1 - u, then u; MODE 1: query blocks u, then nblk - 1 - u), so every
 // workgroup walks about nblk + 1 blocks' worth of tiles (the d = 64 kernels' pairing).
-template <int MODE, bool CAUSAL, bool PAIR = false>
+template <int MODE, bool CAUSAL, bool PAIR = false, int AHEAD = 3>
 __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_head) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
     // accumulate products of k-step 0.
     constexpr int kNA = MODE == 0 ? 16 : 8;  // accumulate products per k-step
     constexpr int kL = 32 + 2 * kNA;
-    constexpr int kAhead = 3;
+    constexpr int kAhead = AHEAD;  // (diagnostics A/B: 2, 4, 5)
     auto operand = [&](int m) __attribute__((always_inline)) -> bf16x8 {
       if (m < 32) {  // T slot: tensor m & 1, 16-row block rt, k-step ks (chains alternate)
         const int idx = m >> 1, rt = 2 * (idx >> 3) + (idx & 1), ks = (idx >> 1) & 3;
@@ -377,6 +377,16 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
                               : causal ? fa_bwd_d128_bf16<0, true> : fa_bwd_d128_bf16<0, false>;
   void (*kq)(AttnArgs, int) = pair ? fa_bwd_d128_bf16<1, true, true>
                               : causal ? fa_bwd_d128_bf16<1, true> : fa_bwd_d128_bf16<1, false>;
+#ifdef MT_DIAGNOSTICS
+  // operand-read distance A/B (knobs 12 / 14 / 15: 2 / 4 / 5 MFMA slots ahead), non-causal
+#define MT_AH(K, A)                                                       \
+  if (!causal && a.knob == K) {                                           \
+    kd = fa_bwd_d128_bf16<0, false, false, A>;                            \
+    kq = fa_bwd_d128_bf16<1, false, false, A>;                            \
+  }
+  MT_AH(12, 2) MT_AH(14, 4) MT_AH(15, 5)
+#undef MT_AH
+#endif
   for (auto k : {kd, kq}) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
     if (e != hipSuccess) return e;

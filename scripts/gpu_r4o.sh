@@ -1,5 +1,7 @@
-# round 4: v6 with the packed scale-and-shift (knob 7) vs the default, 10 rounds, C3
+# round 4: v6 with the packed scale-and-shift (knob 7) vs the default, 10 rounds, C3; the d = 128
+# backward's operand-read distance (knobs 12 / 14 / 15 = 2 / 4 / 5 slots; 0 = 3)
 set -o pipefail
 mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${TAG:-r4o}
-ROUNDS=10 MT_DIAG=1 ENVAB=MT_KNOB:0,7 timeout -k 10 300 python scripts/ablate.py 140 > gpurun_out/ab_pk_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_pk_$TAG.txt; exit $rc
+ROUNDS=10 MT_DIAG=1 ENVAB=MT_KNOB:0,7 timeout -k 10 300 python scripts/ablate.py 140 > gpurun_out/ab_pk_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_pk_$TAG.txt; [ $rc -eq 0 ] || exit $rc
+SHAPE=8,16,4096,128 MT_DIAG=1 ENVAB=MT_KNOB:0,12,14,15 timeout -k 10 300 python scripts/ablate_bwd.py 0 > gpurun_out/ab_d128ah_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_d128ah_$TAG.txt; exit $rc
