@@ -12,7 +12,7 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
-enum Op { EXP = 0, FMA, PKFMA, PKADD, CVT, NOP_ };
+enum Op { EXP = 0, FMA, PKFMA, PKADD, CVT, EXPH, EXPHS, CVTH, NOP_ };
 
 template <int OP>
 __device__ __forceinline__ void op8(float (&x)[16]) {
@@ -33,6 +33,14 @@ __device__ __forceinline__ void op8(float (&x)[16]) {
       asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(v) : "v"(a));
       x[2 * (j & 3)] = v[0];
       x[2 * (j & 3) + 1] = v[1];
+    }
+    if (OP == EXPH) asm volatile("v_exp_f16 %0, %0" : "+v"(x[j]));
+    if (OP == EXPHS)  // the high half in place (SDWA): a packed f16 pair's second exponential
+      asm volatile("v_exp_f16_sdwa %0, %0 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(x[j]));
+    if (OP == CVTH) {
+      unsigned r;
+      asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(x[j]), "v"(x[(j + 1) & 7]));
+      x[j] = __uint_as_float(r);
     }
     if (OP == CVT) {
       unsigned r;
@@ -109,12 +117,18 @@ int main(int argc, char** argv) {
     run<PKFMA, 0, 2>("pk_fma only", w);
     run<PKADD, 0, 2>("pk_add only", w);
     run<CVT, 0, 2>("cvt_pk_bf16 only", w);
+    run<EXPH, 0, 2>("exp_f16 only", w);
+    run<EXPHS, 0, 2>("exp_f16 sdwa hi only", w);
+    run<CVTH, 0, 2>("cvt_pk_f16 only", w);
     run<EXP, 1, 0>("mfma only", w);
     run<EXP, 1, 1>("mfma + 8 exp", w);
     run<FMA, 1, 1>("mfma + 8 fma", w);
     run<PKFMA, 1, 1>("mfma + 8 pk_fma", w);
     run<PKADD, 1, 1>("mfma + 8 pk_add", w);
     run<CVT, 1, 1>("mfma + 8 cvt_pk", w);
+    run<EXPH, 1, 1>("mfma + 8 exp_f16", w);
+    run<EXPHS, 1, 1>("mfma + 8 exp_f16 sdwa hi", w);
+    run<CVTH, 1, 1>("mfma + 8 cvt_pk_f16", w);
     run<EXP, 2, 0>("mfma chains of 4", w);
     run<EXP, 3, 0>("mfma one dependent chain", w);
     run<FMA, 2, 1>("mfma chains of 4 + 8 fma", w);
