@@ -82,6 +82,7 @@ constexpr int64_t kSlabCap = (int64_t)1 << 30;      // dQ partial bytes per laun
 // partial stores and the ordered reduce kernel after the pass)
 constexpr int kFormRot = 32, kFormR3 = 16;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 static_assert(kSub % 16 == 0, "16-B aligned sub-tiles");
 
 __device__ __forceinline__ int swf(int r) {
@@ -123,7 +124,7 @@ __device__ __forceinline__ void tr_offsets(int lane, int db, int& lo, int& hi) {
 // hipcc issues each MFMA's reads right before it and waits lgkmcnt(0), which serialises the
 // LDS latency into every product. Masked tiles (causal diagonal, ragged tail, padding) read
 // at use: the mask's registers on top of sixteen live fragments spill.
-template <bool CAUSAL, bool MASK, bool PF>
+template <bool CAUSAL, bool MASK, bool PF, bool PKM = false>
 __device__ __forceinline__ void fdkv_tile(const char* sub, const FCtx& c, f32x16 (&dK)[2],
                                           f32x16 (&dV)[2], float c2, int qt, int N, int Nk,
                                           int my_k, int hf, bf16* dsrow, int fk, int u) {
@@ -173,11 +174,22 @@ __device__ __forceinline__ void fdkv_tile(const char* sub, const FCtx& c, f32x16
       if (q >= N || my_k >= Nk || (CAUSAL && my_k > q)) S[r] = -INFINITY;
     }
   }
+  if (PKM) {  // diagnostics (VAR 64): the scale and the dS product as v_pk_mul_f32 pairs
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float pv = __builtin_amdgcn_exp2f(S[r] * c2);
-    S[r] = pv;
-    dP[r] = pv * dP[r];
+    for (int r = 0; r < 16; r += 2) {
+      const f32x2 x = f32x2{S[r], S[r + 1]} * f32x2{c2, c2};
+      const f32x2 pv = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+      const f32x2 ds = pv * f32x2{dP[r], dP[r + 1]};
+      S[r] = pv[0]; S[r + 1] = pv[1];
+      dP[r] = ds[0]; dP[r + 1] = ds[1];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pv = __builtin_amdgcn_exp2f(S[r] * c2);
+      S[r] = pv;
+      dP[r] = pv * dP[r];
+    }
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -263,6 +275,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   constexpr bool R3 = VAR & 16;
   constexpr bool NORED = (VAR & 1) || R3, NOARR = (VAR & 2) || R3, PLAIN = (VAR & 4) || R3, GATOM = VAR & 8;
   constexpr bool ROT = (VAR & 32) && !CAUSAL;
+  constexpr bool PKM = VAR & 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
@@ -434,7 +447,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   {                                                                                      \
     const int qt_ = qt0 + sq(T_) * kStep + (U_) * kQT;                                   \
     bf16* dsr_ = dsrow0 + (SLOT_) * (kKB * kStep);                                       \
-    fdkv_tile<CAUSAL, MASK_, kPF && !(MASK_)>(smem + (2 * (SLOT_) + (U_)) * kSub, c, dK, dV, c2, qt_, N,  \
+    fdkv_tile<CAUSAL, MASK_, kPF && !(MASK_), PKM>(smem + (2 * (SLOT_) + (U_)) * kSub, c, dK, dV, c2, qt_, N,  \
                              Nk, my_k, hf, dsr_, fk, U_);                                \
   }
 #define FSTEP(MASK_, SLOT_, T_, DQ_)                                                     \
@@ -664,7 +677,7 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
 #define MT_FVAR(V) \
   if (a.knob == V) { kfn = pair ? fa_bwd_fused_bf16<true, true, V> : causal ? fa_bwd_fused_bf16<true, false, V> : fa_bwd_fused_bf16<false, false, V>; form = V; }
   MT_FVAR(1) MT_FVAR(2) MT_FVAR(3) MT_FVAR(4) MT_FVAR(7) MT_FVAR(8) MT_FVAR(16) MT_FVAR(32) MT_FVAR(40)
-  MT_FVAR(33)
+  MT_FVAR(33) MT_FVAR(80) MT_FVAR(96)
 #undef MT_FVAR
   if (a.knob == 64) {  // the round-4 first form: in-kernel reduce, unrotated walks
     kfn = pair ? fa_bwd_fused_bf16<true, true, 0> : causal ? fa_bwd_fused_bf16<true, false, 0> : fa_bwd_fused_bf16<false, false, 0>;

@@ -6,3 +6,4 @@ TAG=${TAG:-r4o}
 ROUNDS=10 MT_DIAG=1 ENVAB=MT_KNOB:0,7 timeout -k 10 300 python scripts/ablate.py 140 > gpurun_out/ab_pk_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_pk_$TAG.txt; [ $rc -eq 0 ] || exit $rc
 SHAPE=8,16,4096,128 MT_DIAG=1 ENVAB=MT_KNOB:0,12,14,15 timeout -k 10 300 python scripts/ablate_bwd.py 0 > gpurun_out/ab_d128ah_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_d128ah_$TAG.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 ./scripts/valu_rate_bench 2.1 > gpurun_out/valu_rate_$TAG.txt 2>&1; cat gpurun_out/valu_rate_$TAG.txt
+MT_DIAG=1 ENVAB=MT_KNOB:0,96 ROUNDS=8 timeout -k 10 300 python scripts/ablate_bwd.py 0 > gpurun_out/ab_bwdpk_$TAG.txt 2>&1 && MT_DIAG=1 ENVAB=MT_KNOB:0,80 timeout -k 10 300 python scripts/ablate_bwd.py 0 causal >> gpurun_out/ab_bwdpk_$TAG.txt 2>&1; grep -v amdgpu.ids gpurun_out/ab_bwdpk_$TAG.txt
