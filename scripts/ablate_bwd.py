@@ -26,7 +26,7 @@ ws = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(B, H, N, d) // 4, 
 dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
 flops = 2.5 * 4.0 * B * H * N * N * d / (2 if causal else 1)
 res = {p: [] for p in arms}
-for rnd in range(5):
+for rnd in range(int(os.environ.get("ROUNDS", "5"))):
     for p in arms:
         if env_vals:
             os.environ[env_name] = p
