@@ -102,6 +102,38 @@ def test_varlen_bf16_d64_vs_oracle(torch_dev, B, H, N, kv, causal, parity_record
                   bound="1e-3 + 2^-7 elementwise (tests/bounds.py)", **{f"{n}_max_abs": e for n, e in worst.items()})
 
 
+def test_varlen_bf16_causal_paired_fused(torch_dev, parity_record):
+    """kv_len on the causal fused backward's paired grid (light / heavy key blocks per
+    workgroup, taken when ceil(nkb / 2)·B·H >= 256): (4,32,1100,64), 384 paired workgroups,
+    rows of every padding kind (full, partial, one key, none); heads of each row against the
+    oracle, and zero dK / dV past kv_len everywhere."""
+    from bounds import grad_bounds
+    from minitorch import _hip
+    torch = torch_dev
+    B, H, N, d = 4, 32, 1100, 64
+    kv = (1100, 700, 1, 0)
+    rng = np.random.default_rng(1100)
+    q, k, v, do = (A.bf16_round(rng.standard_normal((B, H, N, d)).astype(np.float32)) for _ in range(4))
+    tq, tk, tv, tdo = (_dev(torch, x, torch.bfloat16) for x in (q, k, v, do))
+    o, m, l = _hip.flash_fwd(tq, tk, tv, True, kv_len=kv)
+    dq, dk, dv = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, True, kv_len=kv)
+    torch.cuda.synchronize()
+    worst = {}
+    for b, h in ((0, 0), (1, 17), (2, 31), (3, 5)):
+        sl = (slice(b, b + 1), slice(h, h + 1))
+        o_ref, m_ref, l_ref = A.attention_fwd(q[sl], k[sl], v[sl], True, kv[b:b + 1])
+        refs = A.attention_bwd(q[sl], k[sl], v[sl], o_ref, do[sl], m_ref, l_ref, True, kv[b:b + 1])
+        bnds = grad_bounds(q[b, h], k[b, h], v[b, h], do[b, h], True, kv=kv[b])
+        for got, ref, bd, name in zip((dq, dk, dv), refs, bnds, ("dq", "dk", "dv")):
+            e = np.abs(_np(got[b, h]) - ref[0, 0])
+            assert (e <= bd).all(), f"{name} (b,h)=({b},{h}) max-abs {e.max():.3e}, ratio {(e / bd).max():.3f}"
+            worst[name] = max(worst.get(name, 0.0), float(e.max()))
+    for b in range(B):
+        assert not _np(dk[b, :, kv[b]:]).any() and not _np(dv[b, :, kv[b]:]).any()
+    parity_record("test_varlen_bf16_causal_paired_fused", f"({B},{H},{N},64) kv={kv} causal",
+                  bound="tests/bounds.py", **{f"{n}_max_abs": e for n, e in worst.items()})
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_mha_padded_batch_branches_agree(torch_dev, causal):
     """MultiHeadAttention on a right-padded batch: the flash branch (kv_len in the kernel),
