@@ -25,6 +25,9 @@ steps = int(args[0]) if args else 5
 prof = sys.argv[sys.argv.index("--prof") + 1] if "--prof" in sys.argv else None
 B, T, V, E, H = 128, 39, 10000, 256, 8
 backend = minitorch.TensorBackend(minitorch.HipKernelOps)
+if os.environ.get("MT_GEMM") == "own":  # A/B: the library's own fp32 MFMA GEMM for every matmul
+    from minitorch import _hip
+    _hip.lib().mt_set_gemm_backend(1)
 rng = np.random.default_rng(0)
 lm = minitorch.DecoderLM(n_vocab=V, n_embd=E, n_head=H, n_positions=40, p_dropout=0.1, backend=backend,
                          use_fused_kernel=True, use_flash_attention=True)
