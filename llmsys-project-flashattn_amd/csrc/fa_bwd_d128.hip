@@ -52,10 +52,12 @@ constexpr int kT = 64;                 // streamed rows per tile
 constexpr int kW = 16;                 // stationary rows per wave
 constexpr int kNW = 8;                 // waves per workgroup
 constexpr int kBR = kW * kNW;          // stationary rows per workgroup
-constexpr int kImgB = kT * D * 2;      // bytes of one streamed tile image (16 KiB)
-constexpr int kSlotB = 2 * kImgB + 2 * kT * 4;  // Y1, Y2 images + the row constants (MODE 0)
-constexpr int kSmem = 2 * kSlotB;
-static_assert(kSmem <= 160 * 1024, "LDS budget");
+// a ring slot of a KT-row staging step: Y1, Y2 images (KT x 128 bf16 each) + the row constants
+// (MODE 0: KT of -lse2/c2, then KT of -δ)
+constexpr int img_bytes(int kt) { return kt * D * 2; }
+constexpr int slot_bytes(int kt) { return 2 * img_bytes(kt) + 2 * kt * 4; }
+constexpr int smem_bytes(int kt) { return 2 * slot_bytes(kt); }
+static_assert(smem_bytes(128) <= 160 * 1024, "LDS budget");
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
@@ -110,12 +112,17 @@ __device__ __forceinline__ void dma4(uint32_t lds, __amdgpu_buffer_rsrc_t rs, in
 }  // namespace
 
 // grid: ceil(N / 128) blocks of stationary rows x B·H, XCD-aware order (one head's blocks on
-// one XCD, where its streamed tiles stay in L2); 512 threads; kSmem bytes of LDS.
+// one XCD, where its streamed tiles stay in L2); 512 threads; smem_bytes(KT) of LDS.
 // PAIR (causal): a workgroup runs a light and a heavy block of one head as two passes (MODE 0:
 // key blocks nblk - 1 - u, then u; MODE 1: query blocks u, then nblk - 1 - u), so every
 // workgroup walks about nblk + 1 blocks' worth of tiles (the d = 64 kernels' pairing).
-template <int MODE, bool CAUSAL, bool PAIR = false, int AHEAD = 3>
+// KT: streamed rows staged per barrier step (64, or 128 = two 64-row halves computed in turn
+// between one pair of barriers: half the barriers and staging waits, twice the LDS)
+template <int MODE, bool CAUSAL, bool PAIR = false, int AHEAD = 3, int KT = 64>
 __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_head) {
+  constexpr int kImgB = img_bytes(KT), kSlotB = slot_bytes(KT);
+  constexpr int NP = KT / 32;  // LDS-DMA pieces of 4 rows per wave per image
+  constexpr int NH = KT / kT;  // 64-row halves per staging step
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -138,33 +145,34 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
       __builtin_amdgcn_make_buffer_rsrc((void*)Y1, (short)0, ((N - 1) * sy1 + D) * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t ry2 =
       __builtin_amdgcn_make_buffer_rsrc((void*)Y2, (short)0, ((N - 1) * sy2 + D) * 2, 0x00020000);
-  int yo1[2], yo2[2];
+  int yo1[NP], yo2[NP];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int dr = 4 * (2 * wave + j) + (lane >> 4), dc = lane & 15;
+  for (int j = 0; j < NP; ++j) {
+    const int dr = 4 * (NP * wave + j) + (lane >> 4), dc = lane & 15;
     const int cs = dc ^ ((dr & 7) << 1);
     yo1[j] = (dr * sy1 + cs * 8) * 2;
     yo2[j] = (dr * sy2 + cs * 8) * 2;
   }
   const uint32_t lds0 = bwdbf16::lds_base(smem);
-  // MODE 0 row constants: waves 0 and 1 each move 64 dwords (−lse2/c2, then −δ) per tile;
-  // a query past N reads an out-of-range offset, i.e. 0
+  // MODE 0 row constants: KT / 64 waves per tensor each move 64 dwords (−lse2/c2, then −δ) per
+  // staging step; a query past N reads an out-of-range offset, i.e. 0
   const __amdgpu_buffer_rsrc_t rcl = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.lse2 + (int64_t)bh * N), (short)0, N * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rcd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.delta + (int64_t)bh * N), (short)0, N * 4, 0x00020000);
   auto stage = [&](int t, int slot) __attribute__((always_inline)) {
     const uint32_t base = lds0 + slot * kSlotB;
-    const int row0 = t * kT;
+    const int row0 = t * KT;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const uint32_t off = (uint32_t)(4 * (2 * wave + j) * D * 2);
+    for (int j = 0; j < NP; ++j) {
+      const uint32_t off = (uint32_t)(4 * (NP * wave + j) * D * 2);
       dma16(base + off, ry1, yo1[j] + row0 * sy1 * 2);
       dma16(base + kImgB + off, ry2, yo2[j] + row0 * sy2 * 2);
     }
-    if (MODE == 0 && wave < 2) {
-      const int q = row0 + lane;
-      dma4(base + 2 * kImgB + wave * kT * 4, wave ? rcd : rcl, q < N ? q * 4 : 0x7ffffff0);
+    if (MODE == 0 && wave < 2 * (KT / 64)) {
+      const int tsel = wave / (KT / 64), ch = wave % (KT / 64);  // tensor (lse2, δ), 64-row chunk
+      const int q = row0 + 64 * ch + lane;
+      dma4(base + 2 * kImgB + (tsel * KT + 64 * ch) * 4, tsel ? rcd : rcl, q < N ? q * 4 : 0x7ffffff0);
     }
   };
 
@@ -220,9 +228,9 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
 
   // the tiles this workgroup walks: MODE 0 queries (causal: from the block's first key), MODE 1
   // keys (causal: up to the block's last query)
-  const int ntile_all = (N + kT - 1) / kT;
-  const int t0 = (MODE == 0 && CAUSAL) ? r0 / kT : 0;
-  const int t1 = (MODE == 1 && CAUSAL) ? min(ntile_all, (min(r0 + kBR, N) + kT - 1) / kT) : ntile_all;
+  const int ntile_all = (N + KT - 1) / KT;
+  const int t0 = (MODE == 0 && CAUSAL) ? r0 / KT : 0;
+  const int t1 = (MODE == 1 && CAUSAL) ? min(ntile_all, (min(r0 + kBR, N) + KT - 1) / KT) : ntile_all;
 
   f32x4 acc1[8], acc2[8];  // MODE 0: dKᵀ, dVᵀ [d block]; MODE 1: dQᵀ in acc1
 #pragma unroll
@@ -236,23 +244,25 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
   for (int t = t0; t < t1; ++t) {
     const int slot = (t - t0) & 1;
     if (t + 1 < t1) stage(t + 1, slot ^ 1);
-    const bf16* I1 = (const bf16*)(smem + slot * kSlotB);
-    const bf16* I2 = (const bf16*)(smem + slot * kSlotB + kImgB);
-    const float* cst = (const float*)(smem + slot * kSlotB + 2 * kImgB);
+#pragma unroll
+    for (int hh2 = 0; hh2 < NH; ++hh2) {  // the step's 64-row halves
+    const bf16* I1 = (const bf16*)(smem + slot * kSlotB) + hh2 * kT * D;
+    const bf16* I2 = (const bf16*)(smem + slot * kSlotB + kImgB) + hh2 * kT * D;
+    const float* cstl = (const float*)(smem + slot * kSlotB + 2 * kImgB) + hh2 * kT;
     // T1 = Y1·X1ᵀ, T2 = Y2·X2ᵀ over the tile's four 16-row blocks, from the row constants
     f32x4 T1[4], T2[4];
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) {
       if (MODE == 0) {
-        T1[rt] = *(const f32x4*)(cst + 16 * rt + 4 * g);
-        T2[rt] = *(const f32x4*)(cst + kT + 16 * rt + 4 * g);
+        T1[rt] = *(const f32x4*)(cstl + 16 * rt + 4 * g);
+        T2[rt] = *(const f32x4*)(cstl + KT + 16 * rt + 4 * g);
       } else {
         T1[rt] = f32x4{nl, nl, nl, nl};
         T2[rt] = f32x4{nd, nd, nd, nd};
       }
     }
     // causal: the diagonal tiles (a streamed row on the wrong side of the lane's row)
-    const int y0 = t * kT;  // first streamed row of the tile
+    const int y0 = t * KT + hh2 * kT;  // first streamed row of the half
     const bool diag = CAUSAL && (MODE == 0 ? y0 < rw + kW : y0 + kT - 1 > rw);
     bf16x8 pf[2], sf[2];  // P and dS of k-steps 0, 1 (B operands of the accumulate products)
     // The tile as one unrolled stream of MFMA slots (sched_barrier after each, so the source
@@ -334,6 +344,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    }  // half
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -387,10 +398,26 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
   MT_AH(12, 2) MT_AH(14, 4) MT_AH(15, 5)
 #undef MT_AH
 #endif
-  for (auto k : {kd, kq}) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
+  int kt_d = 64, kt_q = 64;
+#ifdef MT_DIAGNOSTICS
+  // 128-row staging steps (knob 17: both passes, 18: the dQ pass, 19: the dK/dV pass)
+  if (a.knob == 17 || a.knob == 19) {
+    kd = pair ? fa_bwd_d128_bf16<0, true, true, 3, 128> : causal ? fa_bwd_d128_bf16<0, true, false, 3, 128>
+                                                          : fa_bwd_d128_bf16<0, false, false, 3, 128>;
+    kt_d = 128;
+  }
+  if (a.knob == 17 || a.knob == 18) {
+    kq = pair ? fa_bwd_d128_bf16<1, true, true, 3, 128> : causal ? fa_bwd_d128_bf16<1, true, false, 3, 128>
+                                                          : fa_bwd_d128_bf16<1, false, false, 3, 128>;
+    kt_q = 128;
+  }
+#endif
+  for (int pass = 0; pass < 2; ++pass) {
+    void (*k)(AttnArgs, int) = pass ? kq : kd;
+    const int smem = smem_bytes(pass ? kt_q : kt_d);
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(512), kSmem, st, a, nbh);
+    hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(512), smem, st, a, nbh);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -1,0 +1,7 @@
+# round 4: the d = 128 backward with 128-row staging steps (knob 17 both passes, 18 dQ, 19 dK/dV)
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${TAG:-r4r}
+DIAGLIB=$PWD/llmsys-project-flashattn_amd/minitorch/_lib/diag/libminitorch_hip_diag.so
+MT_HIP_LIB=$DIAGLIB MT_KNOB=17 timeout -k 10 600 python -u -m pytest tests/test_flash_gpu.py -k "d128" -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/tests_d128kt_$TAG.log 2>&1; rc=$?; grep -E "FAILED|Error|passed|failed" gpurun_out/tests_d128kt_$TAG.log | tail -5; [ $rc -eq 0 ] || exit $rc
+SHAPE=8,16,4096,128 ROUNDS=6 MT_DIAG=1 ENVAB=MT_KNOB:0,17,18,19 timeout -k 10 300 python scripts/ablate_bwd.py 0 > gpurun_out/ab_d128kt_$TAG.txt 2>&1 && SHAPE=8,16,4096,128 ROUNDS=6 MT_DIAG=1 ENVAB=MT_KNOB:0,17 timeout -k 10 300 python scripts/ablate_bwd.py 0 causal >> gpurun_out/ab_d128kt_$TAG.txt 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_d128kt_$TAG.txt; exit $rc
