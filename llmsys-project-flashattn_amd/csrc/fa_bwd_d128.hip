@@ -1,5 +1,7 @@
 // FlashAttention backward, bf16 I/O, head dim 128 (BASELINE config 4's head dim): the split
-// form (a dK/dV pass and a dQ pass) on the 16x16x32 MFMA, two waves per SIMD.
+// form (a dK/dV pass and a dQ pass) on the 16x16x32 MFMA. Two kernel bodies: the two-wave form
+// (16 stationary rows per wave, 8 waves; described below) and the product's one-wave-per-SIMD
+// form (32 stationary rows per wave, 4 waves; fa_bwd_d128w_bf16), same layouts and slot stream.
 //
 // Same mathematics as every backward here (reference backward_kernel,
 // src/flashattention_kernel.cu:115-255, with its dV term corrected):
@@ -62,11 +64,20 @@ static_assert(smem_bytes(128) <= 160 * 1024, "LDS budget");
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 __device__ __forceinline__ int swz(int r, int c) { return r * D + ((c ^ ((r & 7) << 1)) << 3); }
 
 __device__ __forceinline__ f32x4 mma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// dst += a·b on the 16x16x32 MFMA with the accumulator pinned to AGPRs (the one-wave form: its
+// score tiles take the VGPR form, file flag -amdgpu-mfma-vgpr-form, so the softmax reads them
+// directly; pinning keeps hipcc from parking loop-carried accumulators in VGPRs and copying
+// them over for every product). Only ever followed by its own next product, tiles later.
+__device__ __forceinline__ void mma16a(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
 
 // Yᵀ fragment (A operand of an accumulate product): d block dt, streamed rows 32 kq + 4 g + 0..3
@@ -373,6 +384,303 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
   }  // pass
 }
 
+// The one-wave-per-SIMD form of the same two passes: 4 waves of 32 stationary rows (two 16-row
+// groups sg, both in registers) per 128-row block, so every streamed operand read from LDS
+// feeds two MFMAs (half the LDS traffic per product of the form above) and no second wave
+// competes for the SIMD's issue port; the price is registers (the accumulators live in AGPRs)
+// and a barrier every SIMD waits at with nothing else to run. So the barrier step is hidden:
+// a three-slot ring staged two tiles ahead keeps the next tile published during the current
+// one, and the operand ring runs across the tile boundary (the last kAhead slots of a tile read
+// the first operands of the next, and its row constants load during the last accumulate
+// products), so the first MFMAs after the barrier find their operands in registers.
+// PK: the softmax on score pairs (packed multiplies: two scores per VALU instruction)
+// ABL (timing-only ablations, WRONG results, diagnostics build): 1 no barrier in the tile loop,
+// 2 no softmax (scores packed as they are), 4 no staging in the tile loop
+template <int MODE, bool CAUSAL, bool PAIR = false, bool PK = true, int ABL = 0>
+__global__ __launch_bounds__(256, 1) void fa_bwd_d128w_bf16(AttnArgs p, int nblk_head) {
+  constexpr int kImgB = img_bytes(kT), kSlotB = slot_bytes(kT);
+  constexpr int kWw = 32;     // stationary rows per wave
+  constexpr int NP = 4;       // LDS-DMA pieces of 4 rows per wave per image
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i16 = lane & 15;
+  const int N = p.N;
+  const int logical = bwdbf16::xcd_remap(blockIdx.x, gridDim.x);
+  const int nslot = PAIR ? (nblk_head + 1) / 2 : nblk_head;
+  const int bh = logical / nslot, u_ = logical % nslot;
+  const int b = bh / p.H, hh = bh % p.H;
+
+  const bf16* Y1 = MODE == 0 ? (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1]
+                             : (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const bf16* Y2 = MODE == 0 ? (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1]
+                             : (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const int sy1 = (int)(MODE == 0 ? p.sq[2] : p.sk[2]), sy2 = (int)(MODE == 0 ? p.sdo[2] : p.sv[2]);
+  const __amdgpu_buffer_rsrc_t ry1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Y1, (short)0, ((N - 1) * sy1 + D) * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Y2, (short)0, ((N - 1) * sy2 + D) * 2, 0x00020000);
+  int yo1[NP], yo2[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int dr = 4 * (NP * wave + j) + (lane >> 4), dc = lane & 15;
+    const int cs = dc ^ ((dr & 7) << 1);
+    yo1[j] = (dr * sy1 + cs * 8) * 2;
+    yo2[j] = (dr * sy2 + cs * 8) * 2;
+  }
+  const uint32_t lds0 = bwdbf16::lds_base(smem);
+  const __amdgpu_buffer_rsrc_t rcl = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.lse2 + (int64_t)bh * N), (short)0, N * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rcd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.delta + (int64_t)bh * N), (short)0, N * 4, 0x00020000);
+  auto stage = [&](int t, int slot) __attribute__((always_inline)) {
+    const uint32_t base = lds0 + slot * kSlotB;
+    const int row0 = t * kT;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const uint32_t off = (uint32_t)(4 * (NP * wave + j) * D * 2);
+      dma16(base + off, ry1, yo1[j] + row0 * sy1 * 2);
+      dma16(base + kImgB + off, ry2, yo2[j] + row0 * sy2 * 2);
+    }
+    if (MODE == 0 && wave < 2) {  // wave 0: −lse2/c2, wave 1: −δ
+      const int q = row0 + lane;
+      dma4(base + 2 * kImgB + wave * kT * 4, wave ? rcd : rcl, q < N ? q * 4 : 0x7ffffff0);
+    }
+  };
+  int ro[4], to[8];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) ro[ks] = swz(i16, 4 * ks + g);
+  {
+    const int q = i16 >> 2, pp = i16 & 3, row = 4 * g + q;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) to[dt] = swz(row, 2 * dt + (pp >> 1)) + 4 * (pp & 1);
+  }
+
+#pragma nounroll
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+  const int light = MODE == 0 ? nblk_head - 1 - u_ : u_, heavy = nblk_head - 1 - light;
+  const int blk = PAIR ? (pass == 0 ? light : heavy) : u_;
+  if (PAIR && pass == 1 && heavy == light) break;
+  const int r0 = blk * kBR;
+  const int rw = r0 + wave * kWw;
+  int my[2];
+  my[0] = rw + i16;
+  my[1] = rw + 16 + i16;
+  const float c2 = p.scale_log2;
+
+  const bf16* X1 = MODE == 0 ? (const bf16*)p.k + b * p.sk[0] + hh * p.sk[1]
+                             : (const bf16*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const bf16* X2 = MODE == 0 ? (const bf16*)p.v + b * p.sv[0] + hh * p.sv[1]
+                             : (const bf16*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const int64_t sx1 = MODE == 0 ? p.sk[2] : p.sq[2], sx2 = MODE == 0 ? p.sv[2] : p.sdo[2];
+  bf16x8 xf1[2][4], xf2[2][4];
+  float nl[2] = {0.f, 0.f}, nd[2] = {0.f, 0.f};
+#pragma unroll
+  for (int sg = 0; sg < 2; ++sg) {
+    const int rr = min(my[sg], N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      xf1[sg][ks] = *(const bf16x8*)(X1 + (int64_t)rr * sx1 + 32 * ks + 8 * g);
+      xf2[sg][ks] = *(const bf16x8*)(X2 + (int64_t)rr * sx2 + 32 * ks + 8 * g);
+    }
+    if (MODE == 1 && my[sg] < N) {
+      nl[sg] = p.lse2[(int64_t)bh * N + my[sg]];
+      nd[sg] = p.delta[(int64_t)bh * N + my[sg]];
+    }
+  }
+  // (waited here, not at first use inside the loop: see the form above)
+#pragma unroll
+  for (int sg = 0; sg < 2; ++sg) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(xf1[sg][ks]), "v"(xf2[sg][ks]));
+    asm volatile("" ::"v"(nl[sg]), "v"(nd[sg]));
+  }
+
+  const int ntile_all = (N + kT - 1) / kT;
+  const int t0 = (MODE == 0 && CAUSAL) ? r0 / kT : 0;
+  const int t1 = (MODE == 1 && CAUSAL) ? min(ntile_all, (min(r0 + kBR, N) + kT - 1) / kT) : ntile_all;
+
+  f32x4 acc1[2][8], acc2[2][8];
+#pragma unroll
+  for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) { acc1[sg][dt] = f32x4{}; acc2[sg][dt] = f32x4{}; }
+
+  if (t0 < t1) {
+    stage(t0, 0);
+    if (t0 + 1 < t1) stage(t0 + 1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  constexpr int kNA = MODE == 0 ? 16 : 8;
+  constexpr int kL = 32 + 2 * kNA;
+  constexpr int kAhead = 7, kR = kAhead + 1;
+  static_assert(kL % kR == 0, "the operand ring runs across tiles");
+  auto operand = [&](const bf16* I1, const bf16* I2, int m) __attribute__((always_inline)) -> bf16x8 {
+    if (m < 32) {
+      const int idx = m >> 1, rt = 2 * (idx >> 3) + (idx & 1), ks = (idx >> 1) & 3;
+      return *(const bf16x8*)(((m & 1) ? I2 : I1) + 16 * rt * D + ro[ks]);
+    }
+    const int j = m - 32, kq = j / kNA, jj = j % kNA;
+    if (MODE == 0) return trread((jj & 1) ? I1 : I2, to, kq, jj >> 1);
+    return trread(I1, to, kq, jj);
+  };
+  f32x4 T1[2][4], T2[2][4];
+  auto tinit = [&](int slot) __attribute__((always_inline)) {
+    const float* cst = (const float*)(smem + slot * kSlotB + 2 * kImgB);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      if (MODE == 0) {
+        const f32x4 l = *(const f32x4*)(cst + 16 * rt + 4 * g);
+        const f32x4 d = *(const f32x4*)(cst + kT + 16 * rt + 4 * g);
+        T1[0][rt] = l; T1[1][rt] = l;
+        T2[0][rt] = d; T2[1][rt] = d;
+      } else {
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) {
+          T1[sg][rt] = f32x4{nl[sg], nl[sg], nl[sg], nl[sg]};
+          T2[sg][rt] = f32x4{nd[sg], nd[sg], nd[sg], nd[sg]};
+        }
+      }
+    }
+  };
+  bf16x8 ring[kR];
+  tinit(0);
+  {
+    const bf16* I1 = (const bf16*)smem;
+    const bf16* I2 = (const bf16*)(smem + kImgB);
+#pragma unroll
+    for (int m = 0; m < kAhead; ++m) ring[m] = operand(I1, I2, m);
+  }
+  int cur = 0;
+  for (int t = t0; t < t1; ++t) {
+    const int nxt = cur == 2 ? 0 : cur + 1, nn = nxt == 2 ? 0 : nxt + 1;
+    if (!(ABL & 4) && t + 2 < t1) stage(t + 2, nn);
+    const bf16* I1 = (const bf16*)(smem + cur * kSlotB);
+    const bf16* I2 = (const bf16*)(smem + cur * kSlotB + kImgB);
+    const bf16* N1 = (const bf16*)(smem + nxt * kSlotB);
+    const bf16* N2 = (const bf16*)(smem + nxt * kSlotB + kImgB);
+    const int y0 = t * kT;
+    const bool diag = CAUSAL && (MODE == 0 ? y0 < rw + kWw : y0 + kT - 1 > rw);
+    bf16x8 pf[2][2], sf[2][2];  // [k-step][sg]
+    auto item = [&](int kq, int sg, int it) __attribute__((always_inline)) {
+      const int rt = 2 * kq + (it >> 2), r = it & 3;
+      float x = T1[sg][rt][r];
+      if (diag) {
+        const int y = y0 + 16 * rt + 4 * g + r;
+        if (MODE == 0 ? my[sg] > y : y > my[sg]) x = -INFINITY;
+      }
+      const float pv = __builtin_amdgcn_exp2f(x * c2);
+      T1[sg][rt][r] = pv;
+      T2[sg][rt][r] = pv * T2[sg][rt][r];
+    };
+    auto piece = [&](int kq, int sg, int k) __attribute__((always_inline)) {
+      const int rt = 2 * kq + (k >> 1), r = 2 * (k & 1);
+      if (MODE == 0) {
+        pf[kq][sg][2 * k] = (bf16)T1[sg][rt][r];
+        pf[kq][sg][2 * k + 1] = (bf16)T1[sg][rt][r + 1];
+      }
+      sf[kq][sg][2 * k] = (bf16)T2[sg][rt][r];
+      sf[kq][sg][2 * k + 1] = (bf16)T2[sg][rt][r + 1];
+    };
+    // scores (rt, r), (rt, r + 1) of pair ip (0..3) of k-step kq
+    auto item2 = [&](int kq, int sg, int ip) __attribute__((always_inline)) {
+      const int rt = 2 * kq + (ip >> 1), r = 2 * (ip & 1);
+      f32x2 x = f32x2{T1[sg][rt][r], T1[sg][rt][r + 1]} * f32x2{c2, c2};
+      if (diag) {
+        const int y = y0 + 16 * rt + 4 * g + r;
+        if (MODE == 0 ? my[sg] > y : y > my[sg]) x[0] = -INFINITY;
+        if (MODE == 0 ? my[sg] > y + 1 : y + 1 > my[sg]) x[1] = -INFINITY;
+      }
+      const f32x2 pv = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+      const f32x2 ds = pv * f32x2{T2[sg][rt][r], T2[sg][rt][r + 1]};
+      T1[sg][rt][r] = pv[0]; T1[sg][rt][r + 1] = pv[1];
+      T2[sg][rt][r] = ds[0]; T2[sg][rt][r + 1] = ds[1];
+    };
+    // softmax action a of k-step kq: items (sg alternating), then packs (24 actions; PK: 16)
+    constexpr int kAct = PK ? 16 : 24;
+    auto action = [&](int kq, int a) __attribute__((always_inline)) {
+      if (ABL & 2) {
+        if (a < 8) piece(kq, a & 1, a >> 1);
+      } else if (PK) {
+        if (a < 8) item2(kq, a & 1, a >> 1);
+        else piece(kq, (a - 8) & 1, (a - 8) >> 1);
+      } else {
+        if (a < 16) item(kq, a & 1, a >> 1);
+        else piece(kq, (a - 16) & 1, (a - 16) >> 1);
+      }
+    };
+#pragma unroll
+    for (int m = 0; m < kL; ++m) {
+      const int mp = m + kAhead;
+      ring[mp % kR] = mp < kL ? operand(I1, I2, mp) : operand(N1, N2, mp - kL);
+      const bf16x8 a = ring[m % kR];
+      if (m < 32) {
+        const int idx = m >> 1, rt = 2 * (idx >> 3) + (idx & 1), ks = (idx >> 1) & 3;
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) {
+          if (m & 1) T2[sg][rt] = mma16(a, xf2[sg][ks], T2[sg][rt]);
+          else T1[sg][rt] = mma16(a, xf1[sg][ks], T1[sg][rt]);
+        }
+      } else {
+        const int j = m - 32, kq = j / kNA, jj = j % kNA;
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) {
+          if (MODE == 0) {
+            if (jj & 1) mma16a(acc1[sg][jj >> 1], a, sf[kq][sg]);
+            else mma16a(acc2[sg][jj >> 1], a, pf[kq][sg]);
+          } else {
+            mma16a(acc1[sg][jj], a, sf[kq][sg]);
+          }
+        }
+      }
+      // softmax of k-step 0 beside the T products of k-step 1 (slots [16, 32)), of k-step 1
+      // beside the accumulate products of k-step 0 (slots [32, 32 + kNA))
+      const int kq = m < 32 ? 0 : 1, w = m < 32 ? m - 16 : m - 32;
+      const int wl = kq == 0 ? 16 : kNA;
+      if (w >= 0 && w < wl) {
+#pragma unroll
+        for (int a2 = w * kAct / wl; a2 < (w + 1) * kAct / wl; ++a2) action(kq, a2);
+      }
+      // the next tile's row constants, once k-step 1's scores are packed
+      if (m == 32 + kNA) tinit(nxt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!(ABL & 1)) __syncthreads();
+    cur = nxt;
+  }
+
+  if (true) {
+    const float sc = p.scale;
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+      if (my[sg] >= N) continue;
+      if (MODE == 0) {
+        bf16* dKg = (bf16*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my[sg] * p.sdk[2];
+        bf16* dVg = (bf16*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my[sg] * p.sdv[2];
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const int col = 16 * dt + 4 * g;
+          store4(dKg + col, acc1[sg][dt][0] * sc, acc1[sg][dt][1] * sc, acc1[sg][dt][2] * sc,
+                 acc1[sg][dt][3] * sc, true);
+          store4(dVg + col, acc2[sg][dt][0], acc2[sg][dt][1], acc2[sg][dt][2], acc2[sg][dt][3], true);
+        }
+      } else {
+        bf16* dQg = (bf16*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)my[sg] * p.sdq[2];
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const int col = 16 * dt + 4 * g;
+          store4(dQg + col, acc1[sg][dt][0] * sc, acc1[sg][dt][1] * sc, acc1[sg][dt][2] * sc,
+                 acc1[sg][dt][3] * sc, true);
+        }
+      }
+    }
+  }
+  }  // pass
+}
+
 // The two passes after the d = 128 prep (fa_bwd_prep_bf16<128>). bf16, d = 128, 16-B rows,
 // every per-head row offset (plus one tile past N) inside the 31-bit buffer range.
 hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st) {
@@ -384,12 +692,23 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
 #endif
   const int64_t nblk = (int64_t)(pair ? (nbh + 1) / 2 : nbh) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  void (*kd)(AttnArgs, int) = pair ? fa_bwd_d128_bf16<0, true, true>
-                              : causal ? fa_bwd_d128_bf16<0, true> : fa_bwd_d128_bf16<0, false>;
-  void (*kq)(AttnArgs, int) = pair ? fa_bwd_d128_bf16<1, true, true>
-                              : causal ? fa_bwd_d128_bf16<1, true> : fa_bwd_d128_bf16<1, false>;
+  // the one-wave-per-SIMD form for both passes (round 4: 3.40 -> 3.30 ms non-causal, 2.08 ->
+  // 1.99 ms causal at (8,16,4096,128) against the two-wave form)
+  void (*kd)(AttnArgs, int) = pair ? fa_bwd_d128w_bf16<0, true, true>
+                              : causal ? fa_bwd_d128w_bf16<0, true> : fa_bwd_d128w_bf16<0, false>;
+  void (*kq)(AttnArgs, int) = pair ? fa_bwd_d128w_bf16<1, true, true>
+                              : causal ? fa_bwd_d128w_bf16<1, true> : fa_bwd_d128w_bf16<1, false>;
+  bool wd = true, wq = true;
+  int kt_d = 64, kt_q = 64;
 #ifdef MT_DIAGNOSTICS
-  // operand-read distance A/B (knobs 12 / 14 / 15: 2 / 4 / 5 MFMA slots ahead), non-causal
+  // the two-wave form (knob 34: both passes; 12 / 14 / 15: with operand reads 2 / 4 / 5 MFMA
+  // slots ahead, non-causal; 17 / 18 / 19: 128-row staging steps in both passes / the dQ pass
+  // / the dK/dV pass, the other pass in the one-wave form)
+  if (a.knob == 34 || a.knob == 12 || a.knob == 14 || a.knob == 15) {
+    kd = pair ? fa_bwd_d128_bf16<0, true, true> : causal ? fa_bwd_d128_bf16<0, true> : fa_bwd_d128_bf16<0, false>;
+    kq = pair ? fa_bwd_d128_bf16<1, true, true> : causal ? fa_bwd_d128_bf16<1, true> : fa_bwd_d128_bf16<1, false>;
+    wd = wq = false;
+  }
 #define MT_AH(K, A)                                                       \
   if (!causal && a.knob == K) {                                           \
     kd = fa_bwd_d128_bf16<0, false, false, A>;                            \
@@ -397,27 +716,40 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
   }
   MT_AH(12, 2) MT_AH(14, 4) MT_AH(15, 5)
 #undef MT_AH
-#endif
-  int kt_d = 64, kt_q = 64;
-#ifdef MT_DIAGNOSTICS
-  // 128-row staging steps (knob 17: both passes, 18: the dQ pass, 19: the dK/dV pass)
   if (a.knob == 17 || a.knob == 19) {
     kd = pair ? fa_bwd_d128_bf16<0, true, true, 3, 128> : causal ? fa_bwd_d128_bf16<0, true, false, 3, 128>
                                                           : fa_bwd_d128_bf16<0, false, false, 3, 128>;
     kt_d = 128;
+    wd = false;
   }
   if (a.knob == 17 || a.knob == 18) {
     kq = pair ? fa_bwd_d128_bf16<1, true, true, 3, 128> : causal ? fa_bwd_d128_bf16<1, true, false, 3, 128>
                                                           : fa_bwd_d128_bf16<1, false, false, 3, 128>;
     kt_q = 128;
+    wq = false;
   }
+  // the one-wave form without the packed softmax (knob 20), and its timing-only ablations
+  // (29 / 30 / 31: ABL 1 / 2 / 4)
+#define MT_W(PK, ABL)                                                                              \
+  {                                                                                                \
+    kd = pair ? fa_bwd_d128w_bf16<0, true, true, PK, ABL> : causal ? fa_bwd_d128w_bf16<0, true, false, PK, ABL> \
+                                                          : fa_bwd_d128w_bf16<0, false, false, PK, ABL>; \
+    kq = pair ? fa_bwd_d128w_bf16<1, true, true, PK, ABL> : causal ? fa_bwd_d128w_bf16<1, true, false, PK, ABL> \
+                                                          : fa_bwd_d128w_bf16<1, false, false, PK, ABL>; \
+  }
+  if (a.knob == 20) MT_W(false, 0)
+  if (a.knob == 29) MT_W(true, 1)
+  if (a.knob == 30) MT_W(true, 2)
+  if (a.knob == 31) MT_W(true, 4)
+#undef MT_W
 #endif
   for (int pass = 0; pass < 2; ++pass) {
     void (*k)(AttnArgs, int) = pass ? kq : kd;
-    const int smem = smem_bytes(pass ? kt_q : kt_d);
+    const bool w = pass ? wq : wd;
+    const int smem = w ? 3 * slot_bytes(kT) : smem_bytes(pass ? kt_q : kt_d);
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(512), smem, st, a, nbh);
+    hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(w ? 256 : 512), smem, st, a, nbh);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
