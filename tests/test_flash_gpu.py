@@ -467,14 +467,17 @@ def test_bf16_bwd_fused_long_vs_oracle(torch_dev, N, causal, parity_record):
                       heads=2, max_abs=e, max_err_over_bound=r)
 
 
-@pytest.mark.parametrize("shape", [(1, 2, 128, 128), (1, 3, 200, 128), (2, 2, 1000, 128),
+@pytest.mark.parametrize("shape", [(1, 2, 17, 128), (1, 2, 128, 128), (1, 2, 129, 128),
+                                   (1, 3, 200, 128), (1, 1, 320, 128), (2, 2, 1000, 128),
                                    (1, 2, 2048, 128)])
 @pytest.mark.parametrize("causal", [False, True])
 def test_bf16_bwd_d128_vs_oracle(torch_dev, shape, causal, parity_record):
-    """The d = 128 split backward (fa_bwd_d128.hip: 16 keys / queries per wave on the
-    16x16x32 MFMA) against the C oracle under tests/bounds.py on whole heads: one block, a
-    ragged N (partial tiles and a partial block of 128), several blocks of both passes, and a
-    causal grid with blocks on both sides of the diagonal."""
+    """The d = 128 split backward (fa_bwd_d128.hip, the one-wave form: 32 keys / queries per
+    wave on the 16x16x32 MFMA, a three-slot tile ring staged two tiles ahead) against the C
+    oracle under tests/bounds.py on whole heads: a single partial tile (N = 17), one block, a
+    one-row second block (N = 129: three tiles, every ring slot once), a ragged N, five tiles
+    (the ring wraps), several blocks of both passes, and a causal grid with blocks on both
+    sides of the diagonal."""
     from minitorch import _hip
     torch = torch_dev
     g = torch.Generator(device="cuda").manual_seed(sum(shape) + causal)
