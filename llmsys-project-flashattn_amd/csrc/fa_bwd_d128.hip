@@ -409,7 +409,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
 // PK: the softmax on score pairs (packed multiplies: two scores per VALU instruction)
 // ABL (timing-only ablations, WRONG results, diagnostics build): 1 no barrier in the tile loop,
 // 2 no softmax (scores packed as they are), 4 no staging in the tile loop
-template <int MODE, bool CAUSAL, bool PAIR = false, bool PK = true, int ABL = 0>
+template <int MODE, bool CAUSAL, bool PAIR = false, bool PK = true, int ABL = 0, int AH = 7>
 __global__ __launch_bounds__(256, 1) void fa_bwd_d128w_bf16(AttnArgs p, int nblk_head) {
   constexpr int kImgB = img_bytes(kT), kSlotB = slot_bytes(kT);
   constexpr int kWw = 32;     // stationary rows per wave
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_d128w_bf16(AttnArgs p, int nblk
 
   constexpr int kNA = MODE == 0 ? 16 : 8;
   constexpr int kL = 32 + 2 * kNA;
-  constexpr int kAhead = 7, kR = kAhead + 1;
+  constexpr int kAhead = AH, kR = kAhead + 1;  // (diagnostics A/B: 3, 15)
   static_assert(kL % kR == 0, "the operand ring runs across tiles");
   auto operand = [&](const bf16* I1, const bf16* I2, int m) __attribute__((always_inline)) -> bf16x8 {
     if (m < 32) {
@@ -1047,6 +1047,16 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
                                                         : fa_bwd_d128x_bf16<1, false, false, ABL>; \
   }
   if (a.knob >= 36 && a.knob <= 38) MT_X(0)
+  // the one-wave form's operand ring 3 / 15 slots ahead (knobs 43 / 44)
+#define MT_A(K, AH)                                                                               \
+  if (a.knob == K) {                                                                              \
+    kd = pair ? fa_bwd_d128w_bf16<0, true, true, true, 0, AH> : causal ? fa_bwd_d128w_bf16<0, true, false, true, 0, AH> \
+                                                              : fa_bwd_d128w_bf16<0, false, false, true, 0, AH>; \
+    kq = pair ? fa_bwd_d128w_bf16<1, true, true, true, 0, AH> : causal ? fa_bwd_d128w_bf16<1, true, false, true, 0, AH> \
+                                                              : fa_bwd_d128w_bf16<1, false, false, true, 0, AH>; \
+  }
+  MT_A(43, 3) MT_A(44, 15)
+#undef MT_A
   if (a.knob == 39) MT_X(1)
   if (a.knob == 40) MT_X(2)
   if (a.knob == 41) MT_X(4)
