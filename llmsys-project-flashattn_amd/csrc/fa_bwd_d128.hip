@@ -409,11 +409,14 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
 // PK: the softmax on score pairs (packed multiplies: two scores per VALU instruction)
 // ABL (timing-only ablations, WRONG results, diagnostics build): 1 no barrier in the tile loop,
 // 2 no softmax (scores packed as they are), 4 no staging in the tile loop
-template <int MODE, bool CAUSAL, bool PAIR = false, bool PK = true, int ABL = 0, int AH = 7>
-__global__ __launch_bounds__(256, 1) void fa_bwd_d128w_bf16(AttnArgs p, int nblk_head) {
+// NWV: waves per workgroup (4: one per SIMD; 8: two per SIMD, 256 stationary rows, for a
+// kernel that fits 256 registers)
+template <int MODE, bool CAUSAL, bool PAIR = false, bool PK = true, int ABL = 0, int AH = 7, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, NWV / 4) void fa_bwd_d128w_bf16(AttnArgs p, int nblk_head) {
   constexpr int kImgB = img_bytes(kT), kSlotB = slot_bytes(kT);
   constexpr int kWw = 32;     // stationary rows per wave
-  constexpr int NP = 4;       // LDS-DMA pieces of 4 rows per wave per image
+  constexpr int NP = 16 / NWV;  // LDS-DMA pieces of 4 rows per wave per image
+  constexpr int kBRw = kWw * NWV;  // stationary rows per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -474,7 +477,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_d128w_bf16(AttnArgs p, int nblk
   const int light = MODE == 0 ? nblk_head - 1 - u_ : u_, heavy = nblk_head - 1 - light;
   const int blk = PAIR ? (pass == 0 ? light : heavy) : u_;
   if (PAIR && pass == 1 && heavy == light) break;
-  const int r0 = blk * kBR;
+  const int r0 = blk * kBRw;
   const int rw = r0 + wave * kWw;
   int my[2];
   my[0] = rw + i16;
@@ -511,7 +514,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_d128w_bf16(AttnArgs p, int nblk
 
   const int ntile_all = (N + kT - 1) / kT;
   const int t0 = (MODE == 0 && CAUSAL) ? r0 / kT : 0;
-  const int t1 = (MODE == 1 && CAUSAL) ? min(ntile_all, (min(r0 + kBR, N) + kT - 1) / kT) : ntile_all;
+  const int t1 = (MODE == 1 && CAUSAL) ? min(ntile_all, (min(r0 + kBRw, N) + kT - 1) / kT) : ntile_all;
 
   f32x4 acc1[2][8], acc2[2][8];
 #pragma unroll
@@ -643,6 +646,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_d128w_bf16(AttnArgs p, int nblk
           if (MODE == 0) {
             if (jj & 1) mma16a(acc1[sg][jj >> 1], a, sf[kq][sg]);
             else mma16a(acc2[sg][jj >> 1], a, pf[kq][sg]);
+          } else if (NWV == 8) {  // all in VGPRs (the 256-register budget of two waves)
+            acc1[sg][jj] = mma16(a, sf[kq][sg], acc1[sg][jj]);
           } else {
             mma16a(acc1[sg][jj], a, sf[kq][sg]);
           }
@@ -989,11 +994,25 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
   // 1.99 ms causal at (8,16,4096,128) against the two-wave form)
   void (*kd)(AttnArgs, int) = pair ? fa_bwd_d128w_bf16<0, true, true>
                               : causal ? fa_bwd_d128w_bf16<0, true> : fa_bwd_d128w_bf16<0, false>;
-  void (*kq)(AttnArgs, int) = pair ? fa_bwd_d128w_bf16<1, true, true>
-                              : causal ? fa_bwd_d128w_bf16<1, true> : fa_bwd_d128w_bf16<1, false>;
+  // the dQ pass in 8-wave workgroups of the same form, two waves per SIMD (256 query rows per
+  // workgroup, the accumulators in VGPRs: 244 registers non-causal with the operand ring 3 slots
+  // ahead; causal with light / heavy pairs of 256-row blocks and the ring 2 ahead, 9 registers
+  // spilled), while the grid still holds a workgroup per CU: (8,16,4096,128) 3.31 -> 3.09 ms,
+  // causal 1.96 -> 1.86 ms; at (2,8,1024,128), 64 workgroups, the 8-wave pass was 0.084
+  // against 0.071 ms
+  const int nbh8 = (a.N + 255) / 256;
+  bool q8 = !causal && (int64_t)nbh8 * a.B * a.H >= 256;
+  bool q8p = causal && (int64_t)((nbh8 + 1) / 2) * a.B * a.H >= 256;
+  void (*kq)(AttnArgs, int) = q8p ? fa_bwd_d128w_bf16<1, true, true, true, 0, 2, 8>
+                              : pair ? fa_bwd_d128w_bf16<1, true, true>
+                              : causal ? fa_bwd_d128w_bf16<1, true>
+                              : q8 ? fa_bwd_d128w_bf16<1, false, false, true, 0, 3, 8> : fa_bwd_d128w_bf16<1, false>;
   bool wd = true, wq = true;
   int kt_d = 64, kt_q = 64;
 #ifdef MT_DIAGNOSTICS
+  void (*const kq_product)(AttnArgs, int) = kq;
+  // knob 50: the dQ pass in the 4-wave form at any grid
+  if (a.knob == 50) kq = pair ? fa_bwd_d128w_bf16<1, true, true> : causal ? fa_bwd_d128w_bf16<1, true> : fa_bwd_d128w_bf16<1, false>;
   // the two-wave form (knob 34: both passes; 12 / 14 / 15: with operand reads 2 / 4 / 5 MFMA
   // slots ahead, non-causal; 17 / 18 / 19: 128-row staging steps in both passes / the dQ pass
   // / the dK/dV pass, the other pass in the one-wave form)
@@ -1062,13 +1081,27 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
   if (a.knob == 41) MT_X(4)
 #undef MT_X
 #endif
+#ifdef MT_DIAGNOSTICS
+  if (kq != kq_product) q8 = q8p = false;  // a diagnostics form replaced the dQ kernel
+  // the 8-wave dQ pass with the operand ring 2 (knob 48) / 5 (knob 49) slots ahead, and causal
+  // ones (47: 3 ahead, 9 registers spilled; 48: 2 ahead)
+  if (a.knob == 47 || a.knob == 48 || (a.knob == 49 && !causal)) {
+    kq = a.knob == 49 ? fa_bwd_d128w_bf16<1, false, false, true, 0, 5, 8>
+         : a.knob == 48 ? (causal ? fa_bwd_d128w_bf16<1, true, false, true, 0, 2, 8> : fa_bwd_d128w_bf16<1, false, false, true, 0, 2, 8>)
+         : causal ? fa_bwd_d128w_bf16<1, true, false, true, 0, 3, 8> : fa_bwd_d128w_bf16<1, false, false, true, 0, 3, 8>;
+    q8 = true;
+  }
+#endif
+  const int nbh_q = (q8 || q8p) ? nbh8 : nbh;
+  const int64_t nblk_q = q8 ? (int64_t)nbh8 * a.B * a.H : q8p ? (int64_t)((nbh8 + 1) / 2) * a.B * a.H : nblk;
   for (int pass = 0; pass < 2; ++pass) {
     void (*k)(AttnArgs, int) = pass ? kq : kd;
     const bool w = pass ? wq : wd;
     const int smem = w ? 3 * slot_bytes(kT) : smem_bytes(pass ? kt_q : kt_d);
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(w ? 256 : 512), smem, st, a, nbh);
+    const int thr = (pass && (q8 || q8p)) ? 512 : w ? 256 : 512;
+    hipLaunchKernelGGL(k, dim3((unsigned)(pass ? nblk_q : nblk)), dim3(thr), smem, st, a, pass ? nbh_q : nbh);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

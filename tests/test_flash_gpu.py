@@ -510,19 +510,24 @@ def test_bf16_bwd_d128_c4_heads(torch_dev):
                     f"(8,16,2048,128) causal={causal}")
 
 
-def test_bf16_bwd_d128_paired_odd(torch_dev):
-    """The causal d = 128 backward with light / heavy block pairs on an odd block count,
-    (4,16,1100,128): 9 blocks of 128 per head (the middle block alone, a ragged last block),
-    a grid large enough to pair; heads against the oracle."""
+@pytest.mark.parametrize("shape,causal", [((4, 16, 1100, 128), True), ((8, 16, 1100, 128), True),
+                                          ((8, 16, 1100, 128), False)])
+def test_bf16_bwd_d128_paired_odd(torch_dev, shape, causal):
+    """The d = 128 backward on odd block counts with a ragged last block, N = 1100: 9 blocks of
+    128 per head (the dK/dV pass's light / heavy pairs, the middle block alone) and 5 of 256
+    (the dQ pass's 8-wave workgroups: at (8,16,..) causal in light / heavy pairs, non-causal
+    one per block; at (4,16,..) the grid is too small for them and the dQ pass keeps 4-wave
+    workgroups); heads against the oracle."""
     from minitorch import _hip
     torch = torch_dev
-    g = torch.Generator(device="cuda").manual_seed(1100)
-    q, k, v, do = (torch.randn((4, 16, 1100, 128), device="cuda", generator=g).to(torch.bfloat16)
+    g = torch.Generator(device="cuda").manual_seed(1100 + shape[0] + causal)
+    q, k, v, do = (torch.randn(shape, device="cuda", generator=g).to(torch.bfloat16)
                    for _ in range(4))
-    o, m, l = _hip.flash_fwd(q, k, v, True)
-    grads = _hip.flash_bwd(q, k, v, o, do, m, l, True)
+    o, m, l = _hip.flash_fwd(q, k, v, causal)
+    grads = _hip.flash_bwd(q, k, v, o, do, m, l, causal)
     torch.cuda.synchronize()
-    _grad_check(q, k, v, do, grads, True, [(0, 0), (2, 7), (3, 15)], "(4,16,1100,128) causal")
+    heads = [(0, 0), (2, 7), (3, 15)] + ([(7, 9)] if shape[0] == 8 else [])
+    _grad_check(q, k, v, do, grads, causal, heads, f"{shape} causal={causal}")
 
 
 @pytest.mark.parametrize("causal", [False, True])
