@@ -1085,6 +1085,10 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
   if (kq != kq_product) q8 = q8p = false;  // a diagnostics form replaced the dQ kernel
   // the 8-wave dQ pass with the operand ring 2 (knob 48) / 5 (knob 49) slots ahead, and causal
   // ones (47: 3 ahead, 9 registers spilled; 48: 2 ahead)
+  if (a.knob == 53 && causal) {  // the paired causal 8-wave dQ pass with the ring 3 ahead
+    kq = fa_bwd_d128w_bf16<1, true, true, true, 0, 3, 8>;
+    q8p = true;
+  }
   if (a.knob == 47 || a.knob == 48 || (a.knob == 49 && !causal)) {
     kq = a.knob == 49 ? fa_bwd_d128w_bf16<1, false, false, true, 0, 5, 8>
          : a.knob == 48 ? (causal ? fa_bwd_d128w_bf16<1, true, false, true, 0, 2, 8> : fa_bwd_d128w_bf16<1, false, false, true, 0, 2, 8>)
