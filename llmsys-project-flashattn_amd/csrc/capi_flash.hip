@@ -30,6 +30,7 @@ hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStrea
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
                               hipStream_t st, int pair, bool ring);
 int64_t bwd_fused_ws_bytes(int64_t B, int64_t H, int64_t N);
+int64_t bwd_fused_abi2_bytes(int64_t B, int64_t H, int64_t N);
 #ifdef MT_DIAGNOSTICS
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
 hipError_t launch_fwd_v4_ablation(const AttnArgs& a, int abl, hipStream_t st);
@@ -252,9 +253,9 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     case kPolV6RowSum: e = launch_fwd_v6(a, causal, 2, st, handled); break;
     case kPolV6RowSumNoKeep: e = launch_fwd_v6(a, causal, 6, st, handled); break;
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
-    case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
+    case kPolV6Split: e = launch_fwd_v6(a, causal, 18 | (a.knob == 8 ? 65536 : 0), st, handled); break;
     case kPolV6Wide:  // diagnostics knobs: 1 the older half's DMA, 2 / 3 priority flips
-      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : a.knob == 4 ? 16384 : a.knob == 7 ? 32768 : 0), st, handled);
+      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : a.knob == 4 ? 16384 : a.knob == 7 ? 32768 : a.knob == 8 ? 65536 : 0), st, handled);
       break;
     case kPolV6Stamp: {
       AttnArgs as = a;
@@ -265,7 +266,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     }
     case kPolV6SplitWide: e = launch_fwd_v6(a, causal, 82, st, handled); break;
     case kPolV6CausalWide:  // diagnostics knob 5: without the Vᵀ reuse (no spills)
-      if (causal) e = launch_fwd_v6(a, true, (a.o_f32 ? 610 : 98) | (a.knob == 5 ? 4 : a.knob == 4 ? 16384 : a.knob == 6 ? 16388 : 0), st, handled);
+      if (causal) e = launch_fwd_v6(a, true, (a.o_f32 ? 610 : 98) | (a.knob == 5 ? 4 : a.knob == 4 ? 16384 : a.knob == 6 ? 16388 : a.knob == 8 ? 65536 : a.knob == 9 ? 16384 + 65536 : 0), st, handled);
       break;
     case kPolV6CausalDual:
       if (causal) e = launch_fwd_v6(a, true, 354, st, handled);
@@ -469,8 +470,12 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       // with each wave's diagonal inside the pipeline, v6 with the widened epilogue stores
       // (policy 142: +1.8 % over 106, r3_ab_v6_wide.txt), else v5 (67). An fp32 O
       // (MT_BF16_F32OUT) takes the fp16-PV form (610): P rounded to 11 bits instead of 8,
-      // within north_star's flat 1e-3 on the causal heads.
-      e = launch_fwd_v6(a, true, a.o_f32 ? 610 : 98, st, handled);
+      // within north_star's flat 1e-3 on the causal heads. The bf16 output
+      // takes 4-wave workgroups (W4, 256 queries, two per CU) where that grid keeps two
+      // workgroups per CU: the two waves of a SIMD then share no barrier (0.2544 vs
+      // 0.2598 ms at C3 causal, profiles/r4_ab_fwd_w4.txt).
+      const bool w4 = !a.o_f32 && (int64_t)((N + 255) / 256 + 1) / 2 * bh >= 512;
+      e = launch_fwd_v6(a, true, a.o_f32 ? 610 : w4 ? (98 | 16384) : 98, st, handled);
       if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
     }
     // ragged N, short N, small causal grids: v4 (causal: paired, light block first, 8 waves
@@ -587,19 +592,37 @@ int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64
   return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(B, H, N, d) ? bwd_fused_ws_bytes(B, H, N) : 0);
 }
 
+static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void* k, const void* v,
+                               const void* o, const void* dout, const float* m, const float* l,
+                               void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
+                               int64_t d, const int64_t* strides, const int* kv_len,
+                               void* workspace, void* stream, bool checked);
+
 int mt_flash_attn_bwd(int dtype, int causal, const void* q, const void* k, const void* v,
                       const void* o, const void* dout, const float* m, const float* l,
                       void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
                       int64_t d, const int64_t* strides, void* workspace, void* stream) {
-  return mt_flash_attn_bwd_varlen(dtype, causal, q, k, v, o, dout, m, l, dq, dk, dv, B, H, N, d,
-                                  strides, nullptr, workspace, stream);
+  return flash_attn_bwd_impl(dtype, causal, q, k, v, o, dout, m, l, dq, dk, dv, B, H, N, d,
+                             strides, nullptr, workspace, stream, false);
 }
 
+// The unchecked entry points (no workspace size) may have a workspace sized by the ABI-2
+// rules, so they take the fused pass only where its current layout fits inside what ABI 2
+// reserved (d = 64, N <= 8192); elsewhere the split backward runs (no slab).
 int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k, const void* v,
                              const void* o, const void* dout, const float* m, const float* l,
                              void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
                              int64_t d, const int64_t* strides, const int* kv_len,
                              void* workspace, void* stream) {
+  return flash_attn_bwd_impl(dtype, causal, q, k, v, o, dout, m, l, dq, dk, dv, B, H, N, d,
+                             strides, kv_len, workspace, stream, false);
+}
+
+static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void* k, const void* v,
+                               const void* o, const void* dout, const float* m, const float* l,
+                               void* dq, void* dk, void* dv, int64_t B, int64_t H, int64_t N,
+                               int64_t d, const int64_t* strides, const int* kv_len,
+                               void* workspace, void* stream, bool checked) {
   if (check_sizes(dtype, B, H, N, d)) return 1;
   if (!q || !k || !v || !o || !dout || !m || !l || !dq || !dk || !dv || !workspace)
     return set_error("mt_flash_attn_bwd: null pointer argument");
@@ -614,7 +637,9 @@ int mt_flash_attn_bwd_varlen(int dtype, int causal, const void* q, const void* k
 #endif
   a.lse2 = (float*)workspace;
   a.delta = a.lse2 + B * H * N;
-  a.slab = fused_bwd_applies(B, H, N, d) ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
+  const bool slab_ok = fused_bwd_applies(B, H, N, d) &&
+                       (checked || (N <= 8192 && bwd_fused_ws_bytes(B, H, N) <= bwd_fused_abi2_bytes(B, H, N)));
+  a.slab = slab_ok ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
   int64_t* dst[8] = {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv};
   for (int i = 0; i < 8; ++i) fill_strides(dst[i], strides ? strides + 3 * i : nullptr, H, N, d);
   a.B = (int)B; a.H = (int)H; a.N = (int)N; a.d = (int)d;
@@ -681,8 +706,8 @@ int mt_flash_attn_bwd_v3(int dtype, int causal, const void* q, const void* k, co
   if (workspace_bytes < need)
     return set_error("mt_flash_attn_bwd_v3: workspace of %lld bytes, %lld needed "
                      "(mt_flash_attn_bwd_workspace_bytes)", (long long)workspace_bytes, (long long)need);
-  return mt_flash_attn_bwd_varlen(dtype, causal, q, k, v, o, dout, m, l, dq, dk, dv, B, H, N, d,
-                                  strides, kv_len, workspace, stream);
+  return flash_attn_bwd_impl(dtype, causal, q, k, v, o, dout, m, l, dq, dk, dv, B, H, N, d,
+                             strides, kv_len, workspace, stream, true);
 }
 
 // ---- reference-compatible host-pointer wrappers ---------------------------------

@@ -298,26 +298,36 @@ __global__ __launch_bounds__(256) void reduce_cols_fold(int fn, float* __restric
   out[t] = hv ? apply_fn(fn, start, v) : start;
 }
 
-// The partial buffer of the column reductions (per device, grown on demand, kept: the
-// reductions of one step reuse it in stream order).
-static void* reduce_scratch(size_t bytes) {
+// The partial buffer of the column reductions, one per (device, stream): grown on demand
+// and kept, so the reductions of one stream reuse it in that stream's order, and reductions
+// enqueued on two streams (or from two host threads on two streams) never share partials.
+static void* reduce_scratch(size_t bytes, hipStream_t st) {
+  struct Slot { int dev; hipStream_t st; void* buf; size_t cap; };
   static std::mutex mu;
-  static void* buf[64] = {};
-  static size_t cap[64] = {};
+  static Slot slots[64] = {};
+  static int nslots = 0;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
   std::lock_guard<std::mutex> lock(mu);
-  if (cap[dev] < bytes) {
-    if (buf[dev]) {
-      if (hipDeviceSynchronize() != hipSuccess) return nullptr;  // in-flight users of the old buffer
-      (void)hipFree(buf[dev]);
-    }
-    buf[dev] = nullptr;
-    cap[dev] = 0;
-    if (hipMalloc(&buf[dev], bytes) != hipSuccess) { buf[dev] = nullptr; return nullptr; }
-    cap[dev] = bytes;
+  Slot* s = nullptr;
+  for (int i = 0; i < nslots && !s; ++i)
+    if (slots[i].dev == dev && slots[i].st == st) s = &slots[i];
+  if (!s) {
+    if (nslots == 64) return nullptr;  // the caller then reduces without row chunks
+    s = &slots[nslots++];
+    *s = Slot{dev, st, nullptr, 0};
   }
-  return buf[dev];
+  if (s->cap < bytes) {
+    if (s->buf) {
+      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;  // in-flight users of the old buffer
+      (void)hipFree(s->buf);
+    }
+    s->buf = nullptr;
+    s->cap = 0;
+    if (hipMalloc(&s->buf, bytes) != hipSuccess) { s->buf = nullptr; return nullptr; }
+    s->cap = bytes;
+  }
+  return s->buf;
 }
 
 // Batched GEMM C[b] = A[b] @ B[b], fp32, exact fp32 MFMA. A: [M,K], B: [K,N], C: [M,N],
@@ -387,9 +397,10 @@ static bool same_shape(const Layout& a, const Layout& b) {
     if (a.shape[d] != b.shape[d]) return false;
   return true;
 }
-// every ordinal below n and every element offset of the layouts below 2^31 (int32 indexing)
+// every ordinal the grid-stride loops form (below n plus one grid stride, at most
+// grid_for's 4096 x 256) and every element offset of the layouts below 2^31 (int32 indexing)
 static bool fits_i32(int64_t n, std::initializer_list<const Layout*> ls) {
-  if (n >= ((int64_t)1 << 31)) return false;
+  if (n + ((int64_t)4096 * 256) >= ((int64_t)1 << 31)) return false;
   for (const Layout* l : ls) {
     int64_t e = 0;
     for (int d = 0; d < l->dims; ++d)
@@ -745,7 +756,7 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
     if (R < 1) R = 1;
     float* part = nullptr;
     if (R > 1) {
-      part = (float*)reduce_scratch((size_t)(outer * R * inner) * 8);
+      part = (float*)reduce_scratch((size_t)(outer * R * inner) * 8, (hipStream_t)stream);
       if (!part) R = 1;
     }
     const int64_t chunk = (len + R - 1) / R;

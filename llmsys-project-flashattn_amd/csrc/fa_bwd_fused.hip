@@ -646,6 +646,10 @@ static int64_t fused_counter_bytes(int64_t B, int64_t H, int64_t N) {
 static int64_t fused_group_heads(int64_t B, int64_t H, int64_t N) {
   return std::min<int64_t>(B * H, kSlabCap / fused_head_slab(N));
 }
+// what ABI 2 (rounds 3) reserved beyond the prep rows for d = 64, N <= 8192: the whole
+// unsplit slab, no counters (the legacy unchecked entry points use the fused pass only where
+// the current layout fits inside that)
+int64_t bwd_fused_abi2_bytes(int64_t B, int64_t H, int64_t N) { return B * H * fused_head_slab(N); }
 int64_t bwd_fused_ws_bytes(int64_t B, int64_t H, int64_t N) {
   // (one buffer resource with 32-bit offsets spans the counters and the slab)
   if (fused_head_slab(N) > kSlabCap || fused_counter_bytes(B, H, N) + kSlabCap > 0x7fffffff) return 0;

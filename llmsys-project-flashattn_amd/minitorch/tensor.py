@@ -7,6 +7,7 @@ dispatches through ``self.f`` (the ``TensorBackend``).
 """
 from __future__ import annotations
 
+import struct
 from dataclasses import dataclass
 from typing import Any, Iterable, List, Optional, Sequence, Tuple, Type, Union
 
@@ -79,7 +80,9 @@ class Tensor:
                 # one device-resident constant per value, filled once and then shared (no
                 # host-to-device copy and no fill launch per scalar operand; no kernel writes
                 # into an operand, and gradients are always fresh tensors or copies)
-                key = (float(b), id(self.backend))
+                # keyed on the fp32 bit pattern: -0.0 and 0.0 stay distinct, and a NaN
+                # operand finds its cached constant like any other value
+                key = (struct.pack("<f", float(b)), id(self.backend))
                 c = _DEV_SCALARS.get(key)
                 if c is None:
                     import torch
