@@ -157,3 +157,26 @@ def test_bench_default_chunking_world4_bitwise():
     assert chunked[0][0]["end_to_end"]["chunks"] == chosen
     for r in range(4):
         np.testing.assert_array_equal(chunked[r][1], serial[r][1])
+
+
+def test_bench_world8_chunked_and_unchunked_bitwise():
+    """gloo world 8, the rank count of the driver's scaling run: bench.run on a scaled-down
+    config 4 (d = 128 -> 32, N 16384 -> 64) with the 4 chunks occupancy_chunks picks for it on
+    a model chip of 2 CUs (the C4 case: every rank's rows in 4 block-cyclic pieces), and
+    unchunked (the C3 case at 8 ranks); both all-gather an O bit-identical to world 1's, and
+    rank 0's line carries the end-to-end leg."""
+    from minitorch.shard import occupancy_chunks
+    shape = (16, 4, 64, 32)
+    chosen = occupancy_chunks(*shape, 8, cus=2)
+    assert chosen == 4
+    base = ["--steps", "1", "--warmup", "1", "--shape", *map(str, shape)]
+    one = _run_world(1, ["--gpus", "1"] + base)
+    ref = one[0][1].reshape((-1,) + shape[2:])
+    for chunks in (chosen, 1):
+        out = _run_world(8, ["--gpus", "8"] + base + ["--chunks", str(chunks)])
+        res = out[0][0]
+        assert res["n_gpus"] == 8 and res["end_to_end"]["tflops"] > 0
+        if chunks > 1:
+            assert res["end_to_end"]["chunks"] == chunks
+        for r in range(8):
+            np.testing.assert_array_equal(out[r][1].reshape(ref.shape), ref)
