@@ -405,6 +405,13 @@ def extra_legs(torch, _hip, time_fn):
     l = torch.empty_like(m)
     extra["fwd_causal_tflops"] = round(fwd_flops(B, H, N, d, True) / (time_fn(
         lambda: _hip.flash_fwd(q, k, v, True, out=o, m=m, l=l), 20, 3) * 1e-3) / 1e12, 2)
+    # the fp32-output forms (MT_BF16_F32OUT: bf16 Q/K/V, O without its final bf16 rounding),
+    # the configuration that meets north_star's flat 1e-3 on every C3 head, causal included
+    o32 = torch.empty(q.shape, dtype=torch.float32, device="cuda")
+    for c_, key in ((False, "fwd_f32out_tflops"), (True, "fwd_causal_f32out_tflops")):
+        extra[key] = round(fwd_flops(B, H, N, d, c_) / (time_fn(
+            lambda: _hip.flash_fwd(q, k, v, c_, out=o32, m=m, l=l), 20, 3) * 1e-3) / 1e12, 2)
+    del o32
     # backward (bf16), FA-2 flop convention 2.5 x fwd
     _hip.flash_fwd(q, k, v, False, out=o, m=m, l=l)
     ws = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(B, H, N, d) // 4,
@@ -535,16 +542,47 @@ def c5_step_leg(torch, steps: int = 20) -> dict:
     gc.collect()
     gc.freeze()
     try:
-        t0 = time.perf_counter()
+        t0, h0 = time.perf_counter(), time.thread_time()
         for _ in range(steps):
             loss = step()
+        host_ms = (time.thread_time() - h0) / steps * 1e3
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / steps * 1e3
     finally:
         gc.unfreeze()
-    return {"c5_step_ms": round(ms, 2), "c5_tokens_per_s": round(B * T / ms * 1e3, 1),
-            "c5_loss": round(float(loss.item()), 4),
-            "c5_batch": "right-padded synthetic tokens, weighted loss, kv_len key padding"}
+    cores, _, quota = _cpu_cores()
+    out = {"c5_step_ms": round(ms, 2), "c5_tokens_per_s": round(B * T / ms * 1e3, 1),
+           "c5_loss": round(float(loss.item()), 4),
+           # the host thread's CPU time per step (minitorch's Python autodiff and the launches):
+           # when it is close to c5_step_ms the step is host-bound
+           "c5_host_ms": round(host_ms, 2), "c5_host_cpu_quota": quota, "c5_host_cores": cores,
+           "c5_batch": "right-padded synthetic tokens, weighted loss, kv_len key padding"}
+    try:  # the GPU's busy time per step: the kernels' own durations (torch.profiler)
+        out.update(_gpu_busy_ms(torch, step, 3, "c5"))
+    except Exception as e:  # noqa: BLE001
+        out["c5_gpu_ms_error"] = repr(e)[:160]
+    return out
+
+
+def _gpu_busy_ms(torch, fn, steps, tag):
+    """Sum of the device kernels' durations per call of fn (torch.profiler's device activity:
+    every HIP kernel of the process, the library's included), and their count per call."""
+    from torch.profiler import ProfilerActivity, profile
+    fn()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+    tot_us, n = 0.0, 0
+    for e in prof.key_averages():
+        us = getattr(e, "self_device_time_total", None)
+        if us is None:
+            us = getattr(e, "self_cuda_time_total", 0.0)
+        if us and us > 0:
+            tot_us += us
+            n += e.count
+    return {f"{tag}_gpu_ms": round(tot_us / steps / 1e3, 3), f"{tag}_gpu_kernels_per_step": round(n / steps, 1)}
 
 
 def parse_args(argv=None):

@@ -57,3 +57,29 @@ def grad_bounds(q, k, v, do, causal, atol=1e-3, r=R_BF16, kv=None, r_dq=None):
     return (atol + sc * ((r_dq * absdS + (1 + r_dq) * E) @ k),   # dQ
             atol + sc * ((r * absdS + (1 + r) * E).T @ q),         # dK
             atol + r * (P.T @ do))                                 # dV
+
+
+def grad_bounds_torch(q, k, v, do, causal, atol=1e-3, r=R_BF16, r_dq=None):
+    """grad_bounds for a batch of heads [n, N, d] as fp64 torch tensors on the device (the
+    same arithmetic; used where the NumPy form over every head of a full-size config would
+    take minutes of host time). Returns the dQ, dK, dV bounds [n, N, d] as fp64 tensors."""
+    import torch
+    q, k, v, do = (t.to(torch.float64) for t in (q, k, v, do))
+    n, N, d = q.shape
+    sc = 1.0 / np.sqrt(d)
+    S = torch.matmul(q, k.transpose(1, 2)) * sc
+    if causal:
+        S.masked_fill_(torch.ones(N, N, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+    S -= S.amax(dim=2, keepdim=True)
+    P = torch.exp(S)
+    P /= P.sum(dim=2, keepdim=True)
+    del S
+    O = torch.matmul(P, v)
+    delta = (do * O).sum(dim=2, keepdim=True)
+    ddelta = r * (do.abs() * torch.matmul(P, v.abs())).sum(dim=2, keepdim=True)
+    absdS = P * (torch.matmul(do, v.transpose(1, 2)) - delta).abs()
+    E = P * ddelta
+    r_dq = r * R_BF16_DQ / R_BF16 if r_dq is None else r_dq
+    return (atol + sc * torch.matmul(r_dq * absdS + (1 + r_dq) * E, k.abs()),
+            atol + sc * torch.matmul((r * absdS + (1 + r) * E).transpose(1, 2), q.abs()),
+            atol + r * torch.matmul(P.transpose(1, 2), do.abs()))

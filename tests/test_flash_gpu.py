@@ -421,12 +421,48 @@ def test_fp32_out_causal_fp16pv_fallback(torch_dev, case):
         assert float((err / bound).max()) <= 1.0, f"{case} (b,h)=({b},{h}) max-abs {float(err.max()):.3e}"
 
 
+def _grad_check_all(q, k, v, do, grads, causal, name_prefix, group=8):
+    """dQ, dK, dV of EVERY (b,h) head vs the C oracle (one OpenMP call over all heads) under
+    the elementwise bounds of tests/bounds.py, the bounds formed in fp64 on the device
+    (grad_bounds_torch, `group` heads at a time); returns {name: (max-abs, max error/bound)}
+    and the number of heads within 1e-3 max-abs on all three gradients."""
+    import torch
+    from bounds import grad_bounds_torch
+    B, H, N, d = q.shape
+    flat = [t.reshape(B * H, N, d) for t in (q, k, v, do)]
+    qs, ks, vs, dos = (_np(t) for t in flat)
+    o_ref, m_ref, l_ref = cref.attn_fwd(qs, ks, vs, causal)
+    g_ref = cref.attn_bwd(qs, ks, vs, dos, m_ref, l_ref, causal)
+    del o_ref
+    out, worst, flat_ok = {}, (0.0, ""), 0
+    for h0 in range(0, B * H, group):
+        sl = slice(h0, min(B * H, h0 + group))
+        bnds = grad_bounds_torch(*(t[sl].float() for t in flat), causal)
+        head_ok = torch.ones(sl.stop - sl.start, dtype=torch.bool, device=q.device)
+        for got, ref, bnd, name in zip(grads, g_ref, bnds, ("dq", "dk", "dv")):
+            err = (got.reshape(B * H, N, d)[sl].double() - torch.from_numpy(ref[sl]).to(q.device).double()).abs()
+            ratio = (err / bnd).amax(dim=(1, 2))
+            emax = err.amax(dim=(1, 2))
+            head_ok &= emax <= 1e-3
+            i = int(ratio.argmax())
+            if float(ratio[i]) > worst[0]:
+                bh = h0 + i
+                worst = (float(ratio[i]), f"{name_prefix} {name} (b,h)=({bh // H},{bh % H}) max-abs "
+                                          f"{float(emax[i]):.3e}, worst error/bound {float(ratio[i]):.3f}")
+            e0, r0 = out.get(name, (0.0, 0.0))
+            out[name] = (max(e0, float(emax.max())), max(r0, float(ratio.max())))
+        flat_ok += int(head_ok.sum())
+        del bnds
+    assert worst[0] <= 1.0, worst[1]
+    return out, flat_ok
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_config3_bf16_grads(torch_dev, causal, parity_record):
-    """BASELINE config 3 backward: dQ, dK, dV of the default bf16 backward on the 16 heads
-    of C3_HEADS (every XCD residue of the forward's block order and every key-block
-    position of the backward's grid across batch rows) under the elementwise bounds of
-    tests/bounds.py; the measured max-abs errors go to the parity record."""
+    """BASELINE config 3 backward: dQ, dK, dV of the default bf16 backward on ALL 128 heads
+    (round 5; round 4 checked the 16 of C3_HEADS) under the elementwise bounds of
+    tests/bounds.py; the measured max-abs errors and the heads within a flat 1e-3 go to the
+    parity record."""
     from minitorch import _hip
     torch = torch_dev
     g = torch.Generator(device="cuda").manual_seed(3)
@@ -438,10 +474,11 @@ def test_config3_bf16_grads(torch_dev, causal, parity_record):
     for t in (dq, dk, dv):
         assert torch.isfinite(t.float()).all()
     case = f"C3 (8,16,4096,64) bf16 {'causal' if causal else 'non-causal'}"
-    gres = _grad_check(q, k, v, do, (dq, dk, dv), causal, C3_HEADS, case)
+    gres, nflat = _grad_check_all(q, k, v, do, (dq, dk, dv), causal, case)
     for name, (e, r) in gres.items():
-        parity_record("test_config3_bf16_grads", f"{case} {name}", heads=len(C3_HEADS), max_abs=e,
-                      max_err_over_bound=r, bound="tests/bounds.py elementwise, r = 2^-7 (dQ 1.5 * 2^-7)")
+        parity_record("test_config3_bf16_grads", f"{case} {name}", heads=128, max_abs=e,
+                      max_err_over_bound=r, heads_all_grads_within_1em3=nflat,
+                      bound="tests/bounds.py elementwise, r = 2^-7 (dQ 1.5 * 2^-7)")
 
 
 @pytest.mark.parametrize("N,causal", [(8192, False), (8192, True), (8256, True), (16384, False),
