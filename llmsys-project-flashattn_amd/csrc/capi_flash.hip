@@ -253,9 +253,9 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     case kPolV6RowSum: e = launch_fwd_v6(a, causal, 2, st, handled); break;
     case kPolV6RowSumNoKeep: e = launch_fwd_v6(a, causal, 6, st, handled); break;
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
-    case kPolV6Split: e = launch_fwd_v6(a, causal, 18 | (a.knob == 8 ? 65536 : 0), st, handled); break;
+    case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
     case kPolV6Wide:  // diagnostics knobs: 1 the older half's DMA, 2 / 3 priority flips
-      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : a.knob == 4 ? 16384 : a.knob == 7 ? 32768 : a.knob == 8 ? 65536 : 0), st, handled);
+      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : a.knob == 4 ? 16384 : a.knob == 7 ? 32768 : 0), st, handled);
       break;
     case kPolV6Stamp: {
       AttnArgs as = a;
@@ -266,7 +266,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     }
     case kPolV6SplitWide: e = launch_fwd_v6(a, causal, 82, st, handled); break;
     case kPolV6CausalWide:  // diagnostics knob 5: without the Vᵀ reuse (no spills)
-      if (causal) e = launch_fwd_v6(a, true, (a.o_f32 ? 610 : 98) | (a.knob == 5 ? 4 : a.knob == 4 ? 16384 : a.knob == 6 ? 16388 : a.knob == 8 ? 65536 : a.knob == 9 ? 16384 + 65536 : 0), st, handled);
+      if (causal) e = launch_fwd_v6(a, true, (a.o_f32 ? 610 : 98) | (a.knob == 5 ? 4 : a.knob == 4 ? 16384 : a.knob == 6 ? 16388 : 0), st, handled);
       break;
     case kPolV6CausalDual:
       if (causal) e = launch_fwd_v6(a, true, 354, st, handled);

@@ -25,6 +25,13 @@
 //    transposed reads of rows 4g .. 4g + 3 by the 32 lanes of a half-wave).
 #include "fa_fwd_bf16.h"
 
+// Timing-only ablations of the bulk loop (WRONG results by construction), built into separate
+// A/B libraries with -DV6ABL=n (scripts/build_abl_fwd.sh), never into the product: 2 no row-sum
+// MFMAs, 4 no exponentials, 8 half the Vᵀ fragment reads (profiles/r5_abl_fwd.txt).
+#ifndef V6ABL
+#define V6ABL 0
+#endif
+
 namespace mt {
 
 namespace {
@@ -37,7 +44,6 @@ constexpr int kKSlots = 4, kVSlots = 2;
 constexpr int kNW = 8;                    // waves per workgroup
 constexpr int kBQ = 64 * kNW;             // queries per workgroup
 constexpr float kLimit = 1.8446744e19f;   // 2^64
-constexpr float kLow = 5.421011e-20f;      // 2^-64 (FQ: the smallest row-sum share kept)
 constexpr float kThr = 8.0f;
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -57,13 +63,6 @@ struct Pf6 {
 
 __device__ __forceinline__ f32x4 mma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-// The QKᵀ product: bf16, or with FQ fp16 operands (K tiles converted to fp16 in LDS, Q
-// pre-scaled by c2 and rounded to fp16 once) held in the same registers.
-template <bool FQ>
-__device__ __forceinline__ f32x4 mma_qk(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-  if (!FQ) return mma16(a, b, c);
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 // The PV product: bf16, or with H fp16 operands (the Vᵀ fragments read from an image the
 // kernel converted to fp16, the P operand packed as fp16) held in the same registers.
@@ -87,36 +86,6 @@ __device__ __forceinline__ void vcvt_write(bf16* tile, int tid, const u32x4& x) 
   }
   *(u32x4*)((char*)tile + tid * 16) = y;
 }
-// FQ: eight bf16 Q values times c2, rounded to fp16 once (in the bf16x8 registers); ovf is
-// set when one of them leaves the fp16 range (or is not finite)
-__device__ __forceinline__ bf16x8 q_f16(const bf16x8& x, float c2, bool& ovf) {
-  const u32x4 w = __builtin_bit_cast(u32x4, x);
-  u32x4 y;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x2 f = {__uint_as_float(w[j] << 16) * c2, __uint_as_float(w[j] & 0xffff0000u) * c2};
-    ovf |= !(fmaxf(fabsf(f[0]), fabsf(f[1])) < 65504.f);
-    y[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(f, f16x2));
-  }
-  return __builtin_bit_cast(bf16x8, y);
-}
-// FQ: 16 B of a staged K tile from bf16 to fp16 in place; kov keeps the running per-half max
-// of the bf16 magnitudes (a half at or above 0x4780 = 65536 overflows fp16, or is inf / NaN)
-__device__ __forceinline__ u32x4 kcvt(const u32x4& x, unsigned& kov) {
-  u32x4 y;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x2 f = {__uint_as_float(x[j] << 16), __uint_as_float(x[j] & 0xffff0000u)};
-    y[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(f, f16x2));
-    typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
-    kov = __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2, kov),
-                                                                 __builtin_bit_cast(u16x2, x[j] & 0x7fff7fffu)));
-  }
-  return y;
-}
-__device__ __forceinline__ bool kov_bad(unsigned kov) {
-  return (kov & 0xffffu) >= 0x4780u || (kov >> 16) >= 0x4780u;
-}
 
 // K fragment f of a tile: 16-key block f >> 1, k-step f & 1 (d 32ks + 8g ..)
 __device__ __forceinline__ bf16x8 kread6(const bf16* sk, const int (&ko)[2], int f) {
@@ -137,10 +106,12 @@ __device__ __forceinline__ bf16x8 vread6(const bf16* sv, const int (&vo)[4], int
 // (i >> 1) & 1, rows 2(i & 1), 2(i & 1) + 1. Exponentials in one MFMA slot, the row-sum add
 // and bf16 pack in the next (no transcendental-to-use stall). PS: the scores already are
 // c2 s - reference (Q pre-scaled, the shift in the MFMA's C operand): no scale-and-shift.
-template <bool PS, bool PK = false>
+template <bool PS, bool PK = false, bool ABL = false>
 __device__ __forceinline__ f32x2 sm6_exp(const Blk6& s, int kk, int i, float c2, const float (&nmc)[2]) {
   const int kbl = i >> 2, qh = (i >> 1) & 1, r0 = 2 * (i & 1);
   const f32x4& v = s.s[2 * kk + kbl][qh];
+  if ((V6ABL & 4) && ABL && !PS)
+    return f32x2{__builtin_fmaf(v[r0], c2, nmc[qh]), __builtin_fmaf(v[r0 + 1], c2, nmc[qh])};
   if (PS) return f32x2{__builtin_amdgcn_exp2f(v[r0]), __builtin_amdgcn_exp2f(v[r0 + 1])};
   if (PK) {  // diagnostics (VAR 32768): the pair's scale-and-shift as one v_pk_fma_f32
     const f32x2 x = __builtin_elementwise_fma(f32x2{v[r0], v[r0 + 1]}, f32x2{c2, c2}, f32x2{nmc[qh], nmc[qh]});
@@ -179,7 +150,7 @@ __device__ __forceinline__ void sm6_slot(int m, const Blk6& s_in, int kk, float 
                                          f32x2 (&acc)[2], Pf6& pf, f32x2& ep, f32x2& ec) {
   if (!EV) {
     if (m & 1) sm6_fin<RS, H>(ep, m >> 1, acc, pf);
-    else ep = sm6_exp<PS, PK>(s_in, kk, m >> 1, c2, nmc);
+    else ep = sm6_exp<PS, PK, true>(s_in, kk, m >> 1, c2, nmc);
     return;
   }
   const int i = m >> 1, j = m & 1, kbl = i >> 2, qh = (i >> 1) & 1, r = 2 * (i & 1) + j;
@@ -194,7 +165,7 @@ __device__ __forceinline__ void sm6_slot(int m, const Blk6& s_in, int kk, float 
 // QKᵀ phase: 16 MFMAs into S (16-key blocks in order, so keys 0-31 finish first), beside the
 // softmax of half kk of s_in. MFMA m: fragment f = m >> 1 (block f >> 1, k-step f & 1),
 // query half m & 1. The chains start from ci[qh] (zero, or the PS shift).
-template <bool SOFT, bool PS, bool RS = false, bool EV = false, bool H = false, bool PK = false, bool FQ = false>
+template <bool SOFT, bool PS, bool RS = false, bool EV = false, bool H = false, bool PK = false>
 __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf16x8 (&qf)[2][2], Blk6& S,
                                     const f32x4 (&ci)[2], const Blk6& s_in, int kk, float c2,
                                     const float (&nmc)[2], f32x2 (&acc)[2], Pf6& pf) {
@@ -206,7 +177,7 @@ __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf
   for (int m = 0; m < 16; ++m) {
     const int f = m >> 1, kb = f >> 1, ks = f & 1, qh = m & 1;
     if (!(m & 1) && f + 2 < 8) kf[f + 2] = kread6(sk, ko, f + 2);
-    S.s[kb][qh] = mma_qk<FQ>(kf[f], qf[qh][ks], ks ? S.s[kb][qh] : ci[qh]);
+    S.s[kb][qh] = mma16(kf[f], qf[qh][ks], ks ? S.s[kb][qh] : ci[qh]);
     if (SOFT) sm6_slot<PS, RS, EV, H, PK>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -235,9 +206,9 @@ __device__ __forceinline__ void pv6(const bf16* sv, const int (&vo)[4], f32x4 (&
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
     const int f = m >> 1, hv = f >> 2, db = f & 3, qh = m & 1;
-    if (KEEP != 2 && !(m & 1) && f + 2 < 8) vf[f + 2] = vread6(sv, vo, f + 2);
+    if (KEEP != 2 && !(m & 1) && f + 2 < 8) vf[f + 2] = ((V6ABL & 8) && SOFT && f + 2 >= 4) ? vf[f - 2] : vread6(sv, vo, f + 2);
     O[db][qh] = mma_pv<H>(vf[f], (hv ? phi : plo).p[qh], O[db][qh]);
-    if (RS && db == 0) R[qh] = mma_pv<H>(ones, (hv ? phi : plo).p[qh], R[qh]);
+    if (RS && db == 0 && !((V6ABL & 2) && SOFT)) R[qh] = mma_pv<H>(ones, (hv ? phi : plo).p[qh], R[qh]);
     if (SOFT) sm6_slot<PS, RS, EV, H, PK>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -308,15 +279,7 @@ __device__ __forceinline__ void dma6s(uint32_t lds, __amdgpu_buffer_rsrc_t rs, i
 // workgroup, for grids with fewer 8-wave workgroups than CUs.
 template <int VAR>
 __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nqb) {
-  // FQ (VAR 65536): the QKᵀ product on fp16 operands, Q pre-scaled by c2 = log2(e)/sqrt(d)
-  // and rounded to fp16 (11 significant bits: 8x finer than policy 101's bf16 pre-scale) and
-  // the K tiles converted to fp16 in LDS (exact for |k| < 65520), so a score leaves the MFMA
-  // already in log2 units minus the frozen reference (C-init) and the softmax is one
-  // v_exp_f32 and half a pack per score, without the v_fma_f32 scale-and-shift. K is staged
-  // three tiles ahead; K(t + 2) is converted in place during tile t. A value past the fp16
-  // range becomes inf and sends the block to the serial pass, which runs the bf16 product.
-  constexpr bool FQ = VAR & 65536;
-  constexpr bool PS = (VAR & 1) || FQ, RS = VAR & 2, EV = RS && (VAR & 8), SPLIT = VAR & 16, CAUSAL = VAR & 32;
+  constexpr bool PS = VAR & 1, RS = VAR & 2, EV = RS && (VAR & 8), SPLIT = VAR & 16, CAUSAL = VAR & 32;
   constexpr bool WIDE = VAR & 64;  // 16-B epilogue stores (T21)
   constexpr bool NOBAR = VAR & 128;  // diagnostics, timing only, racy: no tile barrier in the bulk loop
   // causal, two 4-wave halves: each half walks its own light / heavy pair of 256-query blocks
@@ -351,8 +314,6 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
   static_assert(!DUAL || CAUSAL, "dual halves: causal");
   static_assert(!H || (CAUSAL && !DUAL && !PS && RS && !EV), "fp16 PV: the causal default form");
-  static_assert(!FQ || (!(VAR & 1) && !H && !DUAL && !PK && !ODMA), "fp16 QK: the default forms");
-  constexpr int KA = FQ ? 3 : 2;  // K tiles staged ahead
   constexpr int VS = H ? 4 : kVSlots;  // V ring slots
   constexpr int K1 = (VAR & 4) ? 0 : 1, K2 = (VAR & 4) ? 0 : 2;
   constexpr int NWQ = (SPLIT || DUAL || W4) ? 4 : kNW;  // waves sharing one query block and its key tiles
@@ -444,13 +405,6 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     for (int i = 0; i < LPT; ++i) dma6(lds_of(sl, i), rv, vdo[i], step);
   };
   const float c2 = p.scale_log2;
-  // FQ: the threads that share a K ring convert a tile in place, 16 B each (NCK chunks)
-  constexpr int NCK = NWQ == 4 ? 2 : 1;
-  const int ct = (SPLIT || DUAL) ? (tid & 255) : tid;
-  auto cvt_k = [&](bf16* sl, unsigned& kov) __attribute__((always_inline)) {
-#pragma unroll
-    for (int c = 0; c < NCK; ++c) *(u32x4*)((char*)sl + (ct + 256 * c) * 16) = kcvt(vcvt_read(sl, ct + 256 * c), kov);
-  };
 
   // One query block [q0, q0 + BQ) of head bh. mode 0: the pipelined pass, then the serial
   // pass when a row sum left 2^64; 1 (DUAL): the pipelined pass only, returning whether the
@@ -458,8 +412,6 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   auto run_block = [&](const int q0, const int mode) __attribute__((always_inline)) -> bool {
   const int qw = q0 + wq * 64;  // first query of this wave (block A; block B = +32)
   bf16x8 qfA[2][2], qfB[2][2];  // [qh][ks]
-  unsigned kov = 0;  // FQ: the K conversions' magnitude max
-  bool qov = false;  // FQ: a pre-scaled Q value past the fp16 range
 #pragma unroll
   for (int qh = 0; qh < 2; ++qh) {
     const bf16* ra = Qg + (int64_t)min(qw + 16 * qh + i16, N - 1) * p.sq[2];
@@ -468,10 +420,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     for (int ks = 0; ks < 2; ++ks) {
       qfA[qh][ks] = *(const bf16x8*)(ra + 32 * ks + 8 * g);
       qfB[qh][ks] = *(const bf16x8*)(rb + 32 * ks + 8 * g);
-      if (FQ) {
-        qfA[qh][ks] = q_f16(qfA[qh][ks], c2, qov);
-        qfB[qh][ks] = q_f16(qfB[qh][ks], c2, qov);
-      } else if (PS) {
+      if (PS) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           qfA[qh][ks][j] = (bf16)((float)qfA[qh][ks][j] * c2);
@@ -481,7 +430,6 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     }
   }
   const float c2e = PS ? 1.f : c2;  // the factor from an MFMA score to log2 units
-  const float c2s = FQ ? c2 : c2e;  // the same in the serial pass (FQ: the bf16 product)
   const f32x4 ci0[2] = {f32x4{}, f32x4{}};
   // Tiles the workgroup stages: non-causal all Nk / 64; causal the keys below its last
   // query. Tiles this wave computes: non-causal all; causal [0, tD] with tD = qw / 64 its
@@ -523,14 +471,8 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   dma_v(sV, 0);
   dma_k(sK + TILE, ktile_b);
   if (H) dma_v(sV + TILE, vtile_b);
-  if (FQ) dma_k(sK + 2 * TILE, 2 * ktile_b);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (FQ) {  // K(0), K(1) to fp16 (K(2) is converted in iteration 0)
-    cvt_k(sK, kov);
-    cvt_k(sK + TILE, kov);
-    __syncthreads();
-  }
   if (H) {  // V(0) to fp16 (V(1) is converted in iteration 0)
 #pragma unroll
     for (int c = 0; c < NCV; ++c) vcvt_write(sV, tid + 256 * c, vcvt_read(sV, tid + 256 * c));
@@ -542,8 +484,8 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       f32x2 dacc[2];
       Pf6 dpf;
       const float z[2] = {0.f, 0.f};
-      qk6<false, false, false, false, false, false, FQ>(sK, ko, qfA, SA, ci0, SA, 0, c2, z, dacc, dpf);
-      qk6<false, false, false, false, false, false, FQ>(sK, ko, qfB, SB, ci0, SB, 0, c2, z, dacc, dpf);
+      qk6<false, false>(sK, ko, qfA, SA, ci0, SA, 0, c2, z, dacc, dpf);
+      qk6<false, false>(sK, ko, qfB, SB, ci0, SB, 0, c2, z, dacc, dpf);
     }
     if (CAUSAL && tD == 0) {  // tile 0 is this wave's diagonal: reference over visible keys
       mask_diag(SA, 0);
@@ -553,16 +495,13 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
     f32x4 ciA[2], ciB[2];
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
-      // FQ: no reference (m' = 0): the scores are already in log2 units, O and l are
-      // normalised by the same factor, and the block goes to the serial pass when a row
-      // sum leaves [2^-64, 2^64]
-      mA[qh] = FQ ? 0.f : quad_max(lane_max6(SA, qh));
-      mB[qh] = FQ ? 0.f : quad_max(lane_max6(SB, qh));
+      mA[qh] = quad_max(lane_max6(SA, qh));
+      mB[qh] = quad_max(lane_max6(SB, qh));
       nmcA[qh] = -(mA[qh] * c2);
       nmcB[qh] = -(mB[qh] * c2);
       ciA[qh] = f32x4{-mA[qh], -mA[qh], -mA[qh], -mA[qh]};
       ciB[qh] = f32x4{-mB[qh], -mB[qh], -mB[qh], -mB[qh]};
-      if (PS && !FQ) {  // tile 0's scores were computed from zero
+      if (PS) {  // tile 0's scores were computed from zero
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
           SA.s[kb][qh] += ciA[qh];
@@ -594,16 +533,13 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       __builtin_amdgcn_sched_barrier(0);
       if (PFLIP && wave >= 4) __builtin_amdgcn_s_setprio(1);
       stamp(-1);
-      dma_k(sK + ((s0 + KA) & 3) * TILE, (t + KA) * ktile_b);
+      dma_k(sK + ((s0 + 2) & 3) * TILE, (t + 2) * ktile_b);
       if (H) dma_v(sV + ((s0 + 2) & 3) * TILE, (t + 2) * vtile_b);
       else dma_v(sV + ((s0 + 1) & 1) * TILE, (t + 1) * vtile_b);
-      u32x4 vraw[NCV], kraw[NCK];
+      u32x4 vraw[NCV];
 #pragma unroll
       for (int c = 0; c < NCV; ++c)
         if (H) vraw[c] = vcvt_read(sV + ((s0 + 1) & 3) * TILE, tid + 256 * c);
-#pragma unroll
-      for (int c = 0; c < NCK; ++c)
-        if (FQ) kraw[c] = vcvt_read(sK + ((s0 + 2) & 3) * TILE, ct + 256 * c);
       int koA[2], koB[2], vv[4];
       const int kslA = s0 * TILE, kslB = ((s0 + 1) & 3) * TILE, vsl = (s0 & (VS - 1)) * TILE;
 #pragma unroll
@@ -614,19 +550,16 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
 #pragma unroll
       for (int db = 0; db < 4; ++db) vv[db] = vo[db] + vsl;
       stamp(0);
-      qk6<true, PS, RS, EV, H, PK, FQ>(sK, koA, qfA, SA, (PS && !FQ) ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
+      qk6<true, PS, RS, EV, H, PK>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);  // P1
 #pragma unroll
       for (int c = 0; c < NCV; ++c)
         if (H) vcvt_write(sV + ((s0 + 1) & 3) * TILE, tid + 256 * c, vraw[c]);
-#pragma unroll
-      for (int c = 0; c < NCK; ++c)
-        if (FQ) *(u32x4*)((char*)(sK + ((s0 + 2) & 3) * TILE) + (ct + 256 * c) * 16) = kcvt(kraw[c], kov);
       stamp(1);
       if (PFLIP == 2 && wave >= 4) __builtin_amdgcn_s_setprio(0);
       pv6<true, K1, PS, RS, EV, H, PK>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);  // P2
       stamp(2);
       if (PFLIP == 3 && wave >= 4) __builtin_amdgcn_s_setprio(0);
-      qk6<true, PS, RS, EV, H, PK, FQ>(sK, koB, qfB, SB, (PS && !FQ) ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
+      qk6<true, PS, RS, EV, H, PK>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
       stamp(3);
       pv6<true, K2, PS, RS, EV, H, PK>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
       stamp(4);
@@ -650,7 +583,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
 #pragma unroll
       for (int db = 0; db < 4; ++db) vv[db] = vo[db] + (t & (VS - 1)) * TILE;
       if (CAUSAL) mask_diag(SB, 32);  // S_B(tD): keys 32-63 are block B's diagonal
-      qk6<true, PS, RS, EV, H, PK, FQ>(sK, koA, qfA, SA, (PS && !FQ) ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
+      qk6<true, PS, RS, EV, H, PK>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
       if (CAUSAL) mask_diag(SA, 0);  // S_A(tD): keys 0-31 its diagonal, 32-63 above it
       pv6<true, K1, PS, RS, EV, H, PK>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);
 #pragma unroll
@@ -693,8 +626,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   if (CAUSAL) {
     // tail: this wave's share of the staging of the tiles the other waves still need
     for (int t = nbulk > 0 ? nbulk - 1 : 0; t + 1 < ntiles; ++t) {
-      dma_k(sK + ((t + KA) & 3) * TILE, (t + KA) * ktile_b);
-      if (FQ) cvt_k(sK + ((t + 2) & 3) * TILE, kov);  // its share of the conversion of K(t + 2)
+      dma_k(sK + ((t + 2) & 3) * TILE, (t + 2) * ktile_b);
       if (H) {  // and its share of the conversion of V(t + 1)
         dma_v(sV + ((t + 2) & 3) * TILE, (t + 2) * vtile_b);
 #pragma unroll
@@ -712,24 +644,13 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // ---- serial path: every tile again with the per-tile deferred-max bookkeeping, when a
   // lane's row-sum share left 2^64 (the workgroup starts over) -----------------------------
   const bool bad = mode != 2 &&
-                   (!(pA[0] <= kLimit) || !(pA[1] <= kLimit) || !(pB[0] <= kLimit) || !(pB[1] <= kLimit) ||
-                    (FQ && (qov || kov_bad(kov) || !(pA[0] >= kLow) || !(pA[1] >= kLow) ||
-                            !(pB[0] >= kLow) || !(pB[1] >= kLow))));
+                   (!(pA[0] <= kLimit) || !(pA[1] <= kLimit) || !(pB[0] <= kLimit) || !(pB[1] <= kLimit));
   if (mode == 0 ? __syncthreads_or(bad) : mode == 2) {
     zero_o();
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
       mA[qh] = mB[qh] = -INFINITY;
       pA[qh] = pB[qh] = 0.f;
-    }
-    if (FQ) {  // the serial pass runs the bf16 product on the raw Q (and the raw K tiles)
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          qfA[qh][ks] = *(const bf16x8*)(Qg + (int64_t)min(qw + 16 * qh + i16, N - 1) * p.sq[2] + 32 * ks + 8 * g);
-          qfB[qh][ks] = *(const bf16x8*)(Qg + (int64_t)min(qw + 32 + 16 * qh + i16, N - 1) * p.sq[2] + 32 * ks + 8 * g);
-        }
     }
     for (int t = 0; t < ntiles; ++t) {
       __syncthreads();  // every wave is done with the previous tile
@@ -762,32 +683,25 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh) {
           const float tmax = quad_max(lane_max6(S, qh));
-          if (__builtin_amdgcn_ballot_w64((tmax - m[qh]) * c2s > kThr)) {
+          if (__builtin_amdgcn_ballot_w64((tmax - m[qh]) * c2e > kThr)) {
             const float m_new = fmaxf(m[qh], tmax);
-            const float alpha = m[qh] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m[qh] - m_new) * c2s);
+            const float alpha = m[qh] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m[qh] - m_new) * c2e);
             m[qh] = m_new;
 #pragma unroll
             for (int db = 0; db < 4; ++db) O[db][qh] *= alpha;
             l[qh] *= alpha;
           }
-          nmc[qh] = -(m[qh] * c2s);
+          nmc[qh] = -(m[qh] * c2e);
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm6_fin(sm6_exp<false>(S, 0, i, c2s, nmc), i, acc, plo);
+        for (int i = 0; i < 8; ++i) sm6_fin(sm6_exp<false>(S, 0, i, c2e, nmc), i, acc, plo);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm6_fin(sm6_exp<false>(S, 1, i, c2s, nmc), i, acc, phi);
+        for (int i = 0; i < 8; ++i) sm6_fin(sm6_exp<false>(S, 1, i, c2e, nmc), i, acc, phi);
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh) l[qh] += acc[qh][0] + acc[qh][1];
         f32x2 d2[2];
         f32x4 dR[2];
         pv6<false, 0, false>(sV, vo, O, plo, phi, S, 0, c2, nmc, d2, dpf, vk, dR);
-      }
-    }
-    if (FQ) {  // m in log2 units, as the pipelined pass leaves it
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh) {
-        mA[qh] *= c2;
-        mB[qh] *= c2;
       }
     }
   }
@@ -911,8 +825,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   if (split && (a.N % (2 * kBK) != 0 || a.N < 4 * kBK)) return hipSuccess;
   if (dual && a.N % (4 * kBQ / 2) != 0) return hipSuccess;  // whole pairs of 256-query blocks per half
   const int64_t lim = (int64_t)1 << 31;
-  const int64_t ahead = (var & 65536) ? 3 : 2;  // K tiles staged ahead (FQ: 3)
-  if (((int64_t)a.N + ahead * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
+  if (((int64_t)a.N + 2 * kBK) * a.sk[2] * 2 >= lim || ((int64_t)a.N + 2 * kBK) * a.sv[2] * 2 >= lim)
     return hipSuccess;
   *handled = true;
   const size_t smem = (size_t)(split || dual ? 2 : 1) * (kKSlots + (var & 512 ? 4 : kVSlots)) * TILE * sizeof(bf16);
@@ -924,10 +837,6 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 610: kern = fa_fwd_bf16_v6<610>; break;  // 98 with fp16 PV (the fp32-output causal default)
     case 16482: kern = fa_fwd_bf16_v6<16482>; break;  // 98 with 4-wave workgroups (the causal default)
 #ifdef MT_DIAGNOSTICS
-    case 65602: kern = fa_fwd_bf16_v6<65602>; break;  // 66 with the fp16 QKᵀ product
-    case 65554: kern = fa_fwd_bf16_v6<65554>; break;  // 18 with the fp16 QKᵀ product
-    case 65634: kern = fa_fwd_bf16_v6<65634>; break;  // 98 with the fp16 QKᵀ product
-    case 82018: kern = fa_fwd_bf16_v6<82018>; break;  // 16482 with the fp16 QKᵀ product
     case 354: kern = fa_fwd_bf16_v6<354>; break;
     case 1090: kern = fa_fwd_bf16_v6<1090>; break;  // 66 with stamps
     case 2114: kern = fa_fwd_bf16_v6<2114>; break;  // 66 with the tile's DMA by waves 0-3
