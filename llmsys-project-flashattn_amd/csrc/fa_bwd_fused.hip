@@ -56,6 +56,15 @@
 
 #include <algorithm>
 
+// Timing-only ablations of the pass (WRONG results by construction), built into separate A/B
+// libraries with -DBWDABL=n (scripts/build_abl.sh fa_bwd_fused BWDABL n), never into the
+// product: 1 no dQ strips (their operand reads and MFMAs), 2 no exponentials, 4 the dQ strips'
+// second K fragment read taken from another k-step's first, 8 the dVᵀ / dKᵀ transposed
+// fragments of k-step 1 taken from k-step 0 (profiles/r5_abl_bwd.txt).
+#ifndef BWDABL
+#define BWDABL 0
+#endif
+
 
 namespace mt {
 
@@ -162,8 +171,8 @@ __device__ __forceinline__ void fdkv_tile(const char* sub, const FCtx& c, f32x16
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
-        tv[s][db] = trf(Oi, 16 * s, c.tlo[db], c.thi[db]);
-        tk[s][db] = trf(Qi, 16 * s, c.tlo[db], c.thi[db]);
+        tv[s][db] = ((BWDABL & 8) && s) ? tv[0][db] : trf(Oi, 16 * s, c.tlo[db], c.thi[db]);
+        tk[s][db] = ((BWDABL & 8) && s) ? tk[0][db] : trf(Qi, 16 * s, c.tlo[db], c.thi[db]);
       }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -186,7 +195,7 @@ __device__ __forceinline__ void fdkv_tile(const char* sub, const FCtx& c, f32x16
   } else {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float pv = __builtin_amdgcn_exp2f(S[r] * c2);
+      const float pv = (BWDABL & 2) ? S[r] * c2 : __builtin_amdgcn_exp2f(S[r] * c2);
       S[r] = pv;
       dP[r] = pv * dP[r];
     }
@@ -230,6 +239,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 template <int S0, int S1, bool PF = true>
 __device__ __forceinline__ void dq_ksteps(const bf16* kimg, const bf16* si, int oa0, int oa1, int ob,
                                           f32x4 (&acc)[2]) {
+  if (BWDABL & 1) return;
   if (!PF) {
 #pragma unroll
     for (int s = S0; s < S1; ++s) {
@@ -244,7 +254,11 @@ __device__ __forceinline__ void dq_ksteps(const bf16* kimg, const bf16* si, int 
   for (int s = S0; s < S1; ++s) {
     bq[s - S0] = dq_frag(si + 32 * s * kStep + ob);
     a0[s - S0] = dq_frag(kimg + 32 * s * D + oa0);
-    a1[s - S0] = dq_frag(kimg + 32 * s * D + oa1);
+    if (!(BWDABL & 4)) a1[s - S0] = dq_frag(kimg + 32 * s * D + oa1);
+  }
+  if (BWDABL & 4) {  // (a rotated copy, so that no two MFMA chains are identical)
+#pragma unroll
+    for (int s = 0; s < S1 - S0; ++s) a1[s] = a0[(s + 1) % (S1 - S0)];
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -279,9 +293,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
-  // operand prefetch (fdkv_tile, dq_ksteps) in the non-causal kernel's unmasked steps only:
-  // in the causal kernels the extra live fragments spill around the masked head loop
-  // (measured: causal 0.991 -> 1.020 ms with it, non-causal 1.643 -> 1.559 ms)
+  // operand prefetch in the unmasked steps: the dQ strips' (dq_ksteps) in every kernel, the
+  // sub-tiles' (fdkv_tile) in the non-causal kernel only: in the causal kernels those extra
+  // live fragments spill around the masked head loop (measured: causal 0.991 -> 1.020 ms with
+  // it, non-causal 1.643 -> 1.559 ms); the dQ prefetch alone took C3 causal 0.905 -> 0.875 ms
+  // (round 5, profiles/r5_ab_bwd_dq.txt)
   constexpr bool kPF = !CAUSAL;
   const int hf = lane >> 5, c32 = lane & 31;
   const int N = p.N;
@@ -457,9 +473,9 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     if (more_) stage(t_ + 1, (SLOT_) ^ 1);                                               \
     f32x4 qa_[2] = {f32x4{}, f32x4{}};                                                   \
     const bf16* si_ = dsimg + ((SLOT_) ^ 1) * (kKB * kStep);                             \
-    if (DQ_) dq_ksteps<0, 4, kPF && !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);             \
+    if (DQ_) dq_ksteps<0, 4, !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);                     \
     FSUB(MASK_, SLOT_, t_, 0)                                                            \
-    if (DQ_) dq_ksteps<4, 8, kPF && !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);             \
+    if (DQ_) dq_ksteps<4, 8, !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);                     \
     FSUB(MASK_, SLOT_, t_, 1)                                                            \
     if (DQ_) dq_store(qa_, sq(t_ - 1));                                                  \
     if (more_ || (DQ_)) publish(DQ_);  /* DQ_: the store of step t - 2 has completed */  \
@@ -492,8 +508,8 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
 #undef FSUB
   if (nstep > 0) {  // the last step's dQ strip
     f32x4 qa[2] = {f32x4{}, f32x4{}};
-    dq_ksteps<0, 4, kPF>(kimg, dsimg + ((nstep - 1) & 1) * (kKB * kStep), oa0, oa1, ob, qa);
-    dq_ksteps<4, 8, kPF>(kimg, dsimg + ((nstep - 1) & 1) * (kKB * kStep), oa0, oa1, ob, qa);
+    dq_ksteps<0, 4>(kimg, dsimg + ((nstep - 1) & 1) * (kKB * kStep), oa0, oa1, ob, qa);
+    dq_ksteps<4, 8>(kimg, dsimg + ((nstep - 1) & 1) * (kKB * kStep), oa0, oa1, ob, qa);
     dq_store(qa, sq(nstep - 1));
   }
   // the last two steps' arrivals: every wave's stores complete, the barrier, the adds

@@ -26,7 +26,7 @@
 #include "fa_fwd_bf16.h"
 
 // Timing-only ablations of the bulk loop (WRONG results by construction), built into separate
-// A/B libraries with -DV6ABL=n (scripts/build_abl_fwd.sh), never into the product: 2 no row-sum
+// A/B libraries with -DV6ABL=n (scripts/build_abl.sh fa_fwd_v6 V6ABL n), never into the product: 2 no row-sum
 // MFMAs, 4 no exponentials, 8 half the Vᵀ fragment reads (profiles/r5_abl_fwd.txt).
 #ifndef V6ABL
 #define V6ABL 0
