@@ -26,8 +26,10 @@
 #include "fa_fwd_bf16.h"
 
 // Timing-only ablations of the bulk loop (WRONG results by construction), built into separate
-// A/B libraries with -DV6ABL=n (scripts/build_abl.sh fa_fwd_v6 V6ABL n), never into the product: 2 no row-sum
-// MFMAs, 4 no exponentials, 8 half the Vᵀ fragment reads (profiles/r5_abl_fwd.txt).
+// A/B libraries with -DV6ABL=n (scripts/build_abl.sh fa_fwd_v6 V6ABL n), never into the product: 1 half
+// the K fragment reads (key blocks 2, 3 take blocks 0, 1's fragments with the k-steps swapped, so
+// no MFMA chain repeats another), 2 no row-sum MFMAs, 4 no exponentials, 8 half the Vᵀ fragment
+// reads (profiles/r5_abl_fwd.txt).
 #ifndef V6ABL
 #define V6ABL 0
 #endif
@@ -176,7 +178,7 @@ __device__ __forceinline__ void qk6(const bf16* sk, const int (&ko)[2], const bf
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
     const int f = m >> 1, kb = f >> 1, ks = f & 1, qh = m & 1;
-    if (!(m & 1) && f + 2 < 8) kf[f + 2] = kread6(sk, ko, f + 2);
+    if (!(m & 1) && f + 2 < 8) kf[f + 2] = ((V6ABL & 1) && SOFT && f + 2 >= 4) ? kf[(f - 2) ^ 1] : kread6(sk, ko, f + 2);
     S.s[kb][qh] = mma16(kf[f], qf[qh][ks], ks ? S.s[kb][qh] : ci[qh]);
     if (SOFT) sm6_slot<PS, RS, EV, H, PK>(m, s_in, kk, c2, nmc, acc, pf, ep, ec);
     __builtin_amdgcn_sched_barrier(0);
