@@ -449,34 +449,24 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
     if (!causal) {
       // v6 (v5's schedule on the 16x16x32 MFMA, row sums on the MFMA pipe, 16-B epilogue
       // stores: policy 140, 102 with the widened stores, profiles/r3_ab_v6_wide.txt) with at
-      // least one 8-wave workgroup per CU; with the keys split between the workgroup halves
-      // (policy 105; its widened form 141 spills: -2.6 %) at one 256-query workgroup per CU
-      // (the 8-GPU C3 shard)
+      // least one 8-wave workgroup per CU; on smaller grids the form with the keys split between
+      // the workgroup halves (policy 105; its widened form 141 spills: -2.6 %). Since round 5
+      // the split form also takes the grids below one split workgroup per CU, which v5's split
+      // had: within ±1 % of it on four of five small shapes and 3 % behind at (2,4,2048,64)
+      // (profiles/r5_ab_smallgrid.txt), so the product's d = 64 forward is v6 with v4 behind it.
       if ((int64_t)((N + 511) / 512) * bh >= 256)
         e = launch_fwd_v6(a, false, 66, st, handled);
-      else if ((int64_t)((N + 255) / 256) * bh >= 256)
-        e = launch_fwd_v6(a, false, 18, st, handled);
-      if (!*handled) {
-        // v5: the 8-wave default (policy 56); on smaller grids its split-keys form (76), or the
-        // 4-wave form where the split does not apply (profiles/r2_ab_split.txt,
-        // r2_ab_small_grids.txt); it declines N % 64 != 0
-        const int var = (int64_t)((N + 511) / 512) * bh >= 256 ? v5::kDefault
-                        : (N % 128 == 0 && N >= 256)          ? (v5::kDefault | v5::kSplit)
-                                                              : (v5::kDma | v5::kUnroll);
-        e = launch_fwd_v5(a, false, 2, var, st, handled);
-      }
+      if (!*handled) e = launch_fwd_v6(a, false, 18, st, handled);
     } else if ((int64_t)((N + 511) / 512 + 1) / 2 * bh >= 256) {
       // causal with at least one 8-wave workgroup per CU: paired light / heavy query blocks
       // with each wave's diagonal inside the pipeline, v6 with the widened epilogue stores
-      // (policy 142: +1.8 % over 106, r3_ab_v6_wide.txt), else v5 (67). An fp32 O
-      // (MT_BF16_F32OUT) takes the fp16-PV form (610): P rounded to 11 bits instead of 8,
-      // within north_star's flat 1e-3 on the causal heads. The bf16 output
-      // takes 4-wave workgroups (W4, 256 queries, two per CU) where that grid keeps two
-      // workgroups per CU: the two waves of a SIMD then share no barrier (0.2544 vs
-      // 0.2598 ms at C3 causal, profiles/r4_ab_fwd_w4.txt).
+      // (policy 142: +1.8 % over 106, r3_ab_v6_wide.txt). An fp32 O (MT_BF16_F32OUT) takes the
+      // fp16-PV form (610): P rounded to 11 bits instead of 8, within north_star's flat 1e-3 on
+      // the causal heads. The bf16 output takes 4-wave workgroups (W4, 256
+      // queries, two per CU) where that grid keeps two workgroups per CU: the two waves of a
+      // SIMD then share no barrier (0.2544 vs 0.2598 ms at C3 causal, profiles/r4_ab_fwd_w4.txt).
       const bool w4 = !a.o_f32 && (int64_t)((N + 255) / 256 + 1) / 2 * bh >= 512;
       e = launch_fwd_v6(a, true, a.o_f32 ? 610 : w4 ? (98 | 16384) : 98, st, handled);
-      if (!*handled) e = launch_fwd_v5(a, true, 2, v5::kDefault, st, handled);
     }
     // ragged N, short N, small causal grids: v4 (causal: paired, light block first, 8 waves
     // from N = 8192; profiles/r1_ab_causal_pair.txt)

@@ -335,7 +335,7 @@ def test_config3_bf16_full_size(torch_dev, causal, parity_record):
 @pytest.mark.parametrize("shape,causal,same_kernel", [
     ((2, 3, 200, 64), False, True),    # ragged N: v4
     ((2, 3, 200, 64), True, True),
-    ((1, 4, 1024, 64), False, True),   # small grid: v5 with the keys split
+    ((1, 4, 1024, 64), False, True),   # small grid: v6 with the keys split
     ((2, 4, 2048, 64), True, True),    # v6 causal
     ((1, 2, 256, 128), False, True),   # d = 128 non-causal: the 16x16x32 kernel writes either O
     ((1, 2, 256, 128), True, True),    # d = 128 causal: the same kernel (paired form)
