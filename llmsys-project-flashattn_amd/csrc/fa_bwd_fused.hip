@@ -60,7 +60,8 @@
 // libraries with -DBWDABL=n (scripts/build_abl.sh fa_bwd_fused BWDABL n), never into the
 // product: 1 no dQ strips (their operand reads and MFMAs), 2 no exponentials, 4 the dQ strips'
 // second K fragment read taken from another k-step's first, 8 the dVᵀ / dKᵀ transposed
-// fragments of k-step 1 taken from k-step 0 (profiles/r5_abl_bwd.txt).
+// fragments of k-step 1 taken from k-step 0, 16 no step barrier in the walk, 32 no Q / dO
+// staging in the walk (profiles/r5_abl_bwd.txt).
 #ifndef BWDABL
 #define BWDABL 0
 #endif
@@ -470,7 +471,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   {                                                                                      \
     const int t_ = (T_);                                                                 \
     const bool more_ = t_ + 1 < nstep;                                                   \
-    if (more_) stage(t_ + 1, (SLOT_) ^ 1);                                               \
+    if (more_ && !(BWDABL & 32)) stage(t_ + 1, (SLOT_) ^ 1);                             \
     f32x4 qa_[2] = {f32x4{}, f32x4{}};                                                   \
     const bf16* si_ = dsimg + ((SLOT_) ^ 1) * (kKB * kStep);                             \
     if (DQ_) dq_ksteps<0, 4, !(MASK_)>(kimg, si_, oa0, oa1, ob, qa_);                     \
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     FSUB(MASK_, SLOT_, t_, 1)                                                            \
     if (DQ_) dq_store(qa_, sq(t_ - 1));                                                  \
     if (more_ || (DQ_)) publish(DQ_);  /* DQ_: the store of step t - 2 has completed */  \
-    __syncthreads();                                                                     \
+    if (!(BWDABL & 16)) __syncthreads();                                                 \
     if (t_ >= 2) arrive(step0 + sq(t_ - 2));                                             \
   }
   if (nstep > 0) {
