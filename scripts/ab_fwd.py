@@ -1,5 +1,6 @@
 """Interleaved in-process A/B timing of forward-kernel policies (diagnostics, GPU box).
-usage: python scripts/ab_fwd.py POL[,POL...] [causal] [B,H,N,d] [rounds]   (DTYPE=fp32 for fp32 I/O)
+usage: python scripts/ab_fwd.py POL[,POL...] [causal] [B,H,N,d] [rounds]   (DTYPE=fp32 for fp32 I/O,
+OUT32=1 for the bf16 kernels' fp32 output)
 MT_DIAG=1: the diagnostics library; ENVAB=NAME:v1,v2,..: the arms are values of an environment
 knob (e.g. MT_KNOB, read per launch by the diagnostics build) under policy POL"""
 import os, sys, time
@@ -22,7 +23,9 @@ rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 7
 g = torch.Generator(device="cuda").manual_seed(0)
 dt = torch.float32 if os.environ.get("DTYPE") == "fp32" else torch.bfloat16
 q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(dt) for _ in range(3))
-o = torch.empty_like(q); m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
+# OUT32=1: the bf16 kernels' fp32 output (MT_BF16_F32OUT)
+o = torch.empty_like(q, dtype=torch.float32 if os.environ.get("OUT32") == "1" else q.dtype)
+m = torch.empty((B, H, N), device="cuda"); l = torch.empty_like(m)
 flops = 4.0 * B * H * N * N * d / (2 if causal else 1)
 t0 = time.time()
 while time.time() - t0 < 0.5:  # clock ramp

@@ -1,5 +1,5 @@
 """Error probe of a forward variant against a torch fp32 reference (diagnostics, GPU box).
-usage: MT_DIAG=1 python scripts/probe_fq.py POL KNOB [causal]
+usage: MT_DIAG=1 [OUT32=1] python scripts/probe_fq.py POL KNOB [causal]   (OUT32: fp32 output)
 Runs the default (policy 0) and POL with MT_KNOB=KNOB on randn inputs and on range cases
 (a K value past the fp16 range, rows whose scores are all far below zero, a 150x spike) and
 prints max-abs O error and max LSE error of each, plus whether the two agree."""
@@ -26,7 +26,7 @@ def ref(q, k, v):
 def run(q, k, v, p, kn):
     os.environ["MT_KNOB"] = kn
     _hip.set_policy(p)
-    o, m, l = _hip.flash_fwd(q, k, v, causal)
+    o, m, l = _hip.flash_fwd(q, k, v, causal, out_dtype=torch.float32 if os.environ.get("OUT32") == "1" else None)
     torch.cuda.synchronize()
     return o.float(), m + torch.log(l)
 
