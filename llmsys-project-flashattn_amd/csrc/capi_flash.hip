@@ -454,8 +454,11 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       // the split form also takes the grids below one split workgroup per CU, which v5's split
       // had: within ±1 % of it on four of five small shapes and 3 % behind at (2,4,2048,64)
       // (profiles/r5_ab_smallgrid.txt), so the product's d = 64 forward is v6 with v4 behind it.
+      // N % 64 != 0 (round 5): the same v6 with the partial last key tile masked in registers
+      // (VAR 65536): (8,16,4000,64) 0.614 ms on v4 against 0.487 ms for N = 4032 on v6
+      // (profiles/r5_ab_ragged.txt)
       if ((int64_t)((N + 511) / 512) * bh >= 256)
-        e = launch_fwd_v6(a, false, 66, st, handled);
+        e = launch_fwd_v6(a, false, N % 64 ? 66 | 65536 : 66, st, handled);
       if (!*handled) e = launch_fwd_v6(a, false, 18, st, handled);
     } else if ((int64_t)((N + 511) / 512 + 1) / 2 * bh >= 256) {
       // causal with at least one 8-wave workgroup per CU: paired light / heavy query blocks
