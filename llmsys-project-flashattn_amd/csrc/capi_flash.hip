@@ -468,8 +468,12 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       // the causal heads. The bf16 output takes 4-wave workgroups (W4, 256
       // queries, two per CU) where that grid keeps two workgroups per CU: the two waves of a
       // SIMD then share no barrier (0.2544 vs 0.2598 ms at C3 causal, profiles/r4_ab_fwd_w4.txt).
+      // N % 64 != 0 (round 5): the same forms with the partial last key tile staged (VAR
+      // 65536; its keys past N are past every query, so the diagonal mask hides them), except
+      // the fp32 output's fp16-PV form
       const bool w4 = !a.o_f32 && (int64_t)((N + 255) / 256 + 1) / 2 * bh >= 512;
-      e = launch_fwd_v6(a, true, a.o_f32 ? 610 : w4 ? (98 | 16384) : 98, st, handled);
+      const int rg = N % 64 ? 65536 : 0;
+      if (!rg || !a.o_f32) e = launch_fwd_v6(a, true, a.o_f32 ? 610 : (w4 ? (98 | 16384) : 98) | rg, st, handled);
     }
     // ragged N, short N, small causal grids: v4 (causal: paired, light block first, 8 waves
     // from N = 8192; profiles/r1_ab_causal_pair.txt)

@@ -311,13 +311,15 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // LDS-DMA pieces per wave)
   constexpr bool W4 = (VAR & 16384) && !SPLIT && !DUAL;
   constexpr bool PK = (VAR & 32768) && !PS;  // diagnostics: packed scale-and-shift (sm6_exp)
-  // RG (VAR 65536, non-causal 8-wave): any N >= 128, not only multiples of 64. The last key
-  // tile is partial: its rows past N arrive as zeros (the buffer range check) and their scores
-  // are masked in registers, S_B's right after the last bulk iteration's P3 computes them (its
-  // P4 starts their softmax), S_A's in the peeled last tile; queries past N are loaded clamped
-  // and not stored, as everywhere
+  // RG (VAR 65536): any N >= 128, not only multiples of 64. The last key tile is partial: its
+  // rows past N arrive as zeros (the buffer range check). Non-causal (8-wave form), their
+  // scores are masked in registers, S_B's right after the last bulk iteration's P3 computes
+  // them (its P4 starts their softmax), S_A's in the peeled last tile. Causal, the diagonal
+  // mask already hides them (a key past N is past every query below N), so only the tile
+  // count changes. Queries past N are loaded clamped and not stored, as everywhere.
   constexpr bool RG = VAR & 65536;
-  static_assert(!RG || (!CAUSAL && !SPLIT && !DUAL && !W4 && !PS), "ragged N: the non-causal 8-wave form");
+  static_assert(!RG || (!SPLIT && !DUAL && !PS && (CAUSAL || !W4)), "ragged N: the 8-wave non-causal and the causal forms");
+  constexpr bool RGM = RG && !CAUSAL;  // the key mask of the partial tile
   // H with W4: 256 threads convert a V tile (8 KiB) in two 16-B chunks each
   constexpr int NCV = W4 ? 2 : 1;
   static_assert(!(SPLIT && CAUSAL), "split keys: non-causal");
@@ -445,7 +447,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
   // diagonal tile (the last, masked; none when the wave's queries are past N). A causal wave
   // that is done keeps staging its share of the later tiles and joins every barrier (the
   // tail loop), so all waves of the workgroup take the same barriers.
-  const int ntiles = CAUSAL ? min(N, q0 + BQ) / kBK : RG ? (Nk + kBK - 1) / kBK : Nk / kBK;
+  const int ntiles = RG ? (min(Nk, CAUSAL ? q0 + BQ : Nk) + kBK - 1) / kBK : CAUSAL ? min(N, q0 + BQ) / kBK : Nk / kBK;
   const int nlast = Nk - (ntiles - 1) * kBK;  // RG: the keys of the last tile (1 .. 64)
   const int tD = qw / kBK;
   const int nbulk = CAUSAL ? (qw < N ? tD + 1 : 0) : ntiles;
@@ -581,7 +583,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       stamp(2);
       if (PFLIP == 3 && wave >= 4) __builtin_amdgcn_s_setprio(0);
       qk6<true, PS, RS, EV, H, PK>(sK, koB, qfB, SB, PS ? ciB : ci0, SA, 1, c2, nmcA, accA, pA1);  // P3
-      if (RG && last_b) mask_tail(SB);  // S_B of the partial last tile (before P4 starts its softmax)
+      if (RGM && last_b) mask_tail(SB);  // S_B of the partial last tile (before P4 starts its softmax)
       stamp(3);
       pv6<true, K2, PS, RS, EV, H, PK>(sV, vv, OA, pA0, pA1, SB, 0, c2, nmcB, accB, pB0, vk, RA);  // P4
       stamp(4);
@@ -591,7 +593,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       stamp(6);
     };
     int t = 0;
-    const int nloop = RG ? nbulk - 1 : nbulk;  // RG: the last bulk iteration peeled (its S_B mask)
+    const int nloop = RGM ? nbulk - 1 : nbulk;  // RGM: the last bulk iteration peeled (its S_B mask)
     for (; t + 4 < nloop; t += 4) {
       iter(t, 0);
       iter(t + 1, 1);
@@ -599,7 +601,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       iter(t + 3, 3);
     }
     for (; t + 1 < nloop; ++t) iter(t, t & 3);
-    if (RG) {
+    if (RGM) {
       iter(t, t & 3, true);
       ++t;
     }
@@ -612,7 +614,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       if (CAUSAL) mask_diag(SB, 32);  // S_B(tD): keys 32-63 are block B's diagonal
       qk6<true, PS, RS, EV, H, PK>(sK, koA, qfA, SA, PS ? ciA : ci0, SB, 1, c2, nmcB, accB, pB1);
       if (CAUSAL) mask_diag(SA, 0);  // S_A(tD): keys 0-31 its diagonal, 32-63 above it
-      if (RG && nlast < kBK) mask_tail(SA);
+      if (RGM && nlast < kBK) mask_tail(SA);
       pv6<true, K1, PS, RS, EV, H, PK>(sV, vv, OB, pB0, pB1, SA, 0, c2, nmcA, accA, pA0, vk, RB);
 #pragma unroll
       for (int i = 0; i < 8; ++i) sm6_fin<RS, H>(sm6_exp<PS>(SA, 1, i, c2, nmcA), i, accA, pA1);
@@ -695,7 +697,7 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
         Pf6 plo, phi, dpf;
         const float z[2] = {0.f, 0.f};
         qk6<false, false>(sK, ko, blk ? qfB : qfA, S, ci0, S, 0, c2, z, acc, dpf);
-        if (RG && t * kBK + kBK > Nk) {
+        if (RGM && t * kBK + kBK > Nk) {
 #pragma unroll
           for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
@@ -858,7 +860,7 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   *handled = false;
   const bool split = (var & 16) != 0;  // (var & 64: the widened epilogue stores)
   const bool dual = (var & 256) != 0;   // causal, two 4-wave halves with a pair each
-  const bool rg = (var & 65536) != 0;  // any N >= 128 (non-causal 8-wave form)
+  const bool rg = (var & 65536) != 0;  // any N >= 128
   if (causal != ((var & 32) != 0) || a.d != 64 || (!rg && a.N % kBK != 0) || a.N < 2 * kBK) return hipSuccess;
   if (split && (a.N % (2 * kBK) != 0 || a.N < 4 * kBK)) return hipSuccess;
   if (dual && a.N % (4 * kBQ / 2) != 0) return hipSuccess;  // whole pairs of 256-query blocks per half
@@ -875,6 +877,8 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 610: kern = fa_fwd_bf16_v6<610>; break;  // 98 with fp16 PV (the fp32-output causal default)
     case 16482: kern = fa_fwd_bf16_v6<16482>; break;  // 98 with 4-wave workgroups (the causal default)
     case 65602: kern = fa_fwd_bf16_v6<65602>; break;  // 66 for any N (the non-causal default for N % 64 != 0)
+    case 65634: kern = fa_fwd_bf16_v6<65634>; break;  // 98 for any N
+    case 82018: kern = fa_fwd_bf16_v6<82018>; break;  // 16482 for any N (the causal default for N % 64 != 0)
 #ifdef MT_DIAGNOSTICS
     case 354: kern = fa_fwd_bf16_v6<354>; break;
     case 1090: kern = fa_fwd_bf16_v6<1090>; break;  // 66 with stamps

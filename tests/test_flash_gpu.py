@@ -602,34 +602,37 @@ def test_long_causal_paired_default(torch_dev, d):
     _subset_check_fwd(torch, q, k, v, o, True, [(0, 0), (0, 2)], 1e-3, 2.0 ** -7)
 
 
+@pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", [(4, 64, 129, 64), (4, 64, 200, 64), (2, 128, 1000, 64),
                                    (1, 64, 4000, 64), (1, 64, 4001, 64)])
-def test_ragged_v6_default_vs_oracle(torch_dev, shape, parity_record):
-    """Non-causal N % 64 != 0 on grids of at least one 8-wave workgroup per CU: the default is
-    v6 with the partial last key tile masked in registers (VAR 65536, round 5; v4 before).
-    Last tiles of 1, 8, 40, 32 and 33 keys; four heads of each shape (the first, the last and
-    two between) against the C oracle at the elementwise bound, the (m, l) contract, and a
-    large score placed in the partial last tile of one row, far above the first tile's max, so
+def test_ragged_v6_default_vs_oracle(torch_dev, shape, causal, parity_record):
+    """N % 64 != 0 on grids of at least one 8-wave workgroup (causal: one pair) per CU: the
+    default is v6 with the partial last key tile staged (VAR 65536, round 5; v4 before), its
+    keys past N masked in registers (non-causal) or by the diagonal (causal; 8-wave and W4
+    forms). Last tiles of 1, 8, 40, 32 and 33 keys; four heads of each shape (the first, the
+    last and two between) against the C oracle at the elementwise bound, the (m, l) contract,
+    and a large score in the partial last tile of one row, far above the first tile's max, so
     its workgroup takes the serial recompute (which masks the same keys)."""
     from minitorch import _hip
     torch = torch_dev
     B, H, N, d = shape
     rng = np.random.default_rng(N)
     q, k, v = (rng.standard_normal(shape).astype(np.float32) for _ in range(3))
-    k[0, 0, N - 1] = q[0, 0, 5] * 40.0  # row 5 of head (0,0): a spike in the last, partial tile
+    row = N - 1 if causal else 5  # a spike in the last, partial tile that this row sees
+    k[0, 0, N - 1] = q[0, 0, row] * 40.0
     q, k, v = (A.bf16_round(x) for x in (q, k, v))
-    o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), False)
+    o, m, l = _hip.flash_fwd(*(_dev(torch, x, torch.bfloat16) for x in (q, k, v)), causal)
     torch.cuda.synchronize()
     heads = [(0, 0), (0, H - 1), (B - 1, H // 2), (B - 1, H - 1)]
     worst = 0.0
     for (b, h) in heads:
-        o_ref, m_ref, l_ref = cref.attn_fwd(q[b, h][None], k[b, h][None], v[b, h][None], False)
+        o_ref, m_ref, l_ref = cref.attn_fwd(q[b, h][None], k[b, h][None], v[b, h][None], causal)
         err = np.abs(_np(o[b, h]) - o_ref[0])
-        bound = 1e-3 + 2.0 ** -7 * _pv_abs(q[b, h][None, None], k[b, h][None, None], v[b, h][None, None], causal=False)[0, 0]
+        bound = 1e-3 + 2.0 ** -7 * _pv_abs(q[b, h][None, None], k[b, h][None, None], v[b, h][None, None], causal=causal)[0, 0]
         assert np.all(err <= bound), f"{shape} (b,h)=({b},{h}): max err/bound {float((err / bound).max()):.3f}"
         _check_ml(_np(m[b, h]), _np(l[b, h]), m_ref[0], l_ref[0], exact=False)
         worst = max(worst, float((err / bound).max()))
-    parity_record("test_ragged_v6_default_vs_oracle", f"{shape}", max_err_over_bound=worst,
+    parity_record("test_ragged_v6_default_vs_oracle", f"{shape} causal={causal}", max_err_over_bound=worst,
                   bound="1e-3 + 2^-7 * (P|V|) elementwise")
 
 
