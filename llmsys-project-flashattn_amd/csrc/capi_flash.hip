@@ -86,8 +86,6 @@ enum : int {
   kPolBwdQ64Dma = 66, kPolBwdQ64Dma8 = 69,  // 69: 66 with 8 waves (256 keys) per workgroup
   kPolBwdStagger = 70,  // 69 with SIMD partners half a step apart (non-causal, N % 64 == 0)
   kPolBwdDqPf = 71,     // 69 with the dQ kernel's Kᵀ fragments read ahead of the softmax
-  kPolBwdW64 = 72,      // dK/dV at one wave per SIMD, 64 keys per wave (non-causal, N % 32 == 0)
-  kPolBwdDqPipe = 73,   // 69 with the in-wave pipelined dQ kernel (non-causal, N % 64 == 0)
   kPolBwdMix0 = 74,     // 43's 32-query dK/dV (128 keys) with the 8-wave dQ
   kPolBwdMix4 = 75,     // 66's 4-wave LDS-DMA dK/dV with the 8-wave dQ
   // v5 with the keys split between the two halves of an 8-wave workgroup (256 queries per
@@ -141,7 +139,7 @@ static const int kValidPolicies[] = {
     kPolV5w4Reg, kPolV5Prio, kPolV5Scalar, kPolV5Stagger, kPolV5ScalarStagger,
     kPolV5StaggerPrio, kPolV5VKeep, kPolV5VKeepPrio, kPolV5Defer, kPolV5Defer3, kPolV5Defer4,
     kPolV5AsmDma, kPolD128w8, kPolD128w4, kPolD128Dma8, kPolD128Dma4, kPolBwdPipe,
-    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdW64, kPolBwdDqPipe, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal, kPolV6Wide, kPolV6SplitWide, kPolV6CausalWide, kPolV6CausalDual, kPolV6Stamp};
+    kPolBwdQ32, kPolBwdQ64OneWave, kPolBwdQ64Dma, kPolBwdQ64Dma8, kPolBwdStagger, kPolBwdDqPf, kPolBwdMix0, kPolBwdMix4, kPolV5Split, kPolBwdQ128, kPolV5RowSum, kPolV5RowSumNoKeep, kPolV6, kPolV6RowSum, kPolV6RowSumNoKeep, kPolV6RowSumEven, kPolV6Split, kPolV6Causal, kPolV5Causal8, kPolV5Causal4, kPolBwdPair, kPolBwdPair8, kPolFwdF32TwoBarrier, kPolFwdF32Ring, kPolFwdF32RingPair, kPolBwdGenNoPair, kPolBwdGenPair, kPolBwdF32Lds, kPolBwdFused, kPolBwdSplit, kPolD128v2, kPolD128v2Vs, kPolD128v2Prio, kPolD128v2w4, kPolD128v2w4Vs, kPolD128v2Ah3, kPolD128v2Ah4, kPolD128v2Causal, kPolV6Wide, kPolV6SplitWide, kPolV6CausalWide, kPolV6CausalDual, kPolV6Stamp};
 #endif
 static std::atomic<int> g_kernel_policy{kPolDefault};
 #ifdef MT_DIAGNOSTICS
@@ -673,8 +671,6 @@ static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void*
                 : pol == kPolBwdQ64Dma8    ? 5
                 : pol == kPolBwdStagger    ? 11
                 : pol == kPolBwdDqPf       ? 12
-                : pol == kPolBwdW64        ? 13
-                : pol == kPolBwdDqPipe     ? 14
                 : pol == kPolBwdMix0       ? 15
                 : pol == kPolBwdMix4       ? 16
                 : pol == kPolBwdQ128       ? 17

@@ -1,4 +1,4 @@
-// Helpers shared by the bf16 d = 64 backward kernels (fa_bwd_bf16.hip, fa_bwd_w64.hip):
+// Helpers shared by the bf16 d = 64 backward kernels (fa_bwd_bf16.hip, fa_bwd_fused.hip):
 // transpose fragments, XCD-aware block order, buffer resources and the LDS-DMA row copy.
 #pragma once
 #include "fa_fwd_bf16.h"

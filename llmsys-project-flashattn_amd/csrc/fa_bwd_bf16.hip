@@ -1088,10 +1088,6 @@ __global__ __launch_bounds__(64 * NW, 2) void fa_bwd_dq_bf16(AttnArgs p, int nqb
 
 // ---------------------------------------------------------------------------------------
 hipError_t launch_bwd_fused(const AttnArgs& a, bool causal, void* ws, hipStream_t st);
-#ifdef MT_DIAGNOSTICS
-hipError_t launch_dkv_w64(const AttnArgs& a, int nkb, unsigned nblk, size_t smem, hipStream_t st);
-hipError_t launch_dq_pipe(const AttnArgs& a, int nqb, unsigned nblk, hipStream_t st);
-#endif
 
 template <bool CAUSAL>
 static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t st) {
@@ -1112,11 +1108,12 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
 #endif
   // variant -> (dK/dV form, dQ form). dK/dV: 0 32-query steps (128 keys), 1 software-
   // pipelined, 3 / 4 64-query steps (one wave per SIMD / LDS-DMA), 5 the 8-wave LDS-DMA form
-  // (256 keys), 11 staggered SIMD partners, 13 one wave per SIMD with 64 keys per wave.
-  // dQ: 4 (128 queries) or 8 waves (256), 8 with the Kᵀ reads ahead (12), in-wave pipelined (14).
+  // (256 keys), 11 staggered SIMD partners. dQ: 4 (128 queries) or 8 waves (256), 8 with the
+  // Kᵀ reads ahead (12). (Round 2's one-wave 64-key dK/dV (13, fa_bwd_w64.hip) and in-wave
+  // pipelined dQ (14, fa_bwd_dq_pipe.hip) lost their A/Bs and were removed in round 5:
+  // profiles/r2_ab_bwd_w64.txt)
   int dkv = variant, dq = variant >= 5 ? 8 : 4;
   if (variant == 12) dkv = 5;
-  if (variant == 14) dkv = 5;
   if (variant == 15) { dkv = 0; dq = 8; }   // causal A/B: 128-key dK/dV, 8-wave dQ
   if (variant == 16) { dkv = 4; dq = 8; }   // causal A/B: 4-wave LDS-DMA dK/dV, 8-wave dQ
   if (variant == 17) { dkv = 17; dq = 8; }  // 8-wave dK/dV with 128-query steps
@@ -1125,16 +1122,14 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
   if (variant == 18) { dkv = 0; dq = 4; }
   if (variant == 19) { dkv = 0; dq = 8; }
   if (variant == 12) dq = 12;
-  if (variant == 14) dq = (CAUSAL || a.N % 64 != 0) ? 8 : 14;  // pipelined dQ: mask-free shapes
   if (dkv == 11 && (CAUSAL || a.N % 64 != 0)) dkv = 5;  // staggered form: mask-free shapes
-  if (dkv == 13 && (CAUSAL || a.N % 32 != 0)) dkv = 5;  // one-wave-per-SIMD form: the same
   {
     const int kkb = dkv >= 5 ? 256 : 128;  // keys per workgroup
-    const int nthr = dkv == 13 ? 256 : kkb * 2;
+    const int nthr = kkb * 2;
     const int nkb = (a.N + kkb - 1) / kkb;
     const int64_t nblk = (int64_t)(pair ? (nkb + 1) / 2 : nkb) * a.B * a.H;
     if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-    const size_t smem = (dkv == 11 || dkv == 17 ? 8 : (dkv == 1 || dkv == 13) ? 3 : dkv >= 2 ? 4 : 2) * (size_t)kBufQ;
+    const size_t smem = (dkv == 11 || dkv == 17 ? 8 : dkv == 1 ? 3 : dkv >= 2 ? 4 : 2) * (size_t)kBufQ;
 #ifndef MT_DIAGNOSTICS
     auto kfn = dkv == 5 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8>
                : pair   ? fa_bwd_dkv_bf16<CAUSAL, true>
@@ -1151,9 +1146,6 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
                : dkv == 8 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 6>
                : dkv == 9 ? fa_bwd_dkv_bf16_q64<CAUSAL, 2, true, 8, 7>
                           : pair ? fa_bwd_dkv_bf16<CAUSAL, true> : fa_bwd_dkv_bf16<CAUSAL>;
-    if (dkv == 13) {
-      e = launch_dkv_w64(a, nkb, (unsigned)nblk, smem, st);
-    } else
 #endif
     {
       e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -1172,7 +1164,6 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
     auto kfn = pair ? fa_bwd_dq_bf16<CAUSAL, 4, false, true>
                : dq == 8 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;
 #else
-    if (dq == 14) return launch_dq_pipe(a, nqb, (unsigned)nblk, st);
     auto kfn = dq == 12 ? fa_bwd_dq_bf16<CAUSAL, 8, true>
                : pair ? (dq == 8 ? fa_bwd_dq_bf16<CAUSAL, 8, false, true> : fa_bwd_dq_bf16<CAUSAL, 4, false, true>)
                : dq == 8 ? fa_bwd_dq_bf16<CAUSAL, 8> : fa_bwd_dq_bf16<CAUSAL>;

@@ -1032,7 +1032,7 @@ def test_fp32_fwd_policies_vs_oracle(torch_dev, policy, causal):
         _hip.set_policy(0)
 
 
-@pytest.mark.parametrize("policy", _shipped((0, 40, 43, 62, 66, 69, 70, 71, 72, 73, 74, 75, 77, 107, 108, 120, 121)))
+@pytest.mark.parametrize("policy", _shipped((0, 40, 43, 62, 66, 69, 70, 71, 74, 75, 77, 107, 108, 120, 121)))
 @pytest.mark.parametrize("causal", [False, True])
 def test_bf16_bwd_policies_vs_oracle(torch_dev, policy, causal):
     """bf16 d=64 backward variants (0 default, 40 software-pipelined dK/dV) against the
