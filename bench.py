@@ -561,6 +561,22 @@ def c5_step_leg(torch, steps: int = 20) -> dict:
         out.update(_gpu_busy_ms(torch, step, 3, "c5"))
     except Exception as e:  # noqa: BLE001
         out["c5_gpu_ms_error"] = repr(e)[:160]
+    try:  # the same step captured once as a hipGraph and replayed (minitorch/graphs.py):
+        # fresh dropout seeds and Adam step size per replay, bitwise the eager step's results
+        # (tests/test_graphs_gpu.py); the host only refills the per-step slots and launches
+        from minitorch.graphs import StepGraph
+        g = StepGraph(step, warmup=2)
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = g.replay()
+        torch.cuda.synchronize()
+        gms = (time.perf_counter() - t0) / steps * 1e3
+        out.update({"c5_graph_step_ms": round(gms, 2), "c5_graph_tokens_per_s": round(B * T / gms * 1e3, 1),
+                    "c5_graph_loss": round(float(loss.item()), 4)})
+    except Exception as e:  # noqa: BLE001
+        out["c5_graph_error"] = repr(e)[:200]
     return out
 
 

@@ -184,6 +184,10 @@ int mt_bias_gelu_fw(float* out, const float* x, const float* bias, int64_t rows,
 int mt_bias_gelu_bw(float* dx, const float* dy, const float* x, const float* bias, int64_t rows, int64_t cols,
                     void* stream);
 int mt_dropout(float* out, const float* x, int64_t n, float p, float scale, uint64_t seed, void* stream);
+/* mt_dropout with the seed read from device memory when the kernel runs (a hipGraph-captured
+ * training step writes a fresh seed there before each replay: minitorch/graphs.py) */
+int mt_dropout_dseed(float* out, const float* x, int64_t n, float p, float scale, const uint64_t* seed,
+                     void* stream);
 
 /* Embedding rows (reference minitorch/modules_basic.py Embedding.forward: one_hot(ids, V) @ W),
  * fp32, ids[ntok] the float token ids, W [V x E] and out / dout [ntok x E] contiguous:
@@ -206,6 +210,11 @@ int mt_embedding_bw(float* dweight, const float* dout, const float* ids, int64_t
 int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
                  float* const* exp_avg_sq, const int64_t* numels, double beta1, double beta2, double eps,
                  double step_size, void* stream);
+/* mt_adam_step with step_size read (as one fp32) from device memory when the kernel runs: the
+ * hipGraph-captured step's per-replay bias correction (minitorch/graphs.py) */
+int mt_adam_step_dstep(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, const int64_t* numels, double beta1, double beta2, double eps,
+                       const float* step_size, void* stream);
 
 /* ---- reference-compatible host-pointer wrappers (companion + combine) ----- */
 /* reference src/softmax_kernel.cu:233 (stream: hipStream_t) */

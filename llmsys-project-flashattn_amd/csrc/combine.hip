@@ -500,7 +500,10 @@ __global__ __launch_bounds__(256) void bias_gelu_kernel(float* __restrict__ out,
 }
 
 __global__ __launch_bounds__(256) void dropout_kernel(float* __restrict__ out, const float* __restrict__ x,
-                                                      int64_t n, float p, float scale, uint64_t seed) {
+                                                      int64_t n, float p, float scale, uint64_t seed,
+                                                      const uint64_t* __restrict__ seedp) {
+  // seedp: the seed in device memory (a graph-captured step draws a fresh one per replay)
+  if (seedp) seed = *seedp;
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
     const uint64_t h = mix64(seed + 0x9e3779b97f4a7c15ull * (uint64_t)(i + 1));
@@ -624,9 +627,10 @@ struct AdamArgs {
   int blk0[kAdamMax + 1];
   int nt;
   float b1, b2, c1, c2, step, eps;  // c1 = 1 - b1, c2 = 1 - b2
+  const float* stepp;  // non-null: the step size in device memory (read instead of step)
 };
 
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a) {
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a, float step) {
   // separately rounded products and sums, like the tensor ops (plain operators under the
   // pragma: the __f*_rn helpers are inlined from a header compiled with contraction on)
 #pragma clang fp contract(off)
@@ -634,7 +638,7 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   v = v * a.b2 + (g * g) * a.c2;
   // the tensor-op form divides as a product with the reciprocal (Tensor.__truediv__ =
   // Mul(a, Inv(b))) and takes the square root as PowerScalar's powf(v, 0.5)
-  p = p - (a.step * m) * (1.f / (powf(v, 0.5f) + a.eps));
+  p = p - (step * m) * (1.f / (powf(v, 0.5f) + a.eps));
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
@@ -647,19 +651,20 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   float* M = a.m[t];
   float* V = a.v[t];
   const bool vec = ((((uintptr_t)P | (uintptr_t)G | (uintptr_t)M | (uintptr_t)V) & 15) == 0);
+  const float step = a.stepp ? *a.stepp : a.step;
   const int64_t i = base + 4 * threadIdx.x;
   if (vec && i + 4 <= n) {
     float4 p = *(float4*)(P + i), m = *(float4*)(M + i), v = *(float4*)(V + i);
     const float4 g = *(const float4*)(G + i);
-    adam_elem(p.x, g.x, m.x, v.x, a);
-    adam_elem(p.y, g.y, m.y, v.y, a);
-    adam_elem(p.z, g.z, m.z, v.z, a);
-    adam_elem(p.w, g.w, m.w, v.w, a);
+    adam_elem(p.x, g.x, m.x, v.x, a, step);
+    adam_elem(p.y, g.y, m.y, v.y, a, step);
+    adam_elem(p.z, g.z, m.z, v.z, a, step);
+    adam_elem(p.w, g.w, m.w, v.w, a, step);
     *(float4*)(P + i) = p;
     *(float4*)(M + i) = m;
     *(float4*)(V + i) = v;
   } else {
-    for (int64_t j = i; j < min(i + 4, n); ++j) adam_elem(P[j], G[j], M[j], V[j], a);
+    for (int64_t j = i; j < min(i + 4, n); ++j) adam_elem(P[j], G[j], M[j], V[j], a, step);
   }
 }
 
@@ -889,8 +894,19 @@ int mt_bias_gelu_bw(float* dx, const float* dy, const float* x, const float* bia
 int mt_dropout(float* out, const float* x, int64_t n, float p, float scale, uint64_t seed, void* stream) {
   if (n < 0) return set_error("mt_dropout: n = %lld", (long long)n);
   if (n == 0) return 0;
-  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, x, n, p, scale, seed);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, x, n, p, scale, seed,
+                     nullptr);
   return check_hip(hipGetLastError(), "mt_dropout");
+}
+
+int mt_dropout_dseed(float* out, const float* x, int64_t n, float p, float scale, const uint64_t* seed,
+                     void* stream) {
+  if (n < 0) return set_error("mt_dropout_dseed: n = %lld", (long long)n);
+  if (!seed) return set_error("mt_dropout_dseed: null seed pointer");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, out, x, n, p, scale,
+                     (uint64_t)0, seed);
+  return check_hip(hipGetLastError(), "mt_dropout_dseed");
 }
 
 int mt_embedding_fw(float* out, const float* ids, const float* weight, int64_t ntok, int64_t V, int64_t E,
@@ -914,16 +930,16 @@ int mt_embedding_bw(float* dweight, const float* dout, const float* ids, int64_t
   return check_hip(hipGetLastError(), "mt_embedding_bw");
 }
 
-int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
-                 float* const* exp_avg_sq, const int64_t* numels, double beta1, double beta2, double eps,
-                 double step_size, void* stream) {
+static int adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                     float* const* exp_avg_sq, const int64_t* numels, double beta1, double beta2, double eps,
+                     double step_size, const float* step_dev, void* stream) {
   if (n_tensors < 0) return set_error("mt_adam_step: n_tensors = %d", n_tensors);
   for (int t0 = 0; t0 < n_tensors; t0 += kAdamMax) {
     AdamArgs a;
     memset(&a, 0, sizeof(a));
     // each constant rounded to fp32 once, as the tensor-op form's scalar operands are
     a.b1 = (float)beta1; a.b2 = (float)beta2; a.c1 = (float)(1.0 - beta1); a.c2 = (float)(1.0 - beta2);
-    a.step = (float)step_size; a.eps = (float)eps;
+    a.step = (float)step_size; a.eps = (float)eps; a.stepp = step_dev;
     int64_t blocks = 0;
     for (int t = t0; t < std::min(n_tensors, t0 + kAdamMax); ++t) {
       if (numels[t] < 0) return set_error("mt_adam_step: numel %lld", (long long)numels[t]);
@@ -942,6 +958,21 @@ int mt_adam_step(int n_tensors, float* const* params, const float* const* grads,
     if (check_hip(hipGetLastError(), "mt_adam_step")) return 1;
   }
   return 0;
+}
+
+int mt_adam_step(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                 float* const* exp_avg_sq, const int64_t* numels, double beta1, double beta2, double eps,
+                 double step_size, void* stream) {
+  return adam_step(n_tensors, params, grads, exp_avg, exp_avg_sq, numels, beta1, beta2, eps, step_size, nullptr,
+                   stream);
+}
+
+int mt_adam_step_dstep(int n_tensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                       float* const* exp_avg_sq, const int64_t* numels, double beta1, double beta2, double eps,
+                       const float* step_size, void* stream) {
+  if (!step_size) return set_error("mt_adam_step_dstep: null step-size pointer");
+  return adam_step(n_tensors, params, grads, exp_avg, exp_avg_sq, numels, beta1, beta2, eps, 0.0, step_size,
+                   stream);
 }
 
 }  // extern "C"

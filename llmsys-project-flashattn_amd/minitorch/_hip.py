@@ -56,6 +56,7 @@ _PROTOS = {
     "mt_bias_gelu_fw": (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_bias_gelu_bw": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp]),
     "mt_dropout": (_int, [_vp, _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_uint64, _vp]),
+    "mt_dropout_dseed": (_int, [_vp, _vp, _i64, ctypes.c_float, ctypes.c_float, _vp, _vp]),
     "mt_embedding_fw": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
     "mt_embedding_bw": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _vp]),
     "mt_softmax_xent_fw": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp]),
@@ -71,6 +72,8 @@ _PROTOS = {
     "mt_rand_uniform": (_int, [_vp, _i64, ctypes.c_uint64, _vp]),
     "mt_adam_step": (_int, [_int, _vpp, _vpp, _vpp, _vpp, _i64p, ctypes.c_double, ctypes.c_double,
                             ctypes.c_double, ctypes.c_double, _vp]),
+    "mt_adam_step_dstep": (_int, [_int, _vpp, _vpp, _vpp, _vpp, _i64p, ctypes.c_double, ctypes.c_double,
+                                  ctypes.c_double, _vp, _vp]),
     "mt_set_gemm_backend": (None, [_int]),
     "launch_attn_softmax": (None, [_fp, _fp, _int, _int, _int, _int, ctypes.c_bool, _vp]),
     "launch_attn_softmax_bw": (None, [_fp, _fp, _int, _int, _vp]),
@@ -290,11 +293,16 @@ def exported_symbols() -> Sequence[str]:
     return tuple(_PROTOS)
 
 
-def adam_step(params, grads, exp_avg, exp_avg_sq, numels, beta1, beta2, eps, step_size) -> None:
+def adam_step(params, grads, exp_avg, exp_avg_sq, numels, beta1, beta2, eps, step_size,
+              step_size_ptr: Optional[int] = None) -> None:
     """One multi-tensor Adam launch (mt_adam_step) over dense fp32 device buffers given as
-    raw pointers, in place, on the current stream."""
+    raw pointers, in place, on the current stream. step_size_ptr: read the step size from
+    that device fp32 instead (mt_adam_step_dstep, a graph-captured step)."""
     n = len(params)
     arr = ctypes.c_void_p * max(1, n)
-    check(lib().mt_adam_step(n, arr(*params), arr(*grads), arr(*exp_avg), arr(*exp_avg_sq),
-                              (ctypes.c_int64 * max(1, n))(*numels), beta1, beta2, eps, step_size,
-                              stream_ptr()), "mt_adam_step")
+    ptrs = (n, arr(*params), arr(*grads), arr(*exp_avg), arr(*exp_avg_sq), (ctypes.c_int64 * max(1, n))(*numels),
+            beta1, beta2, eps)
+    if step_size_ptr is None:
+        check(lib().mt_adam_step(*ptrs, step_size, stream_ptr()), "mt_adam_step")
+    else:
+        check(lib().mt_adam_step_dstep(*ptrs, step_size_ptr, stream_ptr()), "mt_adam_step_dstep")

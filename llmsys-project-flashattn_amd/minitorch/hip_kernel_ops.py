@@ -267,8 +267,12 @@ class HipKernelOps(TensorOps):
         rand(shape) > p, never stored: the backward redraws it from the seed)."""
         x = _dense(x)
         out = _out(x, x.shape)
-        _hip.check(_hip.lib().mt_dropout(_ptr(out), _ptr(x), x.size, ctypes.c_float(p), ctypes.c_float(scale),
-                                         seed & 0xFFFFFFFFFFFFFFFF, _stream()), "dropout")
+        if isinstance(seed, int):
+            _hip.check(_hip.lib().mt_dropout(_ptr(out), _ptr(x), x.size, ctypes.c_float(p), ctypes.c_float(scale),
+                                             seed & 0xFFFFFFFFFFFFFFFF, _stream()), "dropout")
+        else:  # a device-resident seed (tensor_functions._DeviceSeed, a graph-captured step)
+            _hip.check(_hip.lib().mt_dropout_dseed(_ptr(out), _ptr(x), x.size, ctypes.c_float(p),
+                                                   ctypes.c_float(scale), seed.ptr, _stream()), "dropout")
         return out
 
     @staticmethod

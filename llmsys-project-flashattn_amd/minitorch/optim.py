@@ -6,7 +6,9 @@ dense fp32 device buffers in one multi-tensor kernel (``mt_adam_step``): the sam
 and order as the tensor-op form below, bit for bit (tests/test_optim_gpu.py), but in place:
 the parameter's storage is updated (the tensor-op form gives ``p.value`` a new tensor) and
 ``p.value.grad`` is left as it is (neither path clears it; call ``zero_grad``). Anything else
-takes the tensor-op form, which is also the CPU backend's path."""
+takes the tensor-op form, which is also the CPU backend's path. Inside a graph capture
+(``graphs.StepGraph``) the fused launch reads its step size from a device slot that every replay
+refills after advancing the step counters (``mt_adam_step_dstep``)."""
 from __future__ import annotations
 
 import math
@@ -43,6 +45,8 @@ class Adam(Optimizer):
         self._states = {id(p): {} for p in parameters}
 
     def step(self) -> None:
+        from .graphs import capturing
+        g = capturing()
         fused = {}  # step count -> [(param, grad, state)]
         for p in self.parameters:
             grad = getattr(p.value, "grad", None) if p.value is not None else None
@@ -50,24 +54,42 @@ class Adam(Optimizer):
                 continue
             st = self._states[id(p)]
             if not st:
+                if g is not None:
+                    raise RuntimeError("Adam: a parameter got its first gradient inside a graph capture; "
+                                       "warm the step up eagerly first")
                 st["step"] = 0
                 st["exp_avg"] = grad.zeros()
                 st["exp_avg_sq"] = grad.zeros()
-            st["step"] += 1
             if _fusable(p.value, grad, st["exp_avg"], st["exp_avg_sq"]):
-                fused.setdefault(st["step"], []).append((p, grad, st))
+                # captured: each replay advances the counter (graphs.StepGraph slot below)
+                fused.setdefault(st["step"] + 1, []).append((p, grad, st))
+                if g is None:
+                    st["step"] += 1
                 continue
+            if g is not None:
+                raise RuntimeError("Adam: only the fused multi-tensor path (dense fp32 device buffers) "
+                                   "can run inside a graph capture")
+            st["step"] += 1
             st["exp_avg"] = st["exp_avg"] * self.beta1 + grad * (1 - self.beta1)
             st["exp_avg_sq"] = st["exp_avg_sq"] * self.beta2 + (grad * grad) * (1 - self.beta2)
             p.update(p.value.detach() - self._step_size(st["step"]) * st["exp_avg"] / (st["exp_avg_sq"] ** 0.5 + self.eps))
         for t, group in fused.items():
             from . import _hip
+            step_ptr = None
+            if g is not None:
+                states = [st for _, _, st in group]
+
+                def advance(states=states):
+                    for st in states:
+                        st["step"] += 1
+                    return self._step_size(states[0]["step"])
+                step_ptr = g.f32_slot(advance)
             _hip.adam_step([p.value._tensor.data_ptr() for p, _, _ in group],
-                           [g._tensor.data_ptr() for _, g, _ in group],
+                           [gr._tensor.data_ptr() for _, gr, _ in group],
                            [st["exp_avg"]._tensor.data_ptr() for _, _, st in group],
                            [st["exp_avg_sq"]._tensor.data_ptr() for _, _, st in group],
                            [p.value._tensor.size for p, _, _ in group],
-                           self.beta1, self.beta2, self.eps, self._step_size(t))
+                           self.beta1, self.beta2, self.eps, self._step_size(t), step_size_ptr=step_ptr)
 
     def _step_size(self, t: int) -> float:
         bc1 = 1.0 - self.beta1 ** t

@@ -88,7 +88,10 @@ class Tensor:
                     import torch
                     st = torch.full((1,), float(b), dtype=torch.float32, device="cuda")
                     c = Tensor(TensorData(st, (1,)), backend=self.backend)
-                    if len(_DEV_SCALARS) < 4096:
+                    # one made inside a graph capture is filled only when the graph runs: not
+                    # shared with eager code
+                    from .graphs import capturing
+                    if len(_DEV_SCALARS) < 4096 and capturing() is None:
                         _DEV_SCALARS[key] = c
                 return c
             return Tensor.make([float(b)], (1,), backend=self.backend)
@@ -309,7 +312,10 @@ class Tensor:
     def backward(self, grad_output: Optional["Tensor"] = None) -> None:
         if grad_output is None:
             assert self.shape == (1,), "Must provide grad_output if non-scalar"
-            grad_output = Tensor.make([1.0], (1,), backend=self.backend, device=self.backend.cuda)
+            # on the HIP backend the shared device constant 1.0: no host-to-device copy (a
+            # pageable copy waits for the queued forward and cannot be captured in a graph)
+            grad_output = (self._ensure_tensor(1.0) if self.backend.cuda else
+                           Tensor.make([1.0], (1,), backend=self.backend))
         backpropagate(self, grad_output)
 
     def zero_grad_(self) -> None:

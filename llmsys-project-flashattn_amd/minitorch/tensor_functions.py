@@ -290,6 +290,14 @@ class EmbeddingGather(Function):
         return 0.0, grad_output.f.embedding_bw(grad_output, ids, V)
 
 
+class _DeviceSeed:
+    """A dropout seed held in device memory (its address), for graph-captured steps."""
+    __slots__ = ("ptr",)
+
+    def __init__(self, ptr: int):
+        self.ptr = ptr
+
+
 class DropoutMask(Function):
     """Dropout with the keep mask drawn on the device from a seed (keep = u > p, then scaled by
     1 / (1 - p), reference modules_basic.py Dropout) in one kernel, and redrawn from the same
@@ -299,8 +307,15 @@ class DropoutMask(Function):
     @staticmethod
     def forward(ctx, x, p):
         rate = float(p.item())
-        seed = int(np.random.randint(0, 2**63 - 1, dtype=np.int64))
         scale = float(np.float32(1.0) / np.float32(1.0 - rate))
+        from .graphs import capturing
+        g = capturing()
+        if g is not None:
+            # a captured step (graphs.StepGraph): the seed lives in a device slot that each
+            # replay refills with this same draw, and the kernels read it from there
+            seed = _DeviceSeed(g.seed_slot(lambda: int(np.random.randint(0, 2**63 - 1, dtype=np.int64))))
+        else:
+            seed = int(np.random.randint(0, 2**63 - 1, dtype=np.int64))
         ctx.save_for_backward(rate, scale, seed)
         return x.f.dropout_fw(x, rate, scale, seed)
 
