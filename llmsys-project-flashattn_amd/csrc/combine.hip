@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <vector>
 
 #include <rocblas/rocblas.h>
 
@@ -298,14 +299,126 @@ __global__ __launch_bounds__(256) void reduce_cols_fold(int fn, float* __restric
   out[t] = hv ? apply_fn(fn, start, v) : start;
 }
 
-// The partial buffer of the column reductions, one per (device, stream): grown on demand
-// and kept, so the reductions of one stream reuse it in that stream's order, and reductions
-// enqueued on two streams (or from two host threads on two streams) never share partials.
+// One-pass column reduction (round 5) for [outer][len][inner] with inner % 4 = 0 and 16-byte
+// aligned rows: workgroup (column block of 256, row chunk r, outer o) has 8 waves; a lane owns 4
+// adjacent columns (float4 loads: a wave reads one 1 KiB row segment per load) and a wave takes
+// every 8th row of the chunk, 8 loads in flight; the 8 wave partials fold through LDS in wave
+// order. With R > 1 chunks the chunk's partial goes to the scratch, the workgroup counts its
+// arrival on the column block's counter (agent scope, after a release fence), and the last of
+// the R arrivals folds the R partials in chunk order (8 waves over consecutive chunk ranges, then
+// in wave order through LDS), writes the result and resets the counter for the next launch.
+// Fixed association for a given shape: deterministic. Replaces the reduce + fold pair at config
+// 5's bias gradients (4992 x 256: 16.6 + 8.6 µs per call in the C5 step, scripts/reduce_probe.py).
+constexpr int kCol1Waves = 8;
+template <int FN>  // FN >= 0: the op folded in at compile time (add, mul, max); -1: fn at run time
+__global__ __launch_bounds__(512) void reduce_cols1_kernel(int fn_rt, float* __restrict__ out,
+                                                           float* __restrict__ part,
+                                                           unsigned* __restrict__ counters,
+                                                           const float* __restrict__ a, int64_t len,
+                                                           int64_t inner, int64_t chunk, float start) {
+  const int fn = FN >= 0 ? FN : fn_rt;
+  __shared__ float4 red[kCol1Waves][64];
+  __shared__ int have_s[kCol1Waves];
+  __shared__ int last_s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cbn = gridDim.x, R = gridDim.y, r = blockIdx.y, o = blockIdx.z;
+  const int64_t col = (int64_t)blockIdx.x * 256 + lane * 4;
+  const bool live = col < inner;
+  const int64_t j0 = (int64_t)r * chunk, j1 = min(len, j0 + chunk);
+  const float* src = a + (int64_t)o * len * inner + col;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  bool have = false;
+  if (live) {
+    for (int64_t j = j0 + w; j < j1; j += 8 * kCol1Waves) {
+      float4 x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // 8 loads in flight (clamped rows, folded only when in range)
+        const int64_t jj = min(j + (int64_t)u * kCol1Waves, j1 - 1);
+        x[u] = *(const float4*)(src + jj * inner);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (j + (int64_t)u * kCol1Waves >= j1) break;
+        if (!have) { acc = x[u]; have = true; continue; }
+        acc.x = apply_fn(fn, acc.x, x[u].x); acc.y = apply_fn(fn, acc.y, x[u].y);
+        acc.z = apply_fn(fn, acc.z, x[u].z); acc.w = apply_fn(fn, acc.w, x[u].w);
+      }
+    }
+  }
+  red[w][lane] = acc;
+  if (lane == 0) have_s[w] = have;
+  __syncthreads();
+  if (w == 0) {
+    float4 v = red[0][lane];  // wave 0 always has a row: every chunk holds at least one
+    for (int k = 1; k < kCol1Waves; ++k) {
+      if (!have_s[k]) break;  // waves past the chunk's last row
+      const float4 y = red[k][lane];
+      v.x = apply_fn(fn, v.x, y.x); v.y = apply_fn(fn, v.y, y.y);
+      v.z = apply_fn(fn, v.z, y.z); v.w = apply_fn(fn, v.w, y.w);
+    }
+    if (R == 1) {
+      if (live) {
+        v.x = apply_fn(fn, start, v.x); v.y = apply_fn(fn, start, v.y);
+        v.z = apply_fn(fn, start, v.z); v.w = apply_fn(fn, start, v.w);
+        *(float4*)(out + (int64_t)o * inner + col) = v;
+      }
+      return;
+    }
+    if (live) *(float4*)(part + ((int64_t)o * R + r) * inner + col) = v;
+    __threadfence();  // release the partial at agent scope before the arrival
+    if (lane == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(counters + (int64_t)o * cbn + blockIdx.x, 1u,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_s = prev == (unsigned)(R - 1);
+    }
+  }
+  __syncthreads();
+  if (R == 1 || !last_s) return;
+  __threadfence();  // acquire: the other chunks' partials
+  const int per = (R + kCol1Waves - 1) / kCol1Waves;
+  const int r0 = w * per, r1 = min(R, r0 + per);
+  const float* p = part + (int64_t)o * R * inner + col;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live && r0 < r1) {
+    v = *(const float4*)(p + (int64_t)r0 * inner);
+    for (int q = r0 + 1; q < r1; ++q) {
+      const float4 y = *(const float4*)(p + (int64_t)q * inner);
+      v.x = apply_fn(fn, v.x, y.x); v.y = apply_fn(fn, v.y, y.y);
+      v.z = apply_fn(fn, v.z, y.z); v.w = apply_fn(fn, v.w, y.w);
+    }
+  }
+  red[w][lane] = v;
+  if (lane == 0) have_s[w] = r0 < r1;
+  __syncthreads();
+  if (w == 0) {
+    float4 t = red[0][lane];
+    for (int k = 1; k < kCol1Waves; ++k) {
+      if (!have_s[k]) break;
+      const float4 y = red[k][lane];
+      t.x = apply_fn(fn, t.x, y.x); t.y = apply_fn(fn, t.y, y.y);
+      t.z = apply_fn(fn, t.z, y.z); t.w = apply_fn(fn, t.w, y.w);
+    }
+    if (live) {
+      t.x = apply_fn(fn, start, t.x); t.y = apply_fn(fn, start, t.y);
+      t.z = apply_fn(fn, start, t.z); t.w = apply_fn(fn, start, t.w);
+      *(float4*)(out + (int64_t)o * inner + col) = t;
+    }
+    if (lane == 0) counters[(int64_t)o * cbn + blockIdx.x] = 0u;  // ready for the next launch
+  }
+}
+
+// The partial buffer of the column reductions and split-K GEMMs, one per (device, stream):
+// grown on demand and kept, so the users of one stream reuse it in that stream's order, and
+// users on two streams (or two host threads on two streams) never share partials. A buffer
+// that is outgrown is retired, not freed: a captured hipGraph (minitorch/graphs.py) keeps the
+// address it was captured with, and an eager call that grows the buffer afterwards must not
+// pull the memory from under its replays.
 static void* reduce_scratch(size_t bytes, hipStream_t st) {
   struct Slot { int dev; hipStream_t st; void* buf; size_t cap; };
   static std::mutex mu;
   static Slot slots[64] = {};
   static int nslots = 0;
+  static std::vector<void*> retired;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
   std::lock_guard<std::mutex> lock(mu);
@@ -318,16 +431,42 @@ static void* reduce_scratch(size_t bytes, hipStream_t st) {
     *s = Slot{dev, st, nullptr, 0};
   }
   if (s->cap < bytes) {
-    if (s->buf) {
-      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;  // in-flight users of the old buffer
-      (void)hipFree(s->buf);
-    }
-    s->buf = nullptr;
-    s->cap = 0;
-    if (hipMalloc(&s->buf, bytes) != hipSuccess) { s->buf = nullptr; return nullptr; }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    // no allocation inside a capture: the caller then takes its unchunked path
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    void* nb = nullptr;
+    bytes = std::max(bytes, 2 * s->cap);
+    if (hipMalloc(&nb, bytes) != hipSuccess) return nullptr;
+    if (s->buf) retired.push_back(s->buf);
+    s->buf = nb;
     s->cap = bytes;
   }
   return s->buf;
+}
+
+// Arrival counters of the one-pass column reduction, one zeroed block per (device, stream),
+// allocated once outside any capture; each launch's last arrivals reset the counters they used.
+constexpr int64_t kColCounters = 1 << 16;
+static unsigned* reduce_counters(hipStream_t st) {
+  struct Slot { int dev; hipStream_t st; unsigned* buf; };
+  static std::mutex mu;
+  static Slot slots[64] = {};
+  static int nslots = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  for (int i = 0; i < nslots; ++i)
+    if (slots[i].dev == dev && slots[i].st == st) return slots[i].buf;
+  if (nslots == 64) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  unsigned* b = nullptr;
+  if (hipMalloc(&b, kColCounters * sizeof(unsigned)) != hipSuccess) return nullptr;
+  // zeroed in the stream's own order: a legacy hipMemset need not precede work on a non-blocking
+  // stream (torch's side streams), and a counter left at garbage never elects a last arrival
+  if (hipMemsetAsync(b, 0, kColCounters * sizeof(unsigned), st) != hipSuccess) { (void)hipFree(b); return nullptr; }
+  slots[nslots++] = Slot{dev, st, b};
+  return b;
 }
 
 // Batched GEMM C[b] = A[b] @ B[b], fp32, exact fp32 MFMA. A: [M,K], B: [K,N], C: [M,N],
@@ -751,7 +890,31 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   for (int d = reduce_dim + 1; d < dims; ++d) inner *= a_shape[d];
   for (int d = 0; d < reduce_dim; ++d) outer *= a_shape[d];
   const int64_t len = a_shape[reduce_dim];
-  if (al.contiguous && ol.contiguous && inner >= 16 && len >= 16 && outer <= 65535) {
+  if (al.contiguous && ol.contiguous && inner % 4 == 0 && inner >= 64 && len >= 16 && outer <= 65535 &&
+      ((((uintptr_t)a | (uintptr_t)out) & 15) == 0)) {
+    // one pass: row chunks of at least 8 rows per wave, about 256 workgroups in all
+    const int64_t cb = (inner + 255) / 256;
+    int64_t R = std::max<int64_t>(1, std::min<int64_t>(256 / (cb * outer), len / (8 * kCol1Waves)));
+    int64_t chunk = (len + R - 1) / R;
+    R = (len + chunk - 1) / chunk;  // every chunk holds a row
+    float* part = nullptr;
+    unsigned* ctr = nullptr;
+    if (R > 1) {
+      part = (float*)reduce_scratch((size_t)(outer * R * inner) * 4, (hipStream_t)stream);
+      ctr = outer * cb <= kColCounters ? reduce_counters((hipStream_t)stream) : nullptr;
+      if (!part || !ctr) { R = 1; chunk = len; }
+    }
+    const dim3 grid((unsigned)cb, (unsigned)R, (unsigned)outer);
+    const hipStream_t st = (hipStream_t)stream;
+    if (fn == FN_ADD)
+      hipLaunchKernelGGL(reduce_cols1_kernel<FN_ADD>, grid, dim3(512), 0, st, fn, out, part, ctr, a, len, inner, chunk, start);
+    else if (fn == FN_MUL)
+      hipLaunchKernelGGL(reduce_cols1_kernel<FN_MUL>, grid, dim3(512), 0, st, fn, out, part, ctr, a, len, inner, chunk, start);
+    else if (fn == FN_MAX)
+      hipLaunchKernelGGL(reduce_cols1_kernel<FN_MAX>, grid, dim3(512), 0, st, fn, out, part, ctr, a, len, inner, chunk, start);
+    else
+      hipLaunchKernelGGL(reduce_cols1_kernel<-1>, grid, dim3(512), 0, st, fn, out, part, ctr, a, len, inner, chunk, start);
+  } else if (al.contiguous && ol.contiguous && inner >= 16 && len >= 16 && outer <= 65535) {
     // R row chunks: as many as give the grid about 512 workgroups, at most kColRMax, chunks of
     // at least 64 rows (128 where the rows allow)
     const int64_t cb = (inner + 63) / 64;
@@ -800,6 +963,23 @@ static rocblas_handle blas_handle() {
   return handles[dev];
 }
 
+// Split-K: C = the S partial products [S][M][N] summed in slice order (fixed: deterministic).
+__global__ __launch_bounds__(256) void splitk_sum_kernel(float* __restrict__ c, const float* __restrict__ part,
+                                                         int S, int64_t M, int64_t N, int64_t ldc) {
+  const int64_t n4 = N / 4, total = M * n4, slice = M * N;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += step) {
+    const int64_t m = t / n4, j = (t - m * n4) * 4;
+    const float* p = part + m * N + j;
+    float4 acc = *(const float4*)p;
+    for (int k = 1; k < S; ++k) {
+      const float4 v = *(const float4*)(p + k * slice);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *(float4*)(c + m * ldc + j) = acc;
+  }
+}
+
 // Row-major C[M,N] = A[M,K]·B[K,N] as column-major Cᵀ = Bᵀ·Aᵀ. Returns false (caller
 // falls back) when a layout has no unit stride or a leading dimension rocBLAS rejects.
 static bool gemm_rocblas(float* c, const float* a, const float* b, int64_t batch, int64_t M,
@@ -830,6 +1010,29 @@ static bool gemm_rocblas(float* c, const float* a, const float* b, int64_t batch
   if (!h) return false;
   rocblas_set_stream(h, st);
   const float alpha = 1.f, beta = 0.f;
+  // A long reduction into a small output (config 5's LM-head dX: 4992 x 256 over K = 10000,
+  // 78 output tiles for 256 CUs) runs as S batched K slices into partials plus an ordered sum:
+  // 547 -> 197 µs at S = 8 (scripts/gemm_probe.py). Only for one matrix, K >= 8192, < 128
+  // tiles of 128 x 128, S | K, N % 4 = 0 and 16-byte aligned rows.
+  if (batch == 1 && K >= 8192 && ((M + 127) / 128) * ((N + 127) / 128) < 128 && N % 4 == 0 && scm % 4 == 0 &&
+      ((uintptr_t)c & 15) == 0) {
+    int S = 0;
+    for (int cand : {8, 4, 2})
+      if (K % cand == 0 && K / cand >= 1024) { S = cand; break; }
+    float* part = S ? (float*)reduce_scratch((size_t)S * M * N * 4, st) : nullptr;
+    if (part) {
+      const int64_t ks = K / S;
+      // slice s: B rows [s ks, (s+1) ks) (the first operand's K offset), A columns likewise
+      const int64_t strb = opb == rocblas_operation_none ? ks * ldb : ks;
+      const int64_t stra = opa == rocblas_operation_none ? ks : ks * lda;
+      *status = rocblas_sgemm_strided_batched(h, opb, opa, (rocblas_int)N, (rocblas_int)M, (rocblas_int)ks,
+                                              &alpha, b, (rocblas_int)ldb, strb, a, (rocblas_int)lda, stra,
+                                              &beta, part, (rocblas_int)N, M * N, (rocblas_int)S);
+      if (*status == rocblas_status_success)
+        hipLaunchKernelGGL(splitk_sum_kernel, dim3(grid_for(M * N / 4)), dim3(256), 0, st, c, part, S, M, N, scm);
+      return true;
+    }
+  }
   *status = rocblas_sgemm_strided_batched(h, opb, opa, (rocblas_int)N, (rocblas_int)M, (rocblas_int)K,
                                           &alpha, b, (rocblas_int)ldb, sb[0], a, (rocblas_int)lda, sa[0],
                                           &beta, c, (rocblas_int)scm, sc[0], (rocblas_int)batch);

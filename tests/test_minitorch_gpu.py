@@ -85,17 +85,21 @@ def test_zip_map_paths(mt, case):
 
 @pytest.mark.parametrize("shape,dim", [((4992, 256), 0), ((300, 10000), 0), ((3, 40, 70), 1),
                                        ((17, 33), 0), ((50, 64, 1), 0), ((4992, 10000), 0),
-                                       ((16, 20), 0), ((3, 4096, 80), 1), ((2000, 17), 0)])
+                                       ((16, 20), 0), ((3, 4096, 80), 1), ((2000, 17), 0),
+                                       ((5, 1000, 300), 1), ((4992, 4), 0), ((70, 128), 0)])
 def test_reduce_paths(mt, shape, dim):
-    """Sum and max over a non-innermost dim (the coalesced column kernel where the layout
-    allows: bias gradients) and the other reduce kernels, against NumPy."""
+    """Sum and max over a non-innermost dim (the one-pass column kernel with arrival counters
+    where the layout allows: bias gradients; the two-kernel column form; the other reduce
+    kernels) against NumPy; a repeated sum is bitwise equal (fixed fold order, counters reset)."""
     minitorch, B = mt
     rng = np.random.default_rng(sum(shape) + dim)
     x = rng.standard_normal(shape).astype(np.float32)
     t = minitorch.tensor_from_numpy(x, B)
-    np.testing.assert_allclose(t.sum(dim).to_numpy(), x.sum(dim, keepdims=True), rtol=1e-4,
+    s1 = t.sum(dim).to_numpy()
+    np.testing.assert_allclose(s1, x.sum(dim, keepdims=True), rtol=1e-4,
                                atol=1e-4 * np.sqrt(shape[dim]))
     np.testing.assert_array_equal(minitorch.max(t, dim).to_numpy(), x.max(dim, keepdims=True))
+    np.testing.assert_array_equal(t.sum(dim).to_numpy(), s1)
 
 
 def test_bias_gelu_fused(mt):
@@ -244,6 +248,26 @@ def test_matmul(mt, shapes, gemm_backend):
         _matmul_case(mt, shapes)
     finally:
         _hip.lib().mt_set_gemm_backend(0)
+
+
+@pytest.mark.parametrize("transposed", [False, True])
+def test_matmul_split_k(mt, transposed):
+    """A long reduction into a small output (K >= 8192, under 128 output tiles: config 5's
+    LM-head dX) runs as 8 batched K slices plus an ordered sum of the partials (combine.hip
+    gemm_rocblas); against NumPy in fp64, plain and with a transposed right operand, and
+    bitwise repeatable."""
+    minitorch, B = mt
+    rng = np.random.default_rng(7)
+    M, K, N = 300, 8192, 64
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    w = rng.standard_normal((K, N)).astype(np.float32)
+    tx = minitorch.tensor_from_numpy(x, B)
+    tw = (minitorch.tensor_from_numpy(np.ascontiguousarray(w.T), B).permute(1, 0) if transposed
+          else minitorch.tensor_from_numpy(w, B))
+    out = (tx @ tw).to_numpy()
+    ref = x.astype(np.float64) @ w.astype(np.float64)
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-6 * K)
+    np.testing.assert_array_equal((tx @ tw).to_numpy(), out)
 
 
 def _matmul_case(mt, shapes):
