@@ -16,6 +16,7 @@
 // for arbitrary strides.
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -197,6 +198,51 @@ __global__ __launch_bounds__(256) void reduce_wave_kernel(int fn, float* out, La
       have = have || hy;
     }
     if (lane == 0) out[out_pos<int64_t>(o, ol)] = have ? apply_fn(fn, start, acc) : start;
+  }
+}
+// Few outputs over a long axis (the loss sums of config 5: 4992 -> 1, where one wave per output
+// ran 23 µs): one 1024-thread workgroup per output, 8 loads in flight per lane, the lanes'
+// partials folded by a butterfly per wave and then in wave order through LDS (deterministic).
+template <int FN>
+__global__ __launch_bounds__(1024) void reduce_block_kernel(int fn_rt, float* out, Layout ol, const float* a,
+                                                            Layout al, int dim, float start) {
+  const int fn = FN >= 0 ? FN : fn_rt;
+  __shared__ float wsum[16];
+  __shared__ int whave[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t o = blockIdx.x;
+  const int64_t len = al.shape[dim], st = al.strides[dim];
+  const int64_t base = bcast_pos<int64_t>(o, ol, al);
+  float acc = 0.f;
+  bool have = false;
+  for (int64_t j0 = threadIdx.x; j0 < len; j0 += 8 * 1024) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = a[base + min(j0 + (int64_t)u * 1024, len - 1) * st];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (j0 + (int64_t)u * 1024 >= len) break;
+      acc = have ? apply_fn(fn, acc, x[u]) : x[u];
+      have = true;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const float y = __shfl_xor(acc, off);
+    const bool hy = __shfl_xor((int)have, off) != 0;
+    if (hy) acc = have ? apply_fn(fn, acc, y) : y;
+    have = have || hy;
+  }
+  if (lane == 0) { wsum[w] = acc; whave[w] = have; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = 0.f;
+    bool hv = false;
+    for (int k = 0; k < 16; ++k) {
+      if (!whave[k]) continue;
+      v = hv ? apply_fn(fn, v, wsum[k]) : wsum[k];
+      hv = true;
+    }
+    out[out_pos<int64_t>(o, ol)] = hv ? apply_fn(fn, start, v) : start;
   }
 }
 __global__ __launch_bounds__(256) void reduce_thread_kernel(int fn, float* out, Layout ol,
@@ -890,11 +936,16 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   for (int d = reduce_dim + 1; d < dims; ++d) inner *= a_shape[d];
   for (int d = 0; d < reduce_dim; ++d) outer *= a_shape[d];
   const int64_t len = a_shape[reduce_dim];
+  // the one-pass form up to 64 MiB of input; above that the two-kernel form streams faster
+  // (4992 x 10000, 200 MB: 57 µs against 84-90 µs at 240-2048 workgroups of the one-pass form)
   if (al.contiguous && ol.contiguous && inner % 4 == 0 && inner >= 64 && len >= 16 && outer <= 65535 &&
-      ((((uintptr_t)a | (uintptr_t)out) & 15) == 0)) {
+      outer * len * inner <= ((int64_t)16 << 20) && ((((uintptr_t)a | (uintptr_t)out) & 15) == 0)) {
     // one pass: row chunks of at least 8 rows per wave, about 256 workgroups in all
     const int64_t cb = (inner + 255) / 256;
+    // about 256 workgroups, 8 rows per wave (8 beat 4, 16, 32 and 64 rows and 128 workgroups at
+    // 4992 x 256: 11.4 µs, scripts/gpu_colab.sh); fewer than 4 chunks: no fold at all
     int64_t R = std::max<int64_t>(1, std::min<int64_t>(256 / (cb * outer), len / (8 * kCol1Waves)));
+    if (R < 4) R = 1;
     int64_t chunk = (len + R - 1) / R;
     R = (len + chunk - 1) / chunk;  // every chunk holds a row
     float* part = nullptr;
@@ -936,6 +987,14 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
       hipLaunchKernelGGL(reduce_cols_fold, dim3((unsigned)((no + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                          fn, out, part, (const int*)(part + outer * R * inner), inner, (int)R, no, start);
     }
+  } else if (n <= 512 && a_shape[reduce_dim] >= 2048) {
+    const hipStream_t st = (hipStream_t)stream;
+    if (fn == FN_ADD)
+      hipLaunchKernelGGL(reduce_block_kernel<FN_ADD>, dim3((unsigned)n), dim3(1024), 0, st, fn, out, ol, a, al, reduce_dim, start);
+    else if (fn == FN_MAX)
+      hipLaunchKernelGGL(reduce_block_kernel<FN_MAX>, dim3((unsigned)n), dim3(1024), 0, st, fn, out, ol, a, al, reduce_dim, start);
+    else
+      hipLaunchKernelGGL(reduce_block_kernel<-1>, dim3((unsigned)n), dim3(1024), 0, st, fn, out, ol, a, al, reduce_dim, start);
   } else if (a_shape[reduce_dim] >= 64) {
     hipLaunchKernelGGL(reduce_wave_kernel, dim3(grid_for(n, 4)), dim3(256), 0,
                        (hipStream_t)stream, fn, out, ol, n, a, al, reduce_dim, start);
@@ -1012,13 +1071,15 @@ static bool gemm_rocblas(float* c, const float* a, const float* b, int64_t batch
   const float alpha = 1.f, beta = 0.f;
   // A long reduction into a small output (config 5's LM-head dX: 4992 x 256 over K = 10000,
   // 78 output tiles for 256 CUs) runs as S batched K slices into partials plus an ordered sum:
-  // 547 -> 197 µs at S = 8 (scripts/gemm_probe.py). Only for one matrix, K >= 8192, < 128
-  // tiles of 128 x 128, S | K, N % 4 = 0 and 16-byte aligned rows.
-  if (batch == 1 && K >= 8192 && ((M + 127) / 128) * ((N + 127) / 128) < 128 && N % 4 == 0 && scm % 4 == 0 &&
+  // 547 -> 197 µs at S = 8; the linears' 256 x 256 dW over K = 4992 (rocBLAS's own split,
+  // 17.7 µs) 15.1 µs at S = 4 (scripts/gemm_probe.py). Only for one matrix, K >= 8192 with
+  // < 128 tiles of 128 x 128 or K >= 4096 with <= 16, S | K, N % 4 = 0, 16-byte aligned rows.
+  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  if (batch == 1 && ((K >= 8192 && tiles < 128) || (K >= 4096 && tiles <= 16)) && N % 4 == 0 && scm % 4 == 0 &&
       ((uintptr_t)c & 15) == 0) {
     int S = 0;
     for (int cand : {8, 4, 2})
-      if (K % cand == 0 && K / cand >= 1024) { S = cand; break; }
+      if (K % cand == 0 && K / cand >= 1024 && (K >= 8192 || cand <= 4)) { S = cand; break; }
     float* part = S ? (float*)reduce_scratch((size_t)S * M * N * 4, st) : nullptr;
     if (part) {
       const int64_t ks = K / S;

@@ -119,5 +119,19 @@ for S in (2, 4, 5, 8, 10):
     torch.cuda.synchronize()
     out[f"dX split-K S={S}"] = {"us": round(us, 1), "TF/s": round(flop / us / 1e6, 1),
                                 "max_rel": float(((dx - refdx).abs().max() / refdx.abs().max()).item())}
+# split-K for the linears' dW (256 x 256 over K = 4992)
+for S in (2, 4, 8):
+    ks = M // S
+    part2 = torch.empty(S, E, E, device="cuda")
+
+    def fn2(S=S, ks=ks, part2=part2):
+        mmb(part2, x2t, dy2, S, E, E, ks, (ks, M, 1), (ks * E, E, 1), (E * E, E, 1))
+        torch.sum(part2, 0, out=dw2)
+    out[f"lin dW split-K S={S} (Xᵀ copy)"] = {"us": round(timed(fn2, 200), 2)}
+
+    def fn3(S=S, ks=ks, part2=part2):
+        mmb(part2, x2.t(), dy2, S, E, E, ks, (ks * E, 1, E), (ks * E, E, 1), (E * E, E, 1))
+        torch.sum(part2, 0, out=dw2)
+    out[f"lin dW split-K S={S} (X view)"] = {"us": round(timed(fn3, 200), 2)}
 out["preferred_blas"] = str(torch.backends.cuda.preferred_blas_library())
 print(json.dumps(out, indent=1))

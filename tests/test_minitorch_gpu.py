@@ -86,7 +86,8 @@ def test_zip_map_paths(mt, case):
 @pytest.mark.parametrize("shape,dim", [((4992, 256), 0), ((300, 10000), 0), ((3, 40, 70), 1),
                                        ((17, 33), 0), ((50, 64, 1), 0), ((4992, 10000), 0),
                                        ((16, 20), 0), ((3, 4096, 80), 1), ((2000, 17), 0),
-                                       ((5, 1000, 300), 1), ((4992, 4), 0), ((70, 128), 0)])
+                                       ((5, 1000, 300), 1), ((4992, 4), 0), ((70, 128), 0),
+                                       ((4992,), 0), ((3, 20000), 1), ((100000,), 0)])
 def test_reduce_paths(mt, shape, dim):
     """Sum and max over a non-innermost dim (the one-pass column kernel with arrival counters
     where the layout allows: bias gradients; the two-kernel column form; the other reduce
@@ -251,14 +252,14 @@ def test_matmul(mt, shapes, gemm_backend):
 
 
 @pytest.mark.parametrize("transposed", [False, True])
-def test_matmul_split_k(mt, transposed):
-    """A long reduction into a small output (K >= 8192, under 128 output tiles: config 5's
-    LM-head dX) runs as 8 batched K slices plus an ordered sum of the partials (combine.hip
-    gemm_rocblas); against NumPy in fp64, plain and with a transposed right operand, and
-    bitwise repeatable."""
+@pytest.mark.parametrize("M,K,N", [(300, 8192, 64), (256, 4992, 256)])
+def test_matmul_split_k(mt, transposed, M, K, N):
+    """A long reduction into a small output (K >= 8192 under 128 output tiles: config 5's
+    LM-head dX; K >= 4096 under 17 tiles: the linears' dW) runs as batched K slices plus an
+    ordered sum of the partials (combine.hip gemm_rocblas); against NumPy in fp64, plain and
+    with a transposed right operand, and bitwise repeatable."""
     minitorch, B = mt
     rng = np.random.default_rng(7)
-    M, K, N = 300, 8192, 64
     x = rng.standard_normal((M, K)).astype(np.float32)
     w = rng.standard_normal((K, N)).astype(np.float32)
     tx = minitorch.tensor_from_numpy(x, B)
