@@ -21,6 +21,7 @@ kernels take (batch, head, seq) strides, so no ``.contiguous()`` copy is made.
 from __future__ import annotations
 
 import ctypes
+import os
 import functools
 from typing import Callable, Optional
 
@@ -45,6 +46,9 @@ def _i64(vals) -> ctypes.Array:
     if type(vals) is not tuple:
         vals = tuple(int(v) for v in vals)
     return _i64_cached(vals)
+
+
+_RIGHT_T = os.environ.get("MT_RIGHT_T", "1") != "0"  # A/B switch (scripts/gpu_colab.sh)
 
 
 def _out(like: Tensor, shape) -> Tensor:
@@ -185,7 +189,12 @@ class HipKernelOps(TensorOps):
             sr, sc = t._tensor.strides[-2], t._tensor.strides[-1]
             if t._tensor.is_dense() or (sc == 1 and sr >= c):
                 return True
-            return left and Mo <= 1024 and No <= 1024 and sr == 1 and sc >= r
+            if sr != 1 or sc < r:
+                return False
+            if left:
+                return Mo <= 1024 and No <= 1024
+            # a small transposed right operand (the linears' Wᵀ in dX = dy·Wᵀ): op T, no copy
+            return _RIGHT_T and r <= 1024 and c <= 1024
 
         def lift(t: Tensor, left: bool) -> Tensor:
             # a 2-D operand as a batch of one over the same storage (a backend op: no autodiff

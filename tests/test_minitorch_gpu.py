@@ -285,6 +285,10 @@ def _matmul_case(mt, shapes):
     order[-1], order[-2] = order[-2], order[-1]
     out2 = xt.permute(*order) @ minitorch.tensor_from_numpy(w, B)
     np.testing.assert_allclose(out2.to_numpy(), ref, rtol=1e-5, atol=1e-5)
+    # transposed (strided) right operand: op T without a copy where it is small
+    wt = minitorch.tensor_from_numpy(np.ascontiguousarray(np.swapaxes(w, -1, -2)), B)
+    out_r = minitorch.tensor_from_numpy(x, B) @ wt.permute(*order)
+    np.testing.assert_allclose(out_r.to_numpy(), ref, rtol=1e-5, atol=1e-5)
     if x.ndim == 3:
         # no unit stride in either matrix dim: (M, K, batch) storage viewed as (batch, M, K)
         xs = minitorch.tensor_from_numpy(np.ascontiguousarray(np.moveaxis(x, 0, -1)), B)
