@@ -289,7 +289,7 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
                                                              int slab_off, int ws_bytes) {
   constexpr bool R3 = VAR & 16;
   constexpr bool NORED = (VAR & 1) || R3, NOARR = (VAR & 2) || R3, PLAIN = (VAR & 4) || R3, GATOM = VAR & 8;
-  constexpr bool ROT = (VAR & 32) && !CAUSAL;
+  constexpr bool ROT = VAR & 32;
   constexpr bool PKM = VAR & 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -379,12 +379,18 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
   const int step0 = qt0 / kStep;
   // a block of padding keys only (k0 >= Nk) stores zero dK / dV and no dQ partials
   const int nstep = N > qt0 && k0 < Nk ? (N - qt0 + kStep - 1) / kStep : 0;
-  // the walk: local step t covers query step step0 + sq(t); rotated only where every step is
-  // mask-free (N % 64 == 0, no padding keys in the head)
-  const int rot = ROT && N % kStep == 0 && Nk == N ? (kb * nstep) / nkb : 0;
+  // steps: [0, nhead) causal diagonal (masked), [nhead, nfull) mask-free, [nfull, nstep) tail.
+  const int nhead = k0 + kKB > Nk ? nstep : CAUSAL ? min(nstep, kKB / kStep) : 0;
+  const int nfull = min(nstep, max(nhead, (N - qt0) / kStep));
+  // the walk: local step t covers query step step0 + sq(t); rotated where the head has no
+  // padding keys and N % 64 == 0: non-causal over all steps, causal over the mask-free steps
+  // only (the diagonal steps come first, as the masked head loop needs)
+  const int nrot = nfull - nhead;
+  const int rot = ROT && N % kStep == 0 && Nk == N && nrot > 1 ? (kb * nrot) / nkb : 0;
   auto sq = [&](int t) __attribute__((always_inline)) {
+    if (rot == 0 || t < nhead || t >= nfull) return t;
     const int r = t + rot;
-    return r >= nstep ? r - nstep : r;
+    return r >= nfull ? r - nrot : r;
   };
   auto stage = [&](int t, int slot) __attribute__((always_inline)) {
     const int qs = qt0 + sq(t) * kStep + wu * kQT;
@@ -452,14 +458,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_fused_bf16(AttnArgs p, int nkb,
     publish(false);
   }
   __syncthreads();
-  // steps: [0, nhead) causal diagonal (masked), [nhead, nfull) mask-free, [nfull, nstep) tail.
   // Step t > 0 also computes the dQ strip of step t - 1 (its dS image, the other parity):
   // half its k-steps before each sub-tile. Masked sub-tiles are computed in full, also when
   // every score of the wave is masked (causal, before the wave's keys; past N): their dS is
   // then exactly zero, as the dS image needs, and a wave-level skip would be a branch around
   // the accumulators (copies and spills in the masked steps).
-  const int nhead = k0 + kKB > Nk ? nstep : CAUSAL ? min(nstep, kKB / kStep) : 0;
-  const int nfull = min(nstep, max(nhead, (N - qt0) / kStep));
 #define FSUB(MASK_, SLOT_, T_, U_)                                                       \
   {                                                                                      \
     const int qt_ = qt0 + sq(T_) * kStep + (U_) * kQT;                                   \

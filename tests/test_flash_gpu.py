@@ -504,6 +504,29 @@ def test_bf16_bwd_fused_long_vs_oracle(torch_dev, N, causal, parity_record):
                       heads=2, max_abs=e, max_err_over_bound=r)
 
 
+@pytest.mark.parametrize("N,causal", [(1000, False), (1000, True), (4001, False), (4001, True),
+                                      (600, True)])
+def test_bf16_bwd_fused_ragged_vs_oracle(torch_dev, N, causal, parity_record):
+    """The d = 64 fused backward at N % 64 != 0 with more than one key block: a walk with a
+    masked diagonal head, mask-free steps and the partial last query step (the tail, which a
+    walk order must map to itself), against the C oracle under tests/bounds.py, every output
+    finite."""
+    from minitorch import _hip
+    torch = torch_dev
+    g = torch.Generator(device="cuda").manual_seed(N + 7 * causal)
+    q, k, v, do = (torch.randn((1, 2, N, 64), device="cuda", generator=g).to(torch.bfloat16)
+                   for _ in range(4))
+    o, m, l = _hip.flash_fwd(q, k, v, causal)
+    dq, dk, dv = _hip.flash_bwd(q, k, v, o, do, m, l, causal)
+    torch.cuda.synchronize()
+    for t in (dq, dk, dv):
+        assert bool(torch.isfinite(t.float()).all())
+    res = _grad_check(q, k, v, do, (dq, dk, dv), causal, [(0, 0), (0, 1)], f"(1,2,{N},64)")
+    for name, (e, r) in res.items():
+        parity_record("test_bf16_bwd_fused_ragged_vs_oracle", f"(1,2,{N},64) causal={causal} {name}",
+                      heads=2, max_abs=e, max_err_over_bound=r)
+
+
 @pytest.mark.parametrize("shape", [(1, 2, 17, 128), (1, 2, 128, 128), (1, 2, 129, 128),
                                    (1, 3, 200, 128), (1, 1, 320, 128), (2, 2, 1000, 128),
                                    (1, 2, 2048, 128)])
