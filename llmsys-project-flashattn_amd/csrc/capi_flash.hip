@@ -12,6 +12,8 @@
 #include "fa_common.h"
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <vector>
 
 namespace mt {
 hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
@@ -214,6 +216,92 @@ static int check_sizes(int dtype, int64_t B, int64_t H, int64_t N, int64_t d) {
     return set_error("sizes out of range (N=%lld, B*H=%lld, d=%lld; d <= 4096)", (long long)N,
                      (long long)(B * H), (long long)d);
   return 0;
+}
+
+// ---- head dims between the MFMA kernels' 64 and 128 (round 5) ------------------------------
+// bf16 heads with 32 < d < 64 or 64 < d < 128 (d % 8 == 0) run the d = 64 / d = 128 kernels on
+// copies zero-padded to that width, with the scale of the real d: a zero column adds nothing to
+// Q·Kᵀ and its O, dQ, dK, dV columns are zero and dropped. (8,16,4096,96): forward 3.52 ->
+// ≈1.1 ms, backward 7.87 -> ≈3.3 ms against the generic kernels (scripts/headdim_bench.py).
+static int64_t pad_dim(int64_t d) {
+  if (d % 8) return 0;
+  return (d > 32 && d < 64) ? 64 : (d > 64 && d < 128) ? 128 : 0;
+}
+// The padded copies live in one library buffer per (device, stream), grown on demand and never
+// freed while the process runs (an outgrown buffer is retired: a captured hipGraph keeps the
+// address it was captured with); nothing is allocated inside a stream capture.
+static void* pad_scratch(size_t bytes, hipStream_t st) {
+  struct Slot { int dev; hipStream_t st; void* buf; size_t cap; };
+  static std::mutex mu;
+  static Slot slots[64] = {};
+  static int nslots = 0;
+  static std::vector<void*> retired;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  Slot* sl = nullptr;
+  for (int i = 0; i < nslots && !sl; ++i)
+    if (slots[i].dev == dev && slots[i].st == st) sl = &slots[i];
+  if (!sl) {
+    if (nslots == 64) return nullptr;
+    sl = &slots[nslots++];
+    *sl = Slot{dev, st, nullptr, 0};
+  }
+  if (sl->cap < bytes) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    void* nb = nullptr;
+    if (hipMalloc(&nb, bytes) != hipSuccess) return nullptr;
+    if (sl->buf) retired.push_back(sl->buf);
+    sl->buf = nb;
+    sl->cap = bytes;
+  }
+  return sl->buf;
+}
+// dst [rows][dp] bf16 (contiguous) <- src rows (b, h, n) at element strides s[3], d columns, the
+// rest zero; one 16-B chunk per thread
+__global__ __launch_bounds__(256) void pad_rows_kernel(uint4* __restrict__ dst, const char* __restrict__ src,
+                                                       int64_t rows, int64_t H, int64_t N, int64_t s0,
+                                                       int64_t s1, int64_t s2, int dchunks, int pchunks) {
+  const int64_t n = rows * pchunks, step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += step) {
+    const int64_t row = t / pchunks;
+    const int c = (int)(t - row * pchunks);
+    const int64_t bh = row / N, r = row - bh * N;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (c < dchunks)
+      v = *(const uint4*)(src + ((bh / H) * s0 + (bh % H) * s1 + r * s2) * 2 + (int64_t)c * 16);
+    dst[t] = v;
+  }
+}
+// dst rows (b, h, n) at element strides s[3] (element size es) <- the first dchunks 16-B chunks of
+// src's contiguous [rows][pchunks] rows
+__global__ __launch_bounds__(256) void unpad_rows_kernel(char* __restrict__ dst, const uint4* __restrict__ src,
+                                                         int64_t rows, int64_t H, int64_t N, int64_t s0,
+                                                         int64_t s1, int64_t s2, int es, int dchunks,
+                                                         int pchunks) {
+  const int64_t n = rows * dchunks, step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += step) {
+    const int64_t row = t / dchunks;
+    const int c = (int)(t - row * dchunks);
+    const int64_t bh = row / N, r = row - bh * N;
+    *(uint4*)(dst + ((bh / H) * s0 + (bh % H) * s1 + r * s2) * es + (int64_t)c * 16) = src[row * pchunks + c];
+  }
+}
+static unsigned pad_grid(int64_t n) { return (unsigned)std::min<int64_t>((n + 255) / 256, 8192); }
+static hipError_t pad_rows(void* dst, const void* src, const int64_t s[3], int64_t B, int64_t H, int64_t N,
+                           int64_t d, int64_t dp, hipStream_t st) {
+  const int64_t rows = B * H * N;
+  hipLaunchKernelGGL(pad_rows_kernel, dim3(pad_grid(rows * (dp / 8))), dim3(256), 0, st, (uint4*)dst,
+                     (const char*)src, rows, H, N, s[0], s[1], s[2], (int)(d / 8), (int)(dp / 8));
+  return hipGetLastError();
+}
+static hipError_t unpad_rows(void* dst, const void* src, const int64_t s[3], int es, int64_t B, int64_t H,
+                             int64_t N, int64_t d, int64_t dp, hipStream_t st) {
+  const int64_t rows = B * H * N, dch = d * es / 16;
+  hipLaunchKernelGGL(unpad_rows_kernel, dim3(pad_grid(rows * dch)), dim3(256), 0, st, (char*)dst,
+                     (const uint4*)src, rows, H, N, s[0], s[1], s[2], es, (int)dch, (int)(dp * es / 16));
+  return hipGetLastError();
 }
 
 #ifdef MT_DIAGNOSTICS
@@ -550,6 +638,26 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
   // key padding (kv_len): the generic / ring kernels, which mask keys >= kv_len[b] (the
   // bf16 d = 64 / 128 MFMA schedules have no per-row key bound)
   if (dtype == MT_BF16 && vec && pol != kPolGeneric && !kv_len) {
+    const int64_t dp = pad_dim(d);
+    if (dp) {  // the d = 64 / 128 kernels on zero-padded copies (pad_dim)
+      const int64_t nel = B * H * N * dp, oes = f32o ? 4 : 2;
+      char* buf = (char*)pad_scratch((size_t)(nel * (3 * 2 + oes)), st);
+      if (buf) {
+        AttnArgs ap = a;
+        ap.q = buf; ap.k = buf + nel * 2; ap.v = buf + nel * 4; ap.out = buf + nel * 6;
+        int64_t* ps[4] = {ap.sq, ap.sk, ap.sv, ap.so};
+        for (int i = 0; i < 4; ++i) fill_strides(ps[i], nullptr, H, N, dp);
+        ap.d = (int)dp;  // the scale stays the real d's
+        hipError_t e = pad_rows((void*)ap.q, q, a.sq, B, H, N, d, dp, st);
+        if (e == hipSuccess) e = pad_rows((void*)ap.k, k, a.sk, B, H, N, d, dp, st);
+        if (e == hipSuccess) e = pad_rows((void*)ap.v, v, a.sv, B, H, N, d, dp, st);
+        bool handled = false;
+        if (e == hipSuccess) e = fwd_bf16_dispatch(ap, causal != 0, pol, st, &handled);
+        if (e == hipSuccess && !handled) return set_error("mt_flash_attn_fwd: no kernel for the padded d = %lld", (long long)dp);
+        if (e == hipSuccess) e = unpad_rows(o, ap.out, a.so, (int)oes, B, H, N, d, dp, st);
+        return check_hip(e, "mt_flash_attn_fwd(bf16, padded d)");
+      }
+    }
     bool handled = false;
     const hipError_t e = fwd_bf16_dispatch(a, causal != 0, pol, st, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_fwd(bf16)");
@@ -584,7 +692,9 @@ static int64_t bwd_rows_bytes(int64_t B, int64_t H, int64_t N) {
 }
 
 int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t d) {
-  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(B, H, N, d) ? bwd_fused_ws_bytes(B, H, N) : 0);
+  // a padded head dim (pad_dim) runs the kernels of its padded width
+  const int64_t de = pad_dim(d) ? pad_dim(d) : d;
+  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(B, H, N, de) ? bwd_fused_ws_bytes(B, H, N) : 0);
 }
 
 static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void* k, const void* v,
@@ -644,6 +754,40 @@ static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void*
   const bool vec = vec_ok(d, es, {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv},
                           {q, k, v, o, dout, dq, dk, dv});
   const int pol = g_kernel_policy.load(std::memory_order_relaxed);
+  const int64_t dp = pad_dim(d);
+  if (dtype == MT_BF16 && vec && pol != kPolGeneric && !kv_len && dp) {
+    // the d = 64 / 128 backward on zero-padded copies (pad_dim): Q, K, V, O, dO in, dQ, dK, dV
+    // out; the fused slab only where a checked caller's workspace holds it
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t nel = B * H * N * dp;
+    char* buf = (char*)pad_scratch((size_t)(nel * 2 * 8), st);
+    if (buf) {
+      AttnArgs ap = a;
+      const void** in[5] = {&ap.q, &ap.k, &ap.v, &ap.o, &ap.dout};
+      const void* src[5] = {q, k, v, o, dout};
+      const int64_t* ss[5] = {a.sq, a.sk, a.sv, a.so, a.sdo};
+      hipError_t e = hipSuccess;
+      for (int i = 0; i < 5 && e == hipSuccess; ++i) {
+        *in[i] = buf + i * nel * 2;
+        e = pad_rows((void*)*in[i], src[i], ss[i], B, H, N, d, dp, st);
+      }
+      ap.dq = buf + 5 * nel * 2; ap.dk = buf + 6 * nel * 2; ap.dv = buf + 7 * nel * 2;
+      int64_t* ps[8] = {ap.sq, ap.sk, ap.sv, ap.so, ap.sdo, ap.sdq, ap.sdk, ap.sdv};
+      for (int i = 0; i < 8; ++i) fill_strides(ps[i], nullptr, H, N, dp);
+      ap.d = (int)dp;
+      ap.slab = fused_bwd_applies(B, H, N, dp) && checked ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
+      bool handled = false;
+      if (e == hipSuccess) {
+        const int split = !causal ? 5 : (int64_t)((N + 255) / 256) * a.B * a.H >= 512 ? 18 : 0;
+        e = launch_bwd_bf16(ap, causal != 0, ap.slab && kFusedBwdDefault ? 20 : split, st, &handled);
+      }
+      if (e == hipSuccess && !handled) return set_error("mt_flash_attn_bwd: no kernel for the padded d = %lld", (long long)dp);
+      if (e == hipSuccess) e = unpad_rows(dq, ap.dq, a.sdq, 2, B, H, N, d, dp, st);
+      if (e == hipSuccess) e = unpad_rows(dk, ap.dk, a.sdk, 2, B, H, N, d, dp, st);
+      if (e == hipSuccess) e = unpad_rows(dv, ap.dv, a.sdv, 2, B, H, N, d, dp, st);
+      return check_hip(e, "mt_flash_attn_bwd(bf16, padded d)");
+    }
+  }
   // key padding (kv_len): the fused bf16 d = 64 kernel or the generic / ring kernels, which
   // mask keys >= kv_len[b] (the split bf16 kernels do not: policy 121 with kv_len runs the
   // generic kernels)

@@ -141,6 +141,35 @@ def test_random_fwd_bwd(torch_dev, B, H, N, d, causal, dtype):
         np.testing.assert_allclose(_np(got), ref, atol=atol["g"] * scale, rtol=0, err_msg=name)
 
 
+@pytest.mark.parametrize("d,causal", [(40, False), (48, True), (56, False), (72, True), (80, False),
+                                      (96, True), (96, False), (120, True)])
+def test_bf16_padded_head_dims(torch_dev, d, causal):
+    """bf16 head dims between the MFMA kernels' widths (32 < d < 64, 64 < d < 128) run the d = 64 /
+    128 kernels on zero-padded copies with the real d's scale (capi_flash.hip pad_dim): forward
+    O (bf16 and fp32 output), (m, l) and all three gradients against the oracle, on strided
+    views (the padding copies read the caller's strides), N ragged."""
+    from minitorch import _hip
+    torch = torch_dev
+    B, H, N = 2, 3, 333
+    rng = np.random.default_rng(d + 3 * causal)
+    q, k, v, do = (A.bf16_round(rng.standard_normal((B, H, N, d)).astype(np.float32)) for _ in range(4))
+    o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
+    dq_ref, dk_ref, dv_ref = A.attention_bwd(q, k, v, o_ref, do, m_ref, l_ref, causal)
+    # [B, N, H, d] storage viewed as [B, H, N, d]
+    tq, tk, tv, tdo = (_dev(torch, np.ascontiguousarray(x.transpose(0, 2, 1, 3)), torch.bfloat16).permute(0, 2, 1, 3)
+                       for x in (q, k, v, do))
+    o, m, l = _hip.flash_fwd(tq, tk, tv, causal)
+    o32, _, _ = _hip.flash_fwd(tq, tk, tv, causal, out_dtype=torch.float32)
+    dq, dk, dv = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, causal)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(o), o_ref, atol=2e-2, rtol=0)
+    np.testing.assert_allclose(_np(o32), o_ref, atol=4e-3, rtol=0)
+    _check_ml(_np(m), _np(l), m_ref, l_ref, exact=False)
+    scale = max(1.0, float(np.abs(dq_ref).max()), float(np.abs(dk_ref).max()), float(np.abs(dv_ref).max()))
+    for got, ref, name in ((dq, dq_ref, "dq"), (dk, dk_ref, "dk"), (dv, dv_ref, "dv")):
+        np.testing.assert_allclose(_np(got), ref, atol=6e-2 * scale, rtol=0, err_msg=name)
+
+
 def test_strided_views(torch_dev):
     """Q/K/V as permuted views of [B, N, H, d] projections (what MultiHeadAttention
     hands over, reference modules_transfomer.py:88-100): no host-side copy needed."""
