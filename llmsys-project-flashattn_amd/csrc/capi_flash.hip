@@ -227,37 +227,8 @@ static int64_t pad_dim(int64_t d) {
   if (d % 8) return 0;
   return (d > 32 && d < 64) ? 64 : (d > 64 && d < 128) ? 128 : 0;
 }
-// The padded copies live in one library buffer per (device, stream), grown on demand and never
-// freed while the process runs (an outgrown buffer is retired: a captured hipGraph keeps the
-// address it was captured with); nothing is allocated inside a stream capture.
-static void* pad_scratch(size_t bytes, hipStream_t st) {
-  struct Slot { int dev; hipStream_t st; void* buf; size_t cap; };
-  static std::mutex mu;
-  static Slot slots[64] = {};
-  static int nslots = 0;
-  static std::vector<void*> retired;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  Slot* sl = nullptr;
-  for (int i = 0; i < nslots && !sl; ++i)
-    if (slots[i].dev == dev && slots[i].st == st) sl = &slots[i];
-  if (!sl) {
-    if (nslots == 64) return nullptr;
-    sl = &slots[nslots++];
-    *sl = Slot{dev, st, nullptr, 0};
-  }
-  if (sl->cap < bytes) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    void* nb = nullptr;
-    if (hipMalloc(&nb, bytes) != hipSuccess) return nullptr;
-    if (sl->buf) retired.push_back(sl->buf);
-    sl->buf = nb;
-    sl->cap = bytes;
-  }
-  return sl->buf;
-}
+// the padded copies: the library's kScratchPad buffer of the stream (stream_scratch, fa_common.h)
+static void* pad_scratch(size_t bytes, hipStream_t st) { return stream_scratch(kScratchPad, bytes, st); }
 // dst [rows][dp] bf16 (contiguous) <- src rows (b, h, n) at element strides s[3], d columns, the
 // rest zero; one 16-B chunk per thread
 __global__ __launch_bounds__(256) void pad_rows_kernel(uint4* __restrict__ dst, const char* __restrict__ src,

@@ -453,16 +453,10 @@ __global__ __launch_bounds__(512) void reduce_cols1_kernel(int fn_rt, float* __r
   }
 }
 
-// The partial buffer of the column reductions and split-K GEMMs, one per (device, stream):
-// grown on demand and kept, so the users of one stream reuse it in that stream's order, and
-// users on two streams (or two host threads on two streams) never share partials. A buffer
-// that is outgrown is retired, not freed: a captured hipGraph (minitorch/graphs.py) keeps the
-// address it was captured with, and an eager call that grows the buffer afterwards must not
-// pull the memory from under its replays.
-static void* reduce_scratch(size_t bytes, hipStream_t st) {
-  struct Slot { int dev; hipStream_t st; void* buf; size_t cap; };
+void* stream_scratch(int pool, size_t bytes, hipStream_t st) {
+  struct Slot { int pool; int dev; hipStream_t st; void* buf; size_t cap; };
   static std::mutex mu;
-  static Slot slots[64] = {};
+  static Slot slots[128] = {};
   static int nslots = 0;
   static std::vector<void*> retired;
   int dev = 0;
@@ -470,15 +464,14 @@ static void* reduce_scratch(size_t bytes, hipStream_t st) {
   std::lock_guard<std::mutex> lock(mu);
   Slot* s = nullptr;
   for (int i = 0; i < nslots && !s; ++i)
-    if (slots[i].dev == dev && slots[i].st == st) s = &slots[i];
+    if (slots[i].pool == pool && slots[i].dev == dev && slots[i].st == st) s = &slots[i];
   if (!s) {
-    if (nslots == 64) return nullptr;  // the caller then reduces without row chunks
+    if (nslots == 128) return nullptr;  // the caller then takes its path without scratch
     s = &slots[nslots++];
-    *s = Slot{dev, st, nullptr, 0};
+    *s = Slot{pool, dev, st, nullptr, 0};
   }
   if (s->cap < bytes) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    // no allocation inside a capture: the caller then takes its unchunked path
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
     void* nb = nullptr;
     bytes = std::max(bytes, 2 * s->cap);
@@ -489,6 +482,7 @@ static void* reduce_scratch(size_t bytes, hipStream_t st) {
   }
   return s->buf;
 }
+static void* reduce_scratch(size_t bytes, hipStream_t st) { return stream_scratch(kScratchReduce, bytes, st); }
 
 // Arrival counters of the one-pass column reduction, one zeroed block per (device, stream),
 // allocated once outside any capture; each launch's last arrivals reset the counters they used.

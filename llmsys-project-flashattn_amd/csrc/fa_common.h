@@ -225,4 +225,14 @@ __device__ __forceinline__ void store4(const ORow& o, int col, float x, float y,
   else store4((bf16*)o.p + col, x, y, z, w, true);
 }
 
+// A device buffer per (pool, device, stream), grown on demand and never freed while the process
+// runs: an outgrown buffer is retired, because a captured hipGraph (minitorch/graphs.py) keeps
+// the address it was captured with. Its users on one stream share it in that stream's order;
+// two streams never share one. Returns nullptr when it would have to grow inside a stream
+// capture (the caller then takes a path without it). Pools: kScratchReduce (column-reduction
+// partials, split-K GEMM partials; combine.hip), kScratchPad (zero-padded head-dim copies;
+// capi_flash.hip). Defined in combine.hip.
+enum { kScratchReduce = 0, kScratchPad = 1 };
+void* stream_scratch(int pool, size_t bytes, hipStream_t st);
+
 }  // namespace mt
