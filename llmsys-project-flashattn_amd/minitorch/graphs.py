@@ -39,6 +39,18 @@ def capturing() -> Optional["StepGraph"]:
     return _CAPTURING
 
 
+def copy_into(t, array) -> None:
+    """Copy host data into the device storage of a minitorch tensor in place (same element
+    count), on torch's current stream: how a captured step's fixed inputs take the next batch
+    before ``replay()``. (A pageable host-to-device copy: the host waits for it.)"""
+    import torch
+    src = torch.as_tensor(np.ascontiguousarray(array, dtype=np.float32).reshape(-1))
+    dst = t._tensor._storage
+    if not isinstance(dst, torch.Tensor) or dst.numel() != src.numel() or not t._tensor.is_dense():
+        raise ValueError("copy_into needs a dense device tensor of the array's size")
+    dst.copy_(src)
+
+
 class StepGraph:
     """Capture ``step_fn`` (a no-argument callable: forward, backward, optimizer step) once
     and replay it. ``warmup`` eager calls run first, on the capture stream."""

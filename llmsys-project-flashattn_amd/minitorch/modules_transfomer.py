@@ -28,6 +28,11 @@ _INDEX_CACHE: dict = {}
 
 
 def _kv_tensor(kv_len, batch_size: int, backend):
+    from .tensor import Tensor
+    if isinstance(kv_len, Tensor):  # already a device tensor (e.g. a graph-captured step's fixed input)
+        if kv_len.size != batch_size:
+            raise ValueError(f"kv_len has {kv_len.size} entries for a batch of {batch_size}")
+        return kv_len
     a = np.ascontiguousarray(np.asarray(kv_len, dtype=datatype).reshape(batch_size))
     key = ("kv", id(backend), a.tobytes())
     t = _INDEX_CACHE.get(key)

@@ -85,6 +85,64 @@ def test_step_graph_matches_eager_bitwise(p_dropout):
         np.testing.assert_array_equal(a, b)
 
 
+def test_step_graph_new_batches_match_eager():
+    """Replays fed a new batch each time through copy_into (tokens, labels, loss weights and a
+    device kv_len tensor in fixed buffers) match eager steps over the same batch sequence bit for
+    bit: losses, parameters and Adam moments."""
+    import torch
+    assert torch.cuda.is_available(), "needs an MI355X"
+    import minitorch
+    from minitorch.graphs import StepGraph, copy_into
+    backend = minitorch.TensorBackend(minitorch.HipKernelOps)
+    B, T, V, E, H = 8, 24, 300, 64, 4
+    rng = np.random.default_rng(3)
+    batches = []
+    for _ in range(5):
+        tok = rng.integers(0, V, size=(B, T + 1)).astype(np.float32)
+        kv = rng.integers(T // 3, T + 1, size=B).astype(np.float32)
+        w = (np.arange(T)[None, :] < kv[:, None]).astype(np.float32)
+        batches.append((tok[:, :-1].copy(), tok[:, 1:].reshape(-1).copy(), w.reshape(-1).copy(), kv))
+
+    def make():
+        np.random.seed(0)
+        lm = minitorch.DecoderLM(n_vocab=V, n_embd=E, n_head=H, n_positions=T + 1, p_dropout=0.1,
+                                 backend=backend, use_fused_kernel=True, use_flash_attention=True)
+        opt = minitorch.Adam(lm.parameters(), lr=1e-3)
+        bufs = [minitorch.tensor_from_numpy(a, backend) for a in batches[0]]
+        x, y, wt, kvt = bufs
+
+        def step():
+            opt.zero_grad()
+            loss = (minitorch.softmax_loss(lm(x, kv_len=kvt).view(B * T, V), y) * wt).sum() / wt.sum()
+            loss.backward()
+            opt.step()
+            return loss
+        return lm, opt, bufs, step
+
+    lm_e, opt_e, bufs_e, step_e = make()
+    np.random.seed(7)
+    eager = []
+    for i in [0, 0, 1, 2, 3, 4]:
+        for t, a in zip(bufs_e, batches[i]):
+            copy_into(t, a)
+        eager.append(float(step_e().to_numpy()[0]))
+    torch.cuda.synchronize()
+
+    lm_g, opt_g, bufs_g, step_g = make()
+    np.random.seed(7)
+    g = StepGraph(step_g, warmup=2)
+    graph = []
+    for i in [1, 2, 3, 4]:
+        for t, a in zip(bufs_g, batches[i]):
+            copy_into(t, a)
+        loss = g.replay()
+        torch.cuda.synchronize()
+        graph.append(float(loss.to_numpy()[0]))
+    assert graph == eager[2:], (graph, eager)
+    for a, b in zip(_state(lm_e, opt_e), _state(lm_g, opt_g)):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_step_graph_fails_loudly_on_host_sync():
     """A step that needs the host inside it (a device value read back) cannot be captured:
     the capture raises instead of recording a step that would replay wrong."""
