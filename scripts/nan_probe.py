@@ -8,7 +8,7 @@ import torch
 from minitorch import _hip
 g = torch.Generator(device="cuda").manual_seed(5)
 shapes = []
-for d in (64, 128):
+for d in (48, 64, 96, 128):
     for N in (65, 127, 255, 257, 511, 513, 1000, 1023, 1025, 2049, 4001):
         for causal in (False, True):
             shapes.append(((2, 3, N, d), causal, None))
