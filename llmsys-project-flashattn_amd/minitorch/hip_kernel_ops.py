@@ -204,6 +204,21 @@ class HipKernelOps(TensorOps):
             st = t._tensor.strides
             return _wrap(t._tensor._storage, (1,) + tuple(t.shape), t.backend, (t.size,) + tuple(st))
 
+        if both_2d:
+            # the common case (every Linear): no batch, no lifted views, one output tensor
+            if not gemm_ready(a, True):
+                a = a.contiguous()
+            if not gemm_ready(b, False):
+                b = b.contiguous()
+            M, K = a.shape
+            K2, N = b.shape
+            assert K == K2, f"matmul shape mismatch {a.shape} @ {b.shape}"
+            out = _out(a, (M, N))
+            sa, sb = a._tensor.strides, b._tensor.strides
+            _hip.check(_hip.lib().mt_matmul_f32(_ptr(out), _ptr(a), _ptr(b), 1, M, N, K,
+                                                _i64((M * K, sa[0], sa[1])), _i64((K * N, sb[0], sb[1])),
+                                                _i64((M * N, N, 1)), _stream()), "matmul")
+            return out
         if a.dims == 2:
             a = lift(a, True)
         if b.dims == 2:

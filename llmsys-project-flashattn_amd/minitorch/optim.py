@@ -14,6 +14,7 @@ from __future__ import annotations
 import math
 from typing import Sequence
 
+from . import graphs as _graphs
 from .module import Parameter
 
 
@@ -45,8 +46,7 @@ class Adam(Optimizer):
         self._states = {id(p): {} for p in parameters}
 
     def step(self) -> None:
-        from .graphs import capturing
-        g = capturing()
+        g = _graphs.capturing()
         fused = {}  # step count -> [(param, grad, state)]
         for p in self.parameters:
             grad = getattr(p.value, "grad", None) if p.value is not None else None

@@ -98,10 +98,13 @@ class TensorData:
     def __init__(self, storage, shape: UserShape, strides: Optional[UserStrides] = None):
         if isinstance(storage, np.ndarray):
             self._storage = np.ascontiguousarray(storage, dtype=datatype).reshape(-1)
+            self._on_dev = False
         elif isinstance(storage, (list, tuple)):
             self._storage = np.array(storage, dtype=datatype).reshape(-1)
+            self._on_dev = False
         else:  # device storage (torch tensor)
             self._storage = storage
+            self._on_dev = True
         shape = tuple(map(int, shape))
         strides = _strides_from_shape(shape) if strides is None else tuple(map(int, strides))
         if len(strides) != len(shape):
@@ -130,12 +133,15 @@ class TensorData:
     # ---- placement --------------------------------------------------------------
     @property
     def on_device(self) -> bool:
-        return _is_device(self._storage)
+        # kept beside the storage (set where the storage is): this is asked thousands of
+        # times per model step (host time of the config-5 step)
+        return self._on_dev
 
     def to_cuda_(self) -> None:
-        if not self.on_device:
+        if not self._on_dev:
             import torch
             self._storage = torch.from_numpy(self._storage).to("cuda", non_blocking=False)
+            self._on_dev = True
 
     def data_ptr(self) -> int:
         if not self.on_device:

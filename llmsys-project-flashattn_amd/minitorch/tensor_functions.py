@@ -23,6 +23,9 @@ def wrap_tuple(x: Any) -> tuple:
     return x if isinstance(x, tuple) else (x,)
 
 
+_History = _Tensor = None  # tensor.History / tensor.Tensor, bound on the first Function.apply
+
+
 class Function:
     @classmethod
     def _backward(cls, ctx: Context, grad_out) -> tuple:
@@ -34,7 +37,10 @@ class Function:
 
     @classmethod
     def apply(cls, *vals):
-        from .tensor import History, Tensor
+        global _History, _Tensor
+        if _Tensor is None:  # bound once (tensor.py imports this module; an import per call was host time)
+            from .tensor import History as _History, Tensor as _Tensor  # noqa: F811
+        History, Tensor = _History, _Tensor
         raw_vals = []
         need_grad = False
         for v in vals:
@@ -308,8 +314,8 @@ class DropoutMask(Function):
     def forward(ctx, x, p):
         rate = float(p.item())
         scale = float(np.float32(1.0) / np.float32(1.0 - rate))
-        from .graphs import capturing
-        g = capturing()
+        from . import graphs
+        g = graphs.capturing()
         if g is not None:
             # a captured step (graphs.StepGraph): the seed lives in a device slot that each
             # replay refills with this same draw, and the kernels read it from there
@@ -332,15 +338,13 @@ class View(Function):
         if not a._tensor.is_dense():
             raise AssertionError("Must be contiguous to view")
         shape2 = [int(shape[i]) for i in range(shape.size)]
-        from .tensor import Tensor
-        return Tensor.make(a._tensor._storage, tuple(shape2), backend=a.backend)
+        return _Tensor.make(a._tensor._storage, tuple(shape2), backend=a.backend)
 
     @staticmethod
     def backward(ctx, grad_output):
         (original,) = ctx.saved_values
-        from .tensor import Tensor
         g = grad_output if grad_output._tensor.is_dense() else grad_output.contiguous()
-        return Tensor.make(g._tensor._storage, original, backend=g.backend), 0.0
+        return _Tensor.make(g._tensor._storage, original, backend=g.backend), 0.0
 
 
 class Copy(Function):

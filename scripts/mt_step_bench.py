@@ -12,8 +12,9 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "llmsys-project-flashattn_amd"))
 sys.path.insert(0, ROOT)
+# MT_PKG_ROOT: another copy of the package (A/B of host-side changes)
+sys.path.insert(0, os.environ.get("MT_PKG_ROOT") or os.path.join(ROOT, "llmsys-project-flashattn_amd"))
 import numpy as np
 import torch
 
