@@ -51,11 +51,17 @@ def _i64(vals) -> ctypes.Array:
 _RIGHT_T = os.environ.get("MT_RIGHT_T", "1") != "0"  # A/B switch (scripts/gpu_colab.sh)
 
 
+_torch_mod = None
+
+
 def _out(like: Tensor, shape) -> Tensor:
     """Uninitialised dense fp32 device output (every kernel below writes all of it)."""
-    import torch
+    global _torch_mod
+    if _torch_mod is None:
+        import torch
+        _torch_mod = torch
     shape = tuple(map(int, shape))
-    st = torch.empty(_prod(shape), dtype=torch.float32, device="cuda")
+    st = _torch_mod.empty(_prod(shape), dtype=_torch_mod.float32, device="cuda")
     return Tensor(TensorData(st, shape), backend=like.backend)
 
 

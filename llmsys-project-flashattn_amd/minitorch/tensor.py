@@ -48,8 +48,16 @@ class Tensor:
         self.history = back
         self.backend = backend
         self.grad: Optional[Tensor] = None
-        self.name = name if name is not None else str(self.unique_id)
+        self._name = name  # None: the unique id, formatted on first use (name)
         self.f = backend
+
+    @property
+    def name(self) -> str:
+        return self._name if self._name is not None else str(self.unique_id)
+
+    @name.setter
+    def name(self, value: str) -> None:
+        self._name = value
 
     # ---- grad flags ------------------------------------------------------------------
     def requires_grad_(self, x: bool) -> None:
