@@ -114,7 +114,25 @@ def lib() -> ctypes.CDLL:
             fn.restype = res
             fn.argtypes = args
         _lib = l
+        _bind_fast(l)
     return _lib
+
+
+fast = None  # the _mtfast extension bound to the loaded library (None: the ops use ctypes)
+
+
+def _bind_fast(l: ctypes.CDLL) -> None:
+    """Hand the generic entry points' addresses of the loaded library to the _mtfast CPython
+    extension (csrc/mtfast.c: tuples in, no ctypes marshalling), when it was built."""
+    global fast
+    try:
+        from . import _mtfast
+    except ImportError:
+        fast = None
+        return
+    addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+    _mtfast.bind(addr(l.mt_tensor_map), addr(l.mt_tensor_zip), addr(l.mt_tensor_reduce), addr(l.mt_matmul_f32))
+    fast = _mtfast
 
 
 def use_library(path: str) -> ctypes.CDLL:

@@ -126,7 +126,12 @@ class HipKernelOps(TensorOps):
         def ret(a: Tensor, out: Optional[Tensor] = None) -> Tensor:
             if out is None:
                 out = _out(a, a.shape)
-            _hip.check(_hip.lib().mt_tensor_map(
+            L = _hip.lib()
+            if _hip.fast is not None:
+                _hip.check(_hip.fast.map(fid, _ptr(out), out.shape, out._tensor.strides, _ptr(a), a.shape,
+                                         a._tensor.strides, _stream()), "map")
+                return out
+            _hip.check(L.mt_tensor_map(
                 fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides), out.dims,
                 _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims, _stream()), "map")
             return out
@@ -138,7 +143,12 @@ class HipKernelOps(TensorOps):
         fid = _fn_id(fn)
 
         def ret(a: Tensor, out: Tensor) -> Tensor:
-            _hip.check(_hip.lib().mt_tensor_map(
+            L = _hip.lib()
+            if _hip.fast is not None:
+                _hip.check(_hip.fast.map(fid, _ptr(out), out.shape, out._tensor.strides, _ptr(a), a.shape,
+                                         a._tensor.strides, _stream()), "cmap")
+                return out
+            _hip.check(L.mt_tensor_map(
                 fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides), out.dims,
                 _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims, _stream()), "cmap")
             return out
@@ -152,7 +162,12 @@ class HipKernelOps(TensorOps):
         def ret(a: Tensor, b: Tensor) -> Tensor:
             shape = shape_broadcast(a.shape, b.shape)
             out = _out(a, shape)
-            _hip.check(_hip.lib().mt_tensor_zip(
+            L = _hip.lib()
+            if _hip.fast is not None:
+                _hip.check(_hip.fast.zip(fid, _ptr(out), out.shape, out._tensor.strides, _ptr(a), a.shape,
+                                         a._tensor.strides, _ptr(b), b.shape, b._tensor.strides, _stream()), "zip")
+                return out
+            _hip.check(L.mt_tensor_zip(
                 fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides), out.dims,
                 _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims,
                 _ptr(b), _i64(b.shape), _i64(b._tensor.strides), b.dims, _stream()), "zip")
@@ -168,7 +183,12 @@ class HipKernelOps(TensorOps):
             shape = list(a.shape)
             shape[dim] = 1
             out = _out(a, shape)
-            _hip.check(_hip.lib().mt_tensor_reduce(
+            L = _hip.lib()
+            if _hip.fast is not None:
+                _hip.check(_hip.fast.reduce(fid, _ptr(out), out.shape, out._tensor.strides, _ptr(a), a.shape,
+                                            a._tensor.strides, int(dim), float(start), _stream()), "reduce")
+                return out
+            _hip.check(L.mt_tensor_reduce(
                 fid, _ptr(out), _i64(out.shape), _i64(out._tensor.strides),
                 _ptr(a), _i64(a.shape), _i64(a._tensor.strides), a.dims, int(dim),
                 ctypes.c_float(start), _stream()), "reduce")
@@ -221,7 +241,12 @@ class HipKernelOps(TensorOps):
             assert K == K2, f"matmul shape mismatch {a.shape} @ {b.shape}"
             out = _out(a, (M, N))
             sa, sb = a._tensor.strides, b._tensor.strides
-            _hip.check(_hip.lib().mt_matmul_f32(_ptr(out), _ptr(a), _ptr(b), 1, M, N, K,
+            L = _hip.lib()
+            if _hip.fast is not None:
+                _hip.check(_hip.fast.matmul(_ptr(out), _ptr(a), _ptr(b), 1, M, N, K, (M * K, sa[0], sa[1]),
+                                            (K * N, sb[0], sb[1]), (M * N, N, 1), _stream()), "matmul")
+                return out
+            _hip.check(L.mt_matmul_f32(_ptr(out), _ptr(a), _ptr(b), 1, M, N, K,
                                                 _i64((M * K, sa[0], sa[1])), _i64((K * N, sb[0], sb[1])),
                                                 _i64((M * N, N, 1)), _stream()), "matmul")
             return out
@@ -254,8 +279,12 @@ class HipKernelOps(TensorOps):
         b, sb = batch_view(b)
         out = _out(a, lead + (M, N))
         so = (M * N, N, 1)
-        _hip.check(_hip.lib().mt_matmul_f32(_ptr(out), _ptr(a), _ptr(b), batch, M, N, K,
-                                            _i64(sa), _i64(sb), _i64(so), _stream()), "matmul")
+        if _hip.lib() is not None and _hip.fast is not None:
+            _hip.check(_hip.fast.matmul(_ptr(out), _ptr(a), _ptr(b), batch, M, N, K, tuple(map(int, sa)),
+                                        tuple(map(int, sb)), so, _stream()), "matmul")
+        else:
+            _hip.check(_hip.lib().mt_matmul_f32(_ptr(out), _ptr(a), _ptr(b), batch, M, N, K,
+                                                _i64(sa), _i64(sb), _i64(so), _stream()), "matmul")
         if both_2d:
             return _wrap(out._tensor._storage, (M, N), out.backend)
         return out

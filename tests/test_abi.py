@@ -156,3 +156,21 @@ def test_product_library_has_no_ablation_kernels():
     syms = subprocess.run(["nm", "-C", "-D", "--defined-only", _hip.LIB_PATH], capture_output=True,
                           text=True).stdout
     assert "launch_fwd_v4_ablation" not in syms
+
+
+def test_mtfast_extension_bound_and_checks_arguments():
+    """The _mtfast CPython extension (csrc/mtfast.c) is built beside the package, bound to the
+    loaded library's entry points at load, and rejects malformed arguments before any call
+    (no GPU needed: nothing below reaches the library)."""
+    from minitorch import _hip
+    _hip.lib()
+    assert _hip.fast is not None, "minitorch/_mtfast*.so missing: make -C llmsys-project-flashattn_amd"
+    f = _hip.fast
+    with pytest.raises(TypeError):
+        f.map(1, 0, [4], (1,), 0, (4,), (1,), 0)          # a list where a tuple belongs
+    with pytest.raises(TypeError):
+        f.zip(1, 0, (4,), (1,))                            # wrong arity
+    with pytest.raises(ValueError):
+        f.map(1, 0, tuple(range(17)), (1,), 0, (4,), (1,), 0)  # more than 16 dims
+    with pytest.raises(ValueError):
+        f.matmul(0, 0, 0, 1, 2, 2, 2, (4, 2), (4, 2, 1), (4, 2, 1), 0)  # strides not triples

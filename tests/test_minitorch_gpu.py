@@ -518,3 +518,31 @@ def test_layernorm_vs_reference_fixtures(mt, parity_record):
         parity_record("test_layernorm_vs_reference_fixtures", name,
                       max_abs_fw=float(np.abs(yn - f["fw"]).max()),
                       max_abs_dinp=float(np.abs(got[2] - f["dinp"]).max()), bound="fw 1e-2, bw 1e-3")
+
+
+def test_mtfast_matches_ctypes_path(mt):
+    """The generic ops through the _mtfast extension and through ctypes give bitwise-equal
+    results (map, broadcast zip, reduce, 2-D and batched matmul)."""
+    from minitorch import _hip
+    minitorch, B = mt
+    assert _hip.fast is not None
+    rng = np.random.default_rng(5)
+    x = minitorch.tensor_from_numpy(rng.standard_normal((64, 96)).astype(np.float32), B)
+    y = minitorch.tensor_from_numpy(rng.standard_normal((96,)).astype(np.float32), B)
+    w = minitorch.tensor_from_numpy(rng.standard_normal((96, 48)).astype(np.float32), B)
+    z = minitorch.tensor_from_numpy(rng.standard_normal((3, 64, 96)).astype(np.float32), B)
+    v = minitorch.tensor_from_numpy(rng.standard_normal((3, 96, 40)).astype(np.float32), B)
+
+    def run():
+        return [(-x).to_numpy(), (x + y).to_numpy(), x.sum(0).to_numpy(), (x @ w).to_numpy(),
+                (z @ v).to_numpy(), x.permute(1, 0).contiguous().to_numpy()]
+
+    got_fast = run()
+    saved = _hip.fast
+    _hip.fast = None
+    try:
+        got_ctypes = run()
+    finally:
+        _hip.fast = saved
+    for a, b in zip(got_fast, got_ctypes):
+        np.testing.assert_array_equal(a, b)
