@@ -331,6 +331,7 @@ def _mha_case(minitorch, backend, batch_size, queries_len, n_embd, num_heads, ca
 MHA_GRID = [
     (8, 128, 64, 2), (8, 128, 256, 4), (4, 512, 512, 8), (2, 1024, 1024, 16),
     (2, 256, 2048, 4), (1, 2048, 128, 2), (3, 100, 96, 4),
+    (2, 4096, 256, 4),  # the reference causal test's longest sequence (tests/test_flash_attention.py:104)
 ]
 
 
