@@ -143,6 +143,56 @@ def test_step_graph_new_batches_match_eager():
         np.testing.assert_array_equal(a, b)
 
 
+def test_step_graph_config5_size_matches_eager():
+    """The same bitwise check at config 5's size (B=128, T=39, V=10000, n_embd 256, 8 heads): the
+    replayed graph then holds the kernels the small model never reaches, the column reductions
+    with arrival counters (4992 x 256 bias gradients) and the split-K LM-head dX GEMM with its
+    scratch partials."""
+    import torch
+    assert torch.cuda.is_available(), "needs an MI355X"
+    import minitorch
+    from minitorch.graphs import StepGraph
+    backend = minitorch.TensorBackend(minitorch.HipKernelOps)
+    B, T, V, E, H = 128, 39, 10000, 256, 8
+    rng = np.random.default_rng(9)
+    tok = rng.integers(0, V, size=(B, T + 1)).astype(np.float32)
+    kv = rng.integers(T // 2, T + 1, size=B).astype(np.int64)
+    w = (np.arange(T)[None, :] < kv[:, None]).astype(np.float32)
+
+    def make():
+        np.random.seed(0)
+        lm = minitorch.DecoderLM(n_vocab=V, n_embd=E, n_head=H, n_positions=T + 1, p_dropout=0.1,
+                                 backend=backend, use_fused_kernel=True, use_flash_attention=True)
+        opt = minitorch.Adam(lm.parameters(), lr=1e-4)
+        x = minitorch.tensor_from_numpy(tok[:, :-1].copy(), backend)
+        y = minitorch.tensor_from_numpy(tok[:, 1:].reshape(-1).copy(), backend)
+        wt = minitorch.tensor_from_numpy(w.reshape(-1).copy(), backend)
+
+        def step():
+            opt.zero_grad()
+            loss = (minitorch.softmax_loss(lm(x, kv_len=kv).view(B * T, V), y) * wt).sum() / wt.sum()
+            loss.backward()
+            opt.step()
+            return loss
+        return lm, opt, step
+
+    lm_e, opt_e, step_e = make()
+    np.random.seed(5)
+    eager = [float(step_e().to_numpy()[0]) for _ in range(4)]
+    torch.cuda.synchronize()
+    lm_g, opt_g, step_g = make()
+    np.random.seed(5)
+    g = StepGraph(step_g, warmup=2)
+    graph = []
+    for _ in range(2):
+        loss = g.replay()
+        torch.cuda.synchronize()
+        graph.append(float(loss.to_numpy()[0]))
+    assert graph == eager[2:], (graph, eager)
+    for a, b in zip(_state(lm_e, opt_e), _state(lm_g, opt_g)):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_step_graph_fails_loudly_on_host_sync():
     """A step that needs the host inside it (a device value read back) cannot be captured:
     the capture raises instead of recording a step that would replay wrong."""
