@@ -641,6 +641,52 @@ __global__ __launch_bounds__(256) void xent_fw_kernel(float* loss, float* lse, c
   }
 }
 
+// Rows of up to 16384 classes (16-B aligned, C % 4 == 0): the row is loaded into registers in one
+// burst (up to 16 float4 per lane, all loads in flight together, where the online form above
+// waits on each load before its exp), then max and sum are two workgroup reductions over the
+// resident values: one exp per element and no branch. Config 5's 10000-class rows take 10 loads.
+constexpr int kXentRegVec = 16;
+__global__ __launch_bounds__(256) void xent_fw_reg_kernel(float* loss, float* lse, const float* x,
+                                                          const float* tgt, int64_t rows, int C) {
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nk = (C + 1023) / 1024;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const float* xr = x + r * C;
+    float4 v[kXentRegVec];
+#pragma unroll
+    for (int k = 0; k < kXentRegVec; ++k) {
+      const int j = 4 * tid + 1024 * k;
+      if (k < nk && j < C) v[k] = *(const float4*)(xr + j);
+      else v[k] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < kXentRegVec; ++k)
+      if (k < nk) m = fmaxf(m, fmaxf(fmaxf(v[k].x, v[k].y), fmaxf(v[k].z, v[k].w)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) red[0][w] = m;
+    __syncthreads();
+    const float M = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kXentRegVec; ++k)
+      if (k < nk) s += (expf(v[k].x - M) + expf(v[k].y - M)) + (expf(v[k].z - M) + expf(v[k].w - M));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) red[1][w] = s;
+    __syncthreads();
+    if (tid == 0) {
+      const float l = M + logf((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+      const int64_t t = (int64_t)tgt[r];
+      lse[r] = l;
+      loss[r] = l - ((t >= 0 && t < C) ? xr[t] : 0.f);
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void xent_bw_kernel(float* dx, const float* g, const float* x,
                                                       const float* tgt, const float* lse,
                                                       int64_t rows, int64_t C, int vec) {
@@ -676,8 +722,12 @@ int mt_softmax_xent_fw(float* loss, float* lse, const float* logits, const float
   if (rows <= 0 || classes <= 0) return set_error("mt_softmax_xent_fw: bad sizes");
   const int vec = (classes % 4 == 0) && al16(logits);
   const unsigned grid = (unsigned)(rows < 65536 ? rows : 65536);
-  hipLaunchKernelGGL(xent_fw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, loss, lse, logits, target,
-                     rows, classes, vec);
+  if (vec && classes <= 1024 * kXentRegVec)
+    hipLaunchKernelGGL(xent_fw_reg_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, loss, lse, logits,
+                       target, rows, (int)classes);
+  else
+    hipLaunchKernelGGL(xent_fw_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, loss, lse, logits, target,
+                       rows, classes, vec);
   return check_hip(hipGetLastError(), "mt_softmax_xent_fw");
 }
 

@@ -29,7 +29,7 @@ def _np_xent(x, t, g):
     return loss, p * g[:, None]
 
 
-@pytest.mark.parametrize("rows,C", [(7, 5), (64, 1000), (33, 1023), (4992, 10000)])
+@pytest.mark.parametrize("rows,C", [(7, 5), (5, 4), (64, 1000), (33, 1023), (16, 16384), (8, 16388), (4992, 10000)])
 def test_softmax_xent_vs_numpy_and_composition(mt, rows, C):
     minitorch, backend = mt
     from minitorch import nn
