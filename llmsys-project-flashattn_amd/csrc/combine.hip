@@ -345,6 +345,69 @@ __global__ __launch_bounds__(256) void reduce_cols_fold(int fn, float* __restric
   out[t] = hv ? apply_fn(fn, start, v) : start;
 }
 
+// Column-group reduction (round 5) for [outer][len][inner], inner % 4 = 0, 16-byte aligned rows,
+// len up to 8192: one workgroup owns 4 adjacent columns (a float4 per row) over ALL rows, so no
+// partial ever leaves the workgroup: no scratch, no fence, no arrival counter. Lane t takes rows
+// t, t + T, ... (8 loads in flight), folds them in row order, the wave folds by a fixed xor
+// butterfly and the waves fold in order through LDS: deterministic. Each load instruction of a
+// wave touches 64 rows, one 16-B piece of each 128-B line; the 8 column groups sharing a line are
+// placed on one XCD (blockIdx % 8 picks the XCD), so each line still comes from HBM once.
+// Config 5's 4992 x 256 bias gradient: 4.8 µs against 9.1 µs for the one-pass chunked form,
+// whose cross-XCD hand-off (release fence, agent atomic, acquire, fold) alone costs 6.4 µs
+// (scripts/colsum_bench.hip).
+__device__ __forceinline__ void fold4(int fn, float4& v, bool& hv, const float4& y, bool hy) {
+  if (!hy) return;
+  if (!hv) { v = y; hv = true; return; }
+  v.x = apply_fn(fn, v.x, y.x); v.y = apply_fn(fn, v.y, y.y);
+  v.z = apply_fn(fn, v.z, y.z); v.w = apply_fn(fn, v.w, y.w);
+}
+template <int FN>
+__global__ __launch_bounds__(1024) void reduce_colgroup_kernel(int fn_rt, float* __restrict__ out,
+                                                               const float* __restrict__ a, int64_t len,
+                                                               int64_t inner, int ncg, int xcd_map,
+                                                               float start) {
+  const int fn = FN >= 0 ? FN : fn_rt;
+  __shared__ float4 red[16];
+  __shared__ int have_s[16];
+  const int b = blockIdx.x, o = blockIdx.y;
+  // xcd_map: the 8 groups of line L sit at blockIdx b with b % 8 == L % 8
+  const int cg = xcd_map ? (((b & 7) + 8 * ((b >> 3) >> 3)) * 8 + ((b >> 3) & 7)) : b;
+  if (cg >= ncg) return;  // padding workgroups of the XCD map: uniform, before any barrier
+  const int t = threadIdx.x, T = blockDim.x, lane = t & 63, w = t >> 6;
+  const float* src = a + (int64_t)o * len * inner + (int64_t)cg * 4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  bool hv = false;
+  for (int64_t j = t; j < len; j += 8 * (int64_t)T) {
+    float4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)  // masked, not clamped: a load instruction costs per row it touches
+      x[u] = j + (int64_t)u * T < len ? *(const float4*)(src + (j + (int64_t)u * T) * inner)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fold4(fn, v, hv, x[u], j + (int64_t)u * T < len);
+  }
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    float4 y;
+    y.x = __shfl_xor(v.x, s); y.y = __shfl_xor(v.y, s); y.z = __shfl_xor(v.z, s); y.w = __shfl_xor(v.w, s);
+    const bool hy = __shfl_xor((int)hv, s) != 0;
+    // the lower lane of each pair keeps (own, partner): lane 0 ends with the rows in a fixed order
+    if (lane & s) { float4 z = v; bool hz = hv; v = y; hv = hy; fold4(fn, v, hv, z, hz); }
+    else fold4(fn, v, hv, y, hy);
+  }
+  if (lane == 0) { red[w] = v; have_s[w] = hv; }
+  __syncthreads();
+  if (t == 0) {
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool hr = false;
+    for (int k = 0; k < T / 64; ++k) fold4(fn, r, hr, red[k], have_s[k] != 0);
+    if (hr) { r.x = apply_fn(fn, start, r.x); r.y = apply_fn(fn, start, r.y);
+              r.z = apply_fn(fn, start, r.z); r.w = apply_fn(fn, start, r.w); }
+    else r = make_float4(start, start, start, start);
+    *(float4*)(out + (int64_t)o * inner + (int64_t)cg * 4) = r;
+  }
+}
+
 // One-pass column reduction (round 5) for [outer][len][inner] with inner % 4 = 0 and 16-byte
 // aligned rows: workgroup (column block of 256, row chunk r, outer o) has 8 waves; a lane owns 4
 // adjacent columns (float4 loads: a wave reads one 1 KiB row segment per load) and a wave takes
@@ -426,11 +489,20 @@ __global__ __launch_bounds__(512) void reduce_cols1_kernel(int fn_rt, float* __r
   const float* p = part + (int64_t)o * R * inner + col;
   float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
   if (live && r0 < r1) {
+    // the partials come from other XCDs' workgroups (misses in this XCD's L2): 16 loads in
+    // flight per batch, folded in chunk order, instead of one dependent miss per partial
     v = *(const float4*)(p + (int64_t)r0 * inner);
-    for (int q = r0 + 1; q < r1; ++q) {
-      const float4 y = *(const float4*)(p + (int64_t)q * inner);
-      v.x = apply_fn(fn, v.x, y.x); v.y = apply_fn(fn, v.y, y.y);
-      v.z = apply_fn(fn, v.z, y.z); v.w = apply_fn(fn, v.w, y.w);
+    for (int q = r0 + 1; q < r1; q += 16) {
+      float4 y[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) y[u] = *(const float4*)(p + (int64_t)min(q + u, r1 - 1) * inner);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        if (q + u < r1) {
+          v.x = apply_fn(fn, v.x, y[u].x); v.y = apply_fn(fn, v.y, y[u].y);
+          v.z = apply_fn(fn, v.z, y[u].z); v.w = apply_fn(fn, v.w, y[u].w);
+        }
+      }
     }
   }
   red[w][lane] = v;
@@ -932,8 +1004,26 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   const int64_t len = a_shape[reduce_dim];
   // the one-pass form up to 64 MiB of input; above that the two-kernel form streams faster
   // (4992 x 10000, 200 MB: 57 µs against 84-90 µs at 240-2048 workgroups of the one-pass form)
-  if (al.contiguous && ol.contiguous && inner % 4 == 0 && inner >= 64 && len >= 16 && outer <= 65535 &&
-      outer * len * inner <= ((int64_t)16 << 20) && ((((uintptr_t)a | (uintptr_t)out) & 15) == 0)) {
+  const bool al16 = ((((uintptr_t)a | (uintptr_t)out) & 15) == 0);
+  if (al.contiguous && ol.contiguous && inner % 4 == 0 && al16 && len >= 2 && len <= 8192 &&
+      outer <= 65535 && outer * (inner / 4) >= 32 && outer * len * inner <= ((int64_t)8 << 20)) {
+    // column groups: every workgroup owns whole columns (see reduce_colgroup_kernel)
+    const int ncg = (int)(inner / 4);
+    const int xcd_map = ncg >= 64;
+    const unsigned gx = (unsigned)(xcd_map ? (ncg + 63) / 64 * 64 : ncg);
+    const int T = (int)std::min<int64_t>(1024, (len + 63) / 64 * 64);
+    const dim3 grid(gx, (unsigned)outer);
+    const hipStream_t st = (hipStream_t)stream;
+    if (fn == FN_ADD)
+      hipLaunchKernelGGL(reduce_colgroup_kernel<FN_ADD>, grid, dim3(T), 0, st, fn, out, a, len, inner, ncg, xcd_map, start);
+    else if (fn == FN_MUL)
+      hipLaunchKernelGGL(reduce_colgroup_kernel<FN_MUL>, grid, dim3(T), 0, st, fn, out, a, len, inner, ncg, xcd_map, start);
+    else if (fn == FN_MAX)
+      hipLaunchKernelGGL(reduce_colgroup_kernel<FN_MAX>, grid, dim3(T), 0, st, fn, out, a, len, inner, ncg, xcd_map, start);
+    else
+      hipLaunchKernelGGL(reduce_colgroup_kernel<-1>, grid, dim3(T), 0, st, fn, out, a, len, inner, ncg, xcd_map, start);
+  } else if (al.contiguous && ol.contiguous && inner % 4 == 0 && inner >= 64 && len >= 16 && outer <= 65535 &&
+      outer * len * inner <= ((int64_t)16 << 20) && al16) {
     // one pass: row chunks of at least 8 rows per wave, about 256 workgroups in all
     const int64_t cb = (inner + 255) / 256;
     // about 256 workgroups, 8 rows per wave (8 beat 4, 16, 32 and 64 rows and 128 workgroups at

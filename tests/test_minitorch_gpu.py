@@ -87,11 +87,14 @@ def test_zip_map_paths(mt, case):
                                        ((17, 33), 0), ((50, 64, 1), 0), ((4992, 10000), 0),
                                        ((16, 20), 0), ((3, 4096, 80), 1), ((2000, 17), 0),
                                        ((5, 1000, 300), 1), ((4992, 4), 0), ((70, 128), 0),
-                                       ((4992,), 0), ((3, 20000), 1), ((100000,), 0)])
+                                       ((4992,), 0), ((3, 20000), 1), ((100000,), 0),
+                                       ((3, 8192, 64), 1), ((8193, 128), 0), ((128, 39, 256), 0),
+                                       ((40, 260), 0), ((2, 7, 64), 1)])
 def test_reduce_paths(mt, shape, dim):
-    """Sum and max over a non-innermost dim (the one-pass column kernel with arrival counters
-    where the layout allows: bias gradients; the two-kernel column form; the other reduce
-    kernels) against NumPy; a repeated sum is bitwise equal (fixed fold order, counters reset)."""
+    """Sum and max over a non-innermost dim (the column-group kernel up to 8192 rows: bias
+    gradients, with and without the XCD placement and its padding workgroups; the one-pass column
+    kernel with arrival counters; the two-kernel column form; the other reduce kernels) against
+    NumPy; a repeated sum is bitwise equal (fixed fold order, counters reset)."""
     minitorch, B = mt
     rng = np.random.default_rng(sum(shape) + dim)
     x = rng.standard_normal(shape).astype(np.float32)
