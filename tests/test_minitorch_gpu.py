@@ -241,7 +241,8 @@ def test_device_rand_and_dropout(mt):
 
 
 @pytest.mark.parametrize("shapes", [((5, 7), (7, 3)), ((4, 33, 65), (4, 65, 70)),
-                                    ((2, 3, 17, 8), (2, 3, 8, 40)), ((1, 64, 96), (3, 96, 5))])
+                                    ((2, 3, 17, 8), (2, 3, 8, 40)), ((1, 64, 96), (3, 96, 5)),
+                                    ((4992, 256), (256, 256))])
 @pytest.mark.parametrize("gemm_backend", [0, 1])
 def test_matmul(mt, shapes, gemm_backend):
     """Batched matmul on both GEMM back ends (0: rocBLAS for plain layouts with the own
@@ -281,22 +282,23 @@ def _matmul_case(mt, shapes):
     w = rng.standard_normal(shapes[1]).astype(np.float32)
     out = minitorch.tensor_from_numpy(x, B) @ minitorch.tensor_from_numpy(w, B)
     ref = np.matmul(x.astype(np.float64), w.astype(np.float64))
-    np.testing.assert_allclose(out.to_numpy(), ref, rtol=1e-5, atol=1e-5)
+    tol = 1e-5 * max(1.0, shapes[0][-1] / 32)  # fp32 sums over K: the error grows with K
+    np.testing.assert_allclose(out.to_numpy(), ref, rtol=1e-5, atol=tol)
     # transposed (strided) operand
     xt = minitorch.tensor_from_numpy(np.ascontiguousarray(np.swapaxes(x, -1, -2)), B)
     order = list(range(xt.dims))
     order[-1], order[-2] = order[-2], order[-1]
     out2 = xt.permute(*order) @ minitorch.tensor_from_numpy(w, B)
-    np.testing.assert_allclose(out2.to_numpy(), ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out2.to_numpy(), ref, rtol=1e-5, atol=tol)
     # transposed (strided) right operand: op T without a copy where it is small
     wt = minitorch.tensor_from_numpy(np.ascontiguousarray(np.swapaxes(w, -1, -2)), B)
     out_r = minitorch.tensor_from_numpy(x, B) @ wt.permute(*order)
-    np.testing.assert_allclose(out_r.to_numpy(), ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out_r.to_numpy(), ref, rtol=1e-5, atol=tol)
     if x.ndim == 3:
         # no unit stride in either matrix dim: (M, K, batch) storage viewed as (batch, M, K)
         xs = minitorch.tensor_from_numpy(np.ascontiguousarray(np.moveaxis(x, 0, -1)), B)
         out3 = xs.permute(2, 0, 1) @ minitorch.tensor_from_numpy(w, B)
-        np.testing.assert_allclose(out3.to_numpy(), ref, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(out3.to_numpy(), ref, rtol=1e-5, atol=tol)
 
 
 def _mha_case(minitorch, backend, batch_size, queries_len, n_embd, num_heads, causal, use_flash,
