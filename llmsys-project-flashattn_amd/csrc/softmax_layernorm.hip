@@ -559,6 +559,52 @@ __global__ __launch_bounds__(256) void ln_bw_vec_seg(float* out, const float* ws
   }
 }
 
+// The blocks' dγ/dβ partials in one launch (round 5): the slab [nb][2][H] read as [nb][2H], a
+// workgroup per 4 adjacent columns over all nb partial rows (lane t: rows t, t + T, ...; a fixed
+// pairwise tree through LDS), so nothing crosses a workgroup: deterministic, and one launch where
+// the segment + final pair took two (config 5, H = 256, nb = 1024: 5.1 + 4.8 µs per LayerNorm).
+// The 8 column groups sharing a 128-B line run on one XCD (blockIdx % 8).
+__global__ __launch_bounds__(1024) void ln_bw_vec_colsum(float* dgamma, float* dbeta, const float* ws,
+                                                         int64_t H, int64_t nb, int ncg) {
+  __shared__ float4 red[1024];
+  const int b = blockIdx.x;
+  const int cg = ncg >= 64 ? (((b & 7) + 8 * ((b >> 3) >> 3)) * 8 + ((b >> 3) & 7)) : b;
+  if (cg >= ncg) return;  // padding workgroups of the XCD placement: uniform, before the barrier
+  const int t = threadIdx.x, T = blockDim.x;  // T = min(1024, nb): every lane has a row
+  const int64_t W = 2 * H;
+  const float* src = ws + (int64_t)cg * 4;
+  float4 v = *(const float4*)(src + (int64_t)t * W);
+  for (int64_t j = t + T; j < nb; j += 8 * (int64_t)T) {
+    float4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      x[u] = j + (int64_t)u * T < nb ? *(const float4*)(src + (j + (int64_t)u * T) * W)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { v.x += x[u].x; v.y += x[u].y; v.z += x[u].z; v.w += x[u].w; }
+  }
+  red[t] = v;
+  __syncthreads();
+  int p2 = 1;
+  while (p2 < T) p2 <<= 1;
+  for (int st = p2 >> 1; st > 0; st >>= 1) {
+    if (t < st && t + st < T) {
+      const float4 y = red[t + st];
+      float4 x = red[t];
+      x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
+      red[t] = x;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const float r[4] = {red[0].x, red[0].y, red[0].z, red[0].w};
+    for (int k = 0; k < 4; ++k) {
+      const int64_t c = (int64_t)cg * 4 + k;
+      if (c < H) dbeta[c] = r[k];
+      else dgamma[c - H] = r[k];
+    }
+  }
+}
 __global__ __launch_bounds__(256) void ln_bw_vec_final(float* dgamma, float* dbeta, const float* ws,
                                                        int64_t H, int64_t nb) {
   const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -846,6 +892,14 @@ int mt_layernorm_bw(float* gamma_grad, float* beta_grad, float* inp_grad, const 
 #undef MT_LN_BW
 #undef MT_LN_BW_ROW
     if (check_hip(hipGetLastError(), "mt_layernorm_bw(fused)")) return 1;
+    if (hidden % 4 == 0 && nb >= 1) {
+      const int ncg = (int)(hidden / 2);  // 2H / 4 column groups
+      const unsigned gx = (unsigned)(ncg >= 64 ? (ncg + 63) / 64 * 64 : ncg);
+      const int T = (int)(nb < 1024 ? nb : 1024);
+      hipLaunchKernelGGL(ln_bw_vec_colsum, dim3(gx), dim3(T), 0, st, gamma_grad, beta_grad, (const float*)ws,
+                         hidden, nb, ncg);
+      return check_hip(hipGetLastError(), "mt_layernorm_bw(colsum)");
+    }
     const int64_t nseg = (nb + kSlabSeg - 1) / kSlabSeg;
     float* ws2 = ws + 2 * nb * hidden;
     hipLaunchKernelGGL(ln_bw_vec_seg, dim3((unsigned)((hidden + 63) / 64), (unsigned)nseg), dim3(256), 0, st,
