@@ -1006,8 +1006,12 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   // the one-pass form up to 64 MiB of input; above that the two-kernel form streams faster
   // (4992 x 10000, 200 MB: 57 µs against 84-90 µs at 240-2048 workgroups of the one-pass form)
   const bool al16 = ((((uintptr_t)a | (uintptr_t)out) & 15) == 0);
+  static const int64_t colgroup_max = [] {  // A/B knob: MT_COLGROUP_MAX (floats)
+    const char* e = getenv("MT_COLGROUP_MAX");
+    return e ? (int64_t)atoll(e) : ((int64_t)8 << 20);
+  }();
   if (al.contiguous && ol.contiguous && inner % 4 == 0 && al16 && len >= 2 && len <= 8192 &&
-      outer <= 65535 && outer * (inner / 4) >= 32 && outer * len * inner <= ((int64_t)8 << 20)) {
+      outer <= 65535 && outer * (inner / 4) >= 32 && outer * len * inner <= colgroup_max) {
     // column groups: every workgroup owns whole columns (see reduce_colgroup_kernel)
     const int ncg = (int)(inner / 4);
     const int xcd_map = ncg >= 64;

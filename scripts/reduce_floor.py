@@ -30,7 +30,7 @@ def timed(fn, n=200):
 backend = minitorch.TensorBackend(minitorch.HipKernelOps)
 rng = np.random.default_rng(0)
 out = {}
-for rows, cols in [(4992, 256), (4992, 1024)]:
+for rows, cols in [(4992, 256), (4992, 1024), (4992, 10000), (128, 9984)]:
     x = rng.standard_normal((rows, cols)).astype(np.float32)
     a = minitorch.tensor_from_numpy(x, backend)
     t = torch.from_numpy(x).cuda()
