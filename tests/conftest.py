@@ -14,6 +14,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
 
 
+def pytest_collection_modifyitems(session, config, items):
+    """The host-sanitizer run of the C ABI (tests/test_asan.py) goes last: it is
+    infrastructure, and under ``-x`` a failure there must not stop the parity tests from
+    running (GPUTEST_r05 stopped at it before any of them)."""
+    items.sort(key=lambda it: it.nodeid.startswith("tests/test_asan.py") or "/test_asan.py" in it.nodeid)
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")

@@ -14,6 +14,8 @@
 // first hipMalloc, which walks every wrapper's error-cleanup path under ASan.
 // Exit status 0 = all checks passed (ASan aborts with its own report on a memory error).
 #include <hip/hip_runtime.h>
+#include <sanitizer/lsan_interface.h>
+#include <unistd.h>
 
 #include <cmath>
 #include <cstdio>
@@ -226,6 +228,7 @@ static void valid_problems(bool gpu) {
 }
 
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IOLBF, 0);  // a sanitizer exit must not lose the progress lines
   int ndev = 0;
   const bool gpu = hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0;
   printf("capi_asan: %s\n", gpu ? "GPU present: full wrapper paths" : "no GPU: error-cleanup paths");
@@ -239,6 +242,15 @@ int main(int argc, char** argv) {
   CHECK(g_live == 0, "%ld device buffers left allocated", g_live);
   printf("capi_asan: %ld device allocations, %ld still live\n", g_mallocs, g_live);
   if (gpu) CHECK(g_mallocs > 100, "the wrappers' hipMalloc calls were not intercepted");
+  // Leak check now, then leave without running the ROCm runtime's static destructors:
+  // with a GPU present, libamdhip64's __cxa_finalize tears the HSA runtime down and then
+  // frees host objects that ASan's device-aware allocator can no longer release
+  // ("CHECK failed: sanitizer_allocator_device.h:125 dev_runtime_unloaded_", exit 1,
+  // GPUTEST_r05) -- a teardown-order fault of the sanitizer runtime, after every check here.
+  const int leaks = __lsan_do_recoverable_leak_check();
+  CHECK(leaks == 0, "LeakSanitizer reported leaks (see its report above)");
   printf("capi_asan: %s (%d failures)\n", g_fail ? "FAILED" : "ok", g_fail);
-  return g_fail ? 1 : 0;
+  fflush(stdout);
+  fflush(stderr);
+  _exit(g_fail ? 1 : 0);
 }
