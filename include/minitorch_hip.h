@@ -46,6 +46,15 @@ int mt_abi_version(void);
  * read atomically at each launch. */
 int mt_flash_set_kernel_policy(int policy);
 int mt_flash_get_kernel_policy(void);
+/* Device scratch the library holds between calls (stream-ordered buffers of the zero-padded
+ * head-dim copies and the column-reduction partials, one per (pool, device, stream)): its
+ * bytes, and a release that frees every buffer no captured hipGraph was handed (after a
+ * synchronize of the buffer's stream). Buffers are re-allocated on the next call that needs
+ * them. (The reference allocates and frees inside each launcher,
+ * src/flashattention_kernel.cu:319-324; here the padded copies are chunked to at most
+ * 512 MiB per call.) */
+int64_t mt_scratch_bytes(void);
+int mt_scratch_release(void);
 
 /* ---- FlashAttention, device pointers ------------------------------------- */
 /* O = softmax(Q Kᵀ/√d [causal]) V;  m[b,h,n] = row max of the scaled logits,

@@ -6,6 +6,7 @@
 // binding (minitorch/cuda_kernel_ops.py:605-892) can load this library unchanged.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/minitorch_hip.h"
@@ -258,6 +259,28 @@ __global__ __launch_bounds__(256) void unpad_rows_kernel(char* __restrict__ dst,
     const int64_t bh = row / N, r = row - bh * N;
     *(uint4*)(dst + ((bh / H) * s0 + (bh % H) * s1 + r * s2) * es + (int64_t)c * 16) = src[row * pchunks + c];
   }
+}
+// The padded copies of one call are taken over groups of heads that keep the scratch within
+// kPadScratchCap (one call at (64,16,16384,96) held ≈ 34 GB): fn(b0, h0, nb, nh)
+// runs the heads h0 .. h0 + nh - 1 of the batch rows b0 .. b0 + nb - 1, in stream order (the
+// groups reuse one buffer). At most 65535 heads per group (the kernels' grid.y bound).
+// (MT_PAD_SCRATCH_CAP=<bytes> lowers the cap: how the tests reach several groups at small sizes.)
+static constexpr int64_t kPadScratchCap = (int64_t)512 << 20;
+template <class F>
+static hipError_t for_head_groups(int64_t B, int64_t H, int64_t bytes_per_head, F&& fn) {
+  int64_t cap = kPadScratchCap;
+  if (const char* e = getenv("MT_PAD_SCRATCH_CAP")) cap = std::max<int64_t>(1, std::min<int64_t>(cap, atoll(e)));
+  const int64_t hc = std::max<int64_t>(1, std::min<int64_t>(cap / bytes_per_head, 65535));
+  if (hc >= H) {
+    const int64_t bc = std::max<int64_t>(1, hc / H);
+    for (int64_t b0 = 0; b0 < B; b0 += bc)
+      if (const hipError_t e = fn(b0, (int64_t)0, std::min(bc, B - b0), H)) return e;
+    return hipSuccess;
+  }
+  for (int64_t b0 = 0; b0 < B; ++b0)
+    for (int64_t h0 = 0; h0 < H; h0 += hc)
+      if (const hipError_t e = fn(b0, h0, (int64_t)1, std::min(hc, H - h0))) return e;
+  return hipSuccess;
 }
 static unsigned pad_grid(int64_t n) { return (unsigned)std::min<int64_t>((n + 255) / 256, 8192); }
 static hipError_t pad_rows(void* dst, const void* src, const int64_t s[3], int64_t B, int64_t H, int64_t N,
@@ -610,24 +633,38 @@ int mt_flash_attn_fwd_varlen(int dtype, int causal, const void* q, const void* k
   // bf16 d = 64 / 128 MFMA schedules have no per-row key bound)
   if (dtype == MT_BF16 && vec && pol != kPolGeneric && !kv_len) {
     const int64_t dp = pad_dim(d);
-    if (dp) {  // the d = 64 / 128 kernels on zero-padded copies (pad_dim)
-      const int64_t nel = B * H * N * dp, oes = f32o ? 4 : 2;
-      char* buf = (char*)pad_scratch((size_t)(nel * (3 * 2 + oes)), st);
-      if (buf) {
+    if (dp) {  // the d = 64 / 128 kernels on zero-padded copies (pad_dim), by groups of heads
+      const int64_t oes = f32o ? 4 : 2;
+      bool declined = false;
+      const hipError_t e = for_head_groups(B, H, N * dp * (3 * 2 + oes), [&](int64_t b0, int64_t h0, int64_t nb, int64_t nh) -> hipError_t {
+        if (declined) return hipSuccess;
+        const int64_t nel = nb * nh * N * dp;
+        char* buf = (char*)pad_scratch((size_t)(nel * (3 * 2 + oes)), st);
+        if (!buf) { declined = true; return hipSuccess; }
         AttnArgs ap = a;
+        ap.B = (int)nb; ap.H = (int)nh;
         ap.q = buf; ap.k = buf + nel * 2; ap.v = buf + nel * 4; ap.out = buf + nel * 6;
         int64_t* ps[4] = {ap.sq, ap.sk, ap.sv, ap.so};
-        for (int i = 0; i < 4; ++i) fill_strides(ps[i], nullptr, H, N, dp);
+        for (int i = 0; i < 4; ++i) fill_strides(ps[i], nullptr, nh, N, dp);
         ap.d = (int)dp;  // the scale stays the real d's
-        hipError_t e = pad_rows((void*)ap.q, q, a.sq, B, H, N, d, dp, st);
-        if (e == hipSuccess) e = pad_rows((void*)ap.k, k, a.sk, B, H, N, d, dp, st);
-        if (e == hipSuccess) e = pad_rows((void*)ap.v, v, a.sv, B, H, N, d, dp, st);
+        const int64_t row0 = (b0 * H + h0) * N;
+        if (a.m) ap.m = a.m + row0;
+        if (a.l) ap.l = a.l + row0;
+        auto at = [&](const void* base, const int64_t* st3, int64_t es) {
+          return (const char*)base + (b0 * st3[0] + h0 * st3[1]) * es;
+        };
+        hipError_t r = pad_rows((void*)ap.q, at(q, a.sq, 2), a.sq, nb, nh, N, d, dp, st);
+        if (r == hipSuccess) r = pad_rows((void*)ap.k, at(k, a.sk, 2), a.sk, nb, nh, N, d, dp, st);
+        if (r == hipSuccess) r = pad_rows((void*)ap.v, at(v, a.sv, 2), a.sv, nb, nh, N, d, dp, st);
         bool handled = false;
-        if (e == hipSuccess) e = fwd_bf16_dispatch(ap, causal != 0, pol, st, &handled);
-        if (e == hipSuccess && !handled) return set_error("mt_flash_attn_fwd: no kernel for the padded d = %lld", (long long)dp);
-        if (e == hipSuccess) e = unpad_rows(o, ap.out, a.so, (int)oes, B, H, N, d, dp, st);
-        return check_hip(e, "mt_flash_attn_fwd(bf16, padded d)");
-      }
+        if (r == hipSuccess) r = fwd_bf16_dispatch(ap, causal != 0, pol, st, &handled);
+        if (r == hipSuccess && !handled) { declined = true; return hipSuccess; }
+        if (r == hipSuccess) r = unpad_rows((void*)at(o, a.so, oes), ap.out, a.so, (int)oes, nb, nh, N, d, dp, st);
+        return r;
+      });
+      // a declined group (no scratch, or no padded kernel for the shape) sends the whole call
+      // to the unpadded dispatch below, which writes every output again
+      if (e != hipSuccess || !declined) return check_hip(e, "mt_flash_attn_fwd(bf16, padded d)");
     }
     bool handled = false;
     const hipError_t e = fwd_bf16_dispatch(a, causal != 0, pol, st, &handled);
@@ -727,37 +764,53 @@ static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void*
   const int pol = g_kernel_policy.load(std::memory_order_relaxed);
   const int64_t dp = pad_dim(d);
   if (dtype == MT_BF16 && vec && pol != kPolGeneric && !kv_len && dp) {
-    // the d = 64 / 128 backward on zero-padded copies (pad_dim): Q, K, V, O, dO in, dQ, dK, dV
-    // out; the fused slab only where a checked caller's workspace holds it
+    // the d = 64 / 128 backward on zero-padded copies (pad_dim) by groups of heads: Q, K, V,
+    // O, dO in, dQ, dK, dV out; each group runs its own prep (lse2, δ at the workspace's
+    // start) and, where a checked caller's workspace holds the whole call's slab, the fused pass
     hipStream_t st = (hipStream_t)stream;
-    const int64_t nel = B * H * N * dp;
-    char* buf = (char*)pad_scratch((size_t)(nel * 2 * 8), st);
-    if (buf) {
+    const bool fused = fused_bwd_applies(B, H, N, dp) && checked && kFusedBwdDefault;
+    bool declined = false;
+    const hipError_t e = for_head_groups(B, H, N * dp * 2 * 8, [&](int64_t b0, int64_t h0, int64_t nb, int64_t nh) -> hipError_t {
+      if (declined) return hipSuccess;
+      const int64_t nel = nb * nh * N * dp;
+      char* buf = (char*)pad_scratch((size_t)(nel * 2 * 8), st);
+      if (!buf) { declined = true; return hipSuccess; }
       AttnArgs ap = a;
+      ap.B = (int)nb; ap.H = (int)nh;
+      auto at = [&](const void* base, const int64_t* st3) {
+        return (const char*)base + (b0 * st3[0] + h0 * st3[1]) * 2;
+      };
       const void** in[5] = {&ap.q, &ap.k, &ap.v, &ap.o, &ap.dout};
       const void* src[5] = {q, k, v, o, dout};
       const int64_t* ss[5] = {a.sq, a.sk, a.sv, a.so, a.sdo};
-      hipError_t e = hipSuccess;
-      for (int i = 0; i < 5 && e == hipSuccess; ++i) {
+      hipError_t r = hipSuccess;
+      for (int i = 0; i < 5 && r == hipSuccess; ++i) {
         *in[i] = buf + i * nel * 2;
-        e = pad_rows((void*)*in[i], src[i], ss[i], B, H, N, d, dp, st);
+        r = pad_rows((void*)*in[i], at(src[i], ss[i]), ss[i], nb, nh, N, d, dp, st);
       }
       ap.dq = buf + 5 * nel * 2; ap.dk = buf + 6 * nel * 2; ap.dv = buf + 7 * nel * 2;
       int64_t* ps[8] = {ap.sq, ap.sk, ap.sv, ap.so, ap.sdo, ap.sdq, ap.sdk, ap.sdv};
-      for (int i = 0; i < 8; ++i) fill_strides(ps[i], nullptr, H, N, dp);
+      for (int i = 0; i < 8; ++i) fill_strides(ps[i], nullptr, nh, N, dp);
       ap.d = (int)dp;
-      ap.slab = fused_bwd_applies(B, H, N, dp) && checked ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
+      const int64_t row0 = (b0 * H + h0) * N;
+      ap.m = a.m + row0; ap.l = a.l + row0;
+      ap.lse2 = (float*)workspace;
+      ap.delta = ap.lse2 + nb * nh * N;
+      ap.slab = fused ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
       bool handled = false;
-      if (e == hipSuccess) {
-        const int split = !causal ? 5 : (int64_t)((N + 255) / 256) * a.B * a.H >= 512 ? 18 : 0;
-        e = launch_bwd_bf16(ap, causal != 0, ap.slab && kFusedBwdDefault ? 20 : split, st, &handled);
+      if (r == hipSuccess) {
+        const int split = !causal ? 5 : (int64_t)((N + 255) / 256) * nb * nh >= 512 ? 18 : 0;
+        r = launch_bwd_bf16(ap, causal != 0, ap.slab ? 20 : split, st, &handled);
       }
-      if (e == hipSuccess && !handled) return set_error("mt_flash_attn_bwd: no kernel for the padded d = %lld", (long long)dp);
-      if (e == hipSuccess) e = unpad_rows(dq, ap.dq, a.sdq, 2, B, H, N, d, dp, st);
-      if (e == hipSuccess) e = unpad_rows(dk, ap.dk, a.sdk, 2, B, H, N, d, dp, st);
-      if (e == hipSuccess) e = unpad_rows(dv, ap.dv, a.sdv, 2, B, H, N, d, dp, st);
-      return check_hip(e, "mt_flash_attn_bwd(bf16, padded d)");
-    }
+      if (r == hipSuccess && !handled) { declined = true; return hipSuccess; }
+      if (r == hipSuccess) r = unpad_rows((void*)at(dq, a.sdq), ap.dq, a.sdq, 2, nb, nh, N, d, dp, st);
+      if (r == hipSuccess) r = unpad_rows((void*)at(dk, a.sdk), ap.dk, a.sdk, 2, nb, nh, N, d, dp, st);
+      if (r == hipSuccess) r = unpad_rows((void*)at(dv, a.sdv), ap.dv, a.sdv, 2, nb, nh, N, d, dp, st);
+      return r;
+    });
+    // a declined group (no scratch, or no padded kernel for the shape) sends the whole call to
+    // the generic kernels below, which write every gradient again
+    if (e != hipSuccess || !declined) return check_hip(e, "mt_flash_attn_bwd(bf16, padded d)");
   }
   // key padding (kv_len): the fused bf16 d = 64 kernel or the generic / ring kernels, which
   // mask keys >= kv_len[b] (the split bf16 kernels do not: policy 121 with kv_len runs the

@@ -472,18 +472,19 @@ __global__ __launch_bounds__(512) void reduce_cols1_kernel(int fn_rt, float* __r
         v.z = apply_fn(fn, start, v.z); v.w = apply_fn(fn, start, v.w);
         *(float4*)(out + (int64_t)o * inner + col) = v;
       }
-      return;
-    }
-    if (live) *(float4*)(part + ((int64_t)o * R + r) * inner + col) = v;
-    __threadfence();  // release the partial at agent scope before the arrival
-    if (lane == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(counters + (int64_t)o * cbn + blockIdx.x, 1u,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last_s = prev == (unsigned)(R - 1);
+    } else {
+      if (live) *(float4*)(part + ((int64_t)o * R + r) * inner + col) = v;
+      __threadfence();  // release the partial at agent scope before the arrival
+      if (lane == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(counters + (int64_t)o * cbn + blockIdx.x, 1u,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_s = prev == (unsigned)(R - 1);
+      }
     }
   }
+  if (R == 1) return;  // uniform: every wave leaves before the second barrier
   __syncthreads();
-  if (R == 1 || !last_s) return;
+  if (!last_s) return;
   __threadfence();  // acquire: the other chunks' partials
   const int per = (R + kCol1Waves - 1) / kCol1Waves;
   const int r0 = w * per, r1 = min(R, r0 + per);
@@ -526,35 +527,57 @@ __global__ __launch_bounds__(512) void reduce_cols1_kernel(int fn_rt, float* __r
   }
 }
 
+namespace {
+struct ScratchSlot { int pool; int dev; hipStream_t st; void* buf; size_t cap; bool captured; };
+std::mutex g_scratch_mu;
+ScratchSlot g_scratch[128] = {};
+int g_nscratch = 0;
+// buffers a stream capture was handed and then outgrown: a captured hipGraph replays with the
+// address it was captured with, so they stay allocated for the life of the process
+std::vector<std::pair<void*, size_t>> g_scratch_kept;
+}  // namespace
+
 void* stream_scratch(int pool, size_t bytes, hipStream_t st) {
-  struct Slot { int pool; int dev; hipStream_t st; void* buf; size_t cap; };
-  static std::mutex mu;
-  static Slot slots[128] = {};
-  static int nslots = 0;
-  static std::vector<void*> retired;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  Slot* s = nullptr;
-  for (int i = 0; i < nslots && !s; ++i)
-    if (slots[i].pool == pool && slots[i].dev == dev && slots[i].st == st) s = &slots[i];
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  ScratchSlot* s = nullptr;
+  for (int i = 0; i < g_nscratch && !s; ++i)
+    if (g_scratch[i].pool == pool && g_scratch[i].dev == dev && g_scratch[i].st == st) s = &g_scratch[i];
   if (!s) {
-    if (nslots == 128) return nullptr;  // the caller then takes its path without scratch
-    s = &slots[nslots++];
-    *s = Slot{pool, dev, st, nullptr, 0};
+    if (g_nscratch == 128) return nullptr;  // the caller then takes its path without scratch
+    s = &g_scratch[g_nscratch++];
+    *s = ScratchSlot{pool, dev, st, nullptr, 0, false};
   }
   if (s->cap < bytes) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if (capturing) return nullptr;  // no allocation inside a capture
+    // the reduction pool doubles (many small, growing asks); the padded-copy pool takes the
+    // exact size (its callers chunk to at most kPadScratchCap bytes)
+    if (pool != kScratchPad) bytes = std::max(bytes, 2 * s->cap);
+    if (s->buf) {
+      if (s->captured) {
+        g_scratch_kept.emplace_back(s->buf, s->cap);
+      } else {
+        // nothing but this stream's pending work can use it: free it once that has run
+        if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+        (void)hipFree(s->buf);
+      }
+      s->buf = nullptr;
+      s->cap = 0;
+      s->captured = false;
+    }
     void* nb = nullptr;
-    bytes = std::max(bytes, 2 * s->cap);
     if (hipMalloc(&nb, bytes) != hipSuccess) return nullptr;
-    if (s->buf) retired.push_back(s->buf);
     s->buf = nb;
     s->cap = bytes;
   }
+  if (capturing) s->captured = true;
   return s->buf;
 }
+
 static void* reduce_scratch(size_t bytes, hipStream_t st) { return stream_scratch(kScratchReduce, bytes, st); }
 
 // Arrival counters of the one-pass column reduction, one zeroed block per (device, stream),
@@ -938,6 +961,35 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 }
 
 extern "C" {
+
+int64_t mt_scratch_bytes(void) {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  int64_t n = 0;
+  for (int i = 0; i < g_nscratch; ++i) n += (int64_t)g_scratch[i].cap;
+  for (const auto& k : g_scratch_kept) n += (int64_t)k.second;
+  return n;
+}
+
+int mt_scratch_release(void) {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  for (int i = 0; i < g_nscratch; ++i) {
+    ScratchSlot& s = g_scratch[i];
+    if (!s.buf || s.captured) continue;  // a captured graph may still replay with it
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s.st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) continue;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return set_error("mt_scratch_release: hipGetDevice failed");
+    if (hipSetDevice(s.dev) != hipSuccess || hipStreamSynchronize(s.st) != hipSuccess) {
+      (void)hipSetDevice(cur);
+      return set_error("mt_scratch_release: stream synchronize failed");
+    }
+    (void)hipFree(s.buf);
+    (void)hipSetDevice(cur);
+    s.buf = nullptr;
+    s.cap = 0;
+  }
+  return 0;
+}
 
 int mt_tensor_map(int fn, float* out, const int64_t* out_shape, const int64_t* out_strides,
                   int out_dims, const float* in, const int64_t* in_shape,

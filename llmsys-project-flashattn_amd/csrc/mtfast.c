@@ -59,6 +59,13 @@ static PyObject* bind(PyObject* self, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+/* a shape tuple and its strides tuple must have the same length (the library is passed only
+   the shape's rank, so shorter strides would be read past their end) */
+#define SAME_RANK(x, y, what)                                                              \
+  if ((x) != (y))                                                                          \
+    return PyErr_Format(PyExc_ValueError, "_mtfast: %s shape has %d dims, strides %d", what, \
+                        (x), (y));
+
 #define NEED(p)                                                              \
   if (!(p)) {                                                                \
     PyErr_SetString(PyExc_RuntimeError, "_mtfast: entry points not bound"); \
@@ -73,6 +80,8 @@ static PyObject* fmap(PyObject* self, PyObject* const* a, Py_ssize_t n) {
   int64_t os[MAXD], ost[MAXD], as[MAXD], ast[MAXD];
   const int od = tup(a[2], os), od2 = tup(a[3], ost), ad = tup(a[5], as), ad2 = tup(a[6], ast);
   if (od < 0 || od2 < 0 || ad < 0 || ad2 < 0) return NULL;
+  SAME_RANK(od, od2, "out");
+  SAME_RANK(ad, ad2, "input");
   const int fid = (int)PyLong_AsLong(a[0]);
   float* out = (float*)ptr_of(a[1]);
   const float* in = (const float*)ptr_of(a[4]);
@@ -90,6 +99,9 @@ static PyObject* fzip(PyObject* self, PyObject* const* a, Py_ssize_t n) {
   const int od = tup(a[2], os), od2 = tup(a[3], ost), ad = tup(a[5], as), ad2 = tup(a[6], ast);
   const int bd = tup(a[8], bs), bd2 = tup(a[9], bst);
   if (od < 0 || od2 < 0 || ad < 0 || ad2 < 0 || bd < 0 || bd2 < 0) return NULL;
+  SAME_RANK(od, od2, "out");
+  SAME_RANK(ad, ad2, "a");
+  SAME_RANK(bd, bd2, "b");
   const int fid = (int)PyLong_AsLong(a[0]);
   float* out = (float*)ptr_of(a[1]);
   const float* x = (const float*)ptr_of(a[4]);
@@ -107,6 +119,8 @@ static PyObject* freduce(PyObject* self, PyObject* const* a, Py_ssize_t n) {
   int64_t os[MAXD], ost[MAXD], as[MAXD], ast[MAXD];
   const int od = tup(a[2], os), od2 = tup(a[3], ost), ad = tup(a[5], as), ad2 = tup(a[6], ast);
   if (od < 0 || od2 < 0 || ad < 0 || ad2 < 0) return NULL;
+  SAME_RANK(od, od2, "out");
+  SAME_RANK(ad, ad2, "input");
   const int fid = (int)PyLong_AsLong(a[0]);
   float* out = (float*)ptr_of(a[1]);
   const float* in = (const float*)ptr_of(a[4]);

@@ -39,6 +39,8 @@ _PROTOS = {
     "mt_abi_version": (_int, []),
     "mt_flash_set_kernel_policy": (_int, [_int]),
     "mt_flash_get_kernel_policy": (_int, []),
+    "mt_scratch_bytes": (_i64, []),
+    "mt_scratch_release": (_int, []),
     "mt_flash_attn_fwd": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,
                                  _i64p, _i64p, _i64p, _i64p, _vp]),
     "mt_flash_attn_fwd_varlen": (_int, [_int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
@@ -305,6 +307,16 @@ def flash_bwd(q, k, v, o, do, m, l, causal: bool = False, dq=None, dk=None, dv=N
                                      workspace.data_ptr(), workspace.numel() * workspace.element_size(),
                                      st), "mt_flash_attn_bwd_v3")
     return dq, dk, dv
+
+
+def scratch_bytes() -> int:
+    """Device bytes the library's stream scratch holds between calls (mt_scratch_bytes)."""
+    return int(lib().mt_scratch_bytes())
+
+
+def scratch_release() -> None:
+    """Free the library's stream scratch that no captured graph holds (mt_scratch_release)."""
+    check(lib().mt_scratch_release(), "mt_scratch_release")
 
 
 def exported_symbols() -> Sequence[str]:

@@ -31,7 +31,7 @@ t0 = time.time()
 while time.time() - t0 < 0.5:  # clock ramp
     _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l); torch.cuda.synchronize()
 res = {p: [] for p in arms}
-reps = max(3, int(2e12 / flops))
+reps = max(int(os.environ.get("REPS", "3")), int(2e12 / flops))
 for rnd in range(rounds):
     for p in arms:
         if env_vals:

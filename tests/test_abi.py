@@ -174,3 +174,10 @@ def test_mtfast_extension_bound_and_checks_arguments():
         f.map(1, 0, tuple(range(17)), (1,), 0, (4,), (1,), 0)  # more than 16 dims
     with pytest.raises(ValueError):
         f.matmul(0, 0, 0, 1, 2, 2, 2, (4, 2), (4, 2, 1), (4, 2, 1), 0)  # strides not triples
+    # a strides tuple shorter (or longer) than its shape
+    with pytest.raises(ValueError):
+        f.map(1, 0, (2, 4), (4,), 0, (2, 4), (4, 1), 0)
+    with pytest.raises(ValueError):
+        f.zip(1, 0, (4,), (1,), 0, (4,), (1,), 0, (2, 4), (4,), 0)
+    with pytest.raises(ValueError):
+        f.reduce(1, 0, (1,), (1,), 0, (4, 1), (1,), 0, 0.0, 0)

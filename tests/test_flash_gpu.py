@@ -170,6 +170,91 @@ def test_bf16_padded_head_dims(torch_dev, d, causal):
         np.testing.assert_allclose(_np(got), ref, atol=6e-2 * scale, rtol=0, err_msg=name)
 
 
+@pytest.mark.parametrize("cap_heads,causal", [(2, False), (2, True), (6, True)])
+def test_bf16_padded_head_groups(torch_dev, cap_heads, causal, monkeypatch):
+    """The padded head dims run in groups of heads that bound the scratch (capi_flash.hip
+    for_head_groups): with the cap lowered (MT_PAD_SCRATCH_CAP) to 2 heads
+    the groups split the heads of one batch row, with 6 they take two whole batch rows; every
+    group's (m, l) and outputs land at their own offsets of strided views."""
+    from minitorch import _hip
+    torch = torch_dev
+    B, H, N, d, dp = 3, 3, 333, 96, 128
+    rng = np.random.default_rng(11 + cap_heads + causal)
+    q, k, v, do = (A.bf16_round(rng.standard_normal((B, H, N, d)).astype(np.float32)) for _ in range(4))
+    o_ref, m_ref, l_ref = A.attention_fwd(q, k, v, causal)
+    dq_ref, dk_ref, dv_ref = A.attention_bwd(q, k, v, o_ref, do, m_ref, l_ref, causal)
+    tq, tk, tv, tdo = (_dev(torch, np.ascontiguousarray(x.transpose(0, 2, 1, 3)), torch.bfloat16).permute(0, 2, 1, 3)
+                       for x in (q, k, v, do))
+    # forward groups hold 8 bytes per padded element (Q, K, V, bf16 O), the backward 16
+    monkeypatch.setenv("MT_PAD_SCRATCH_CAP", str(cap_heads * N * dp * 8))
+    o, m, l = _hip.flash_fwd(tq, tk, tv, causal)
+    monkeypatch.setenv("MT_PAD_SCRATCH_CAP", str(cap_heads * N * dp * 16))
+    dq, dk, dv = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, causal)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(o), o_ref, atol=2e-2, rtol=0)
+    _check_ml(_np(m), _np(l), m_ref, l_ref, exact=False)
+    scale = max(1.0, float(np.abs(dq_ref).max()), float(np.abs(dk_ref).max()), float(np.abs(dv_ref).max()))
+    for got, ref, name in ((dq, dq_ref, "dq"), (dk, dk_ref, "dk"), (dv, dv_ref, "dv")):
+        np.testing.assert_allclose(_np(got), ref, atol=6e-2 * scale, rtol=0, err_msg=name)
+
+
+def test_bf16_padded_more_heads_than_grid_y(torch_dev):
+    """d = 48 with B*H > 65535 (the padded kernels' grid.y bound) still runs
+    the padded d = 64 kernels, in groups of at most 65535 heads; heads of the first, a middle
+    and the last group against the oracle."""
+    from minitorch import _hip
+    torch = torch_dev
+    B, H, N, d = 1, 65600, 128, 48
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q, k, v, do = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(4))
+    for causal in (False, True):
+        o, m, l = _hip.flash_fwd(q, k, v, causal)
+        dq, dk, dv = _hip.flash_bwd(q, k, v, o, do, m, l, causal)
+        torch.cuda.synchronize()
+        for h in (0, 4095, 4096, 40000, H - 1):
+            qh, kh, vh, doh = (_np(x[:, h:h + 1]) for x in (q, k, v, do))
+            o_ref, m_ref, l_ref = A.attention_fwd(qh, kh, vh, causal)
+            dq_ref, dk_ref, dv_ref = A.attention_bwd(qh, kh, vh, o_ref, doh, m_ref, l_ref, causal)
+            np.testing.assert_allclose(_np(o[:, h:h + 1]), o_ref, atol=2e-2, rtol=0, err_msg=f"O head {h}")
+            _check_ml(_np(m[:, h:h + 1]), _np(l[:, h:h + 1]), m_ref, l_ref, exact=False)
+            scale = max(1.0, float(np.abs(dq_ref).max()), float(np.abs(dk_ref).max()), float(np.abs(dv_ref).max()))
+            for got, ref, name in ((dq, dq_ref, "dq"), (dk, dk_ref, "dk"), (dv, dv_ref, "dv")):
+                np.testing.assert_allclose(_np(got[:, h:h + 1]), ref, atol=6e-2 * scale, rtol=0,
+                                           err_msg=f"{name} head {h} causal={causal}")
+        del o, m, l, dq, dk, dv
+
+
+def test_padded_scratch_bounded(torch_dev):
+    """the padded-d backward at (64,16,16384,96) holds at most 1 GiB of
+    library scratch (it held ≈ 34 GB in round 5), and mt_scratch_release frees it. Two heads
+    of the last group against a torch fp32 autograd reference of the same bf16 inputs."""
+    from minitorch import _hip
+    torch = torch_dev
+    _hip.scratch_release()
+    B, H, N, d = 64, 16, 16384, 96
+    g = torch.Generator(device="cuda").manual_seed(9)
+    q, k, v, do = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(4))
+    o, m, l = _hip.flash_fwd(q, k, v, False)
+    dq, dk, dv = _hip.flash_bwd(q, k, v, o, do, m, l, False)
+    torch.cuda.synchronize()
+    held = _hip.scratch_bytes()
+    assert held <= (1 << 30), f"library scratch {held / 2**30:.2f} GiB after the padded backward"
+    for b, h in ((B - 1, H - 1), (B - 1, 0)):
+        qh, kh, vh = (x[b, h].float().requires_grad_() for x in (q, k, v))
+        p = torch.softmax(qh @ kh.T / d ** 0.5, dim=-1)
+        oh = p @ vh
+        oh.backward(do[b, h].float())
+        assert float((o[b, h].float() - oh).abs().max()) < 2e-2
+        for got, ref, name in ((dq, qh.grad, "dq"), (dk, kh.grad, "dk"), (dv, vh.grad, "dv")):
+            scale = max(1.0, float(ref.abs().max()))
+            err = float((got[b, h].float() - ref).abs().max())
+            assert err < 6e-2 * scale, f"{name} ({b},{h}) max|err| {err:.3g}"
+        del qh, kh, vh, p, oh
+    del q, k, v, do, o, dq, dk, dv
+    _hip.scratch_release()
+    assert _hip.scratch_bytes() <= held
+
+
 def test_strided_views(torch_dev):
     """Q/K/V as permuted views of [B, N, H, d] projections (what MultiHeadAttention
     hands over, reference modules_transfomer.py:88-100): no host-side copy needed."""
