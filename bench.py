@@ -379,6 +379,32 @@ def cpu_baseline(shape, seconds=12.0):
     }
 
 
+def timed_parity(torch, _hip, q, k, v, o, causal, heads=8):
+    """Part of the CPU leg (rank 0, N = 1): the max-abs error of the output the timed region
+    wrote (o, the bf16 forward) and of the fp32-output form of the same forward, on a sample of
+    heads spread over B*H, against the C restatement of the reference's CPU attention
+    (oracle/attn_ref.c, fp32) fed the same bf16 inputs. north_star's bound is a flat 1e-3."""
+    import numpy as np
+    from oracle import cref
+    B, H, N, d = q.shape
+    BH = B * H
+    pick = sorted({int(round(i * (BH - 1) / max(heads - 1, 1))) for i in range(heads)})
+    o32 = torch.empty(q.shape, dtype=torch.float32, device=q.device)
+    _hip.flash_fwd(q, k, v, causal, out=o32)
+    torch.cuda.synchronize()
+    flat = lambda t: t.reshape(BH, N, d)  # noqa: E731
+    idx = torch.tensor(pick, device=q.device)
+    qs, ks, vs = (flat(t).index_select(0, idx).float().cpu().numpy() for t in (q, k, v))
+    ref, _, _ = cref.attn_fwd(qs, ks, vs, causal=causal, nthreads=_cpu_cores()[0])
+    err_bf16 = float(np.abs(flat(o).index_select(0, idx).float().cpu().numpy() - ref).max())
+    err_f32 = float(np.abs(flat(o32).index_select(0, idx).cpu().numpy() - ref).max())
+    del o32
+    return {"bound": 1e-3, "heads": pick, "of_heads": BH,
+            "reference": "oracle/attn_ref.c fp32 on the same bf16 Q/K/V (C restatement of fast_ops attention)",
+            "timed_bf16_out_max_abs": err_bf16, "timed_bf16_out_within_bound": err_bf16 <= 1e-3,
+            "f32_out_max_abs": err_f32, "f32_out_within_bound": err_f32 <= 1e-3}
+
+
 def load_pmc_traffic(tag):
     """HBM bytes per launch (and MFMA-busy fraction, effective clock) of the forward kernel
     from the committed rocprofv3 PMC capture (profiles/pmc_<tag>.json)."""
@@ -651,7 +677,7 @@ def main():
         m, l = ml[key]
         _hip.flash_fwd(q, k, v, causal, out=out, m=m, l=l)
 
-    result, _, _ = run(args, attn_ml, torch, dist, world, rank, f"cuda:{local}", torch.bfloat16)
+    result, o_timed, qkv = run(args, attn_ml, torch, dist, world, rank, f"cuda:{local}", torch.bfloat16)
 
     if rank == 0 and world == 1 and not args.no_extra and args.config == "c3":
         clock = Clock(torch, "cuda")
@@ -675,6 +701,9 @@ def main():
         cpu = cpu_baseline(CONFIGS[args.config])
         cpu["gpu_over_cpu"] = round(result["value"] / cpu["value"], 1) if cpu["value"] > 0 else None
         result["cpu_baseline"] = cpu
+        # the error of what the timed region computed (CPU leg: the oracle as the checker)
+        result["parity"] = timed_parity(torch, _hip, *qkv, o_timed, args.causal,
+                                        heads=128 if args.config == "c3" else 2)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

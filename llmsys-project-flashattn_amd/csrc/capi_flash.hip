@@ -335,7 +335,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
     case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
     case kPolV6Wide:  // diagnostics knobs: 1 the older half's DMA, 2 / 3 priority flips
-      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : a.knob == 4 ? 16384 : a.knob == 7 ? 32768 : 0), st, handled);
+      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : a.knob == 4 ? 16384 : a.knob == 7 ? 32768 : a.knob == 8 ? (16384 | (1 << 20)) : 0), st, handled);
       break;
     case kPolV6Stamp: {
       AttnArgs as = a;
@@ -537,7 +537,15 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       // N % 64 != 0 (round 5): the same v6 with the partial last key tile masked in registers
       // (VAR 65536): (8,16,4000,64) 0.614 ms on v4 against 0.487 ms for N = 4032 on v6
       // (profiles/r5_ab_ragged.txt)
-      if ((int64_t)((N + 511) / 512) * bh >= 256)
+      // Round 6: 4-wave workgroups two per CU (W4, 256 queries each: the two waves of a SIMD
+      // from different workgroups) where that grid keeps two per CU and N % 64 == 0; same-box
+      // interleaved A/Bs against the 8-wave form: C3 +0.9 / +2.0 % (bf16 / fp32 O),
+      // (16,16,2048,64) +7 / +5 %, (4,16,8192,64) +0.8 / +0.3 %, (2,16,16384,64) -0.1 / -0.4 %
+      // (profiles/r6_ab_fwd_w4_noncausal.txt, r6_ab_fwd_onewave.txt); round 4 had measured it
+      // within +-1.3 % (r4_ab_fwd_w4.txt)
+      if (N % 64 == 0 && (int64_t)((N + 255) / 256) * bh >= 512)
+        e = launch_fwd_v6(a, false, 66 | 16384, st, handled);
+      else if ((int64_t)((N + 511) / 512) * bh >= 256)
         e = launch_fwd_v6(a, false, N % 64 ? 66 | 65536 : 66, st, handled);
       if (!*handled) e = launch_fwd_v6(a, false, 18, st, handled);
     } else if ((int64_t)((N + 511) / 512 + 1) / 2 * bh >= 256) {

@@ -29,7 +29,7 @@
 // A/B libraries with -DV6ABL=n (scripts/build_abl.sh fa_fwd_v6 V6ABL n), never into the product: 1 half
 // the K fragment reads (key blocks 2, 3 take blocks 0, 1's fragments with the k-steps swapped, so
 // no MFMA chain repeats another), 2 no row-sum MFMAs, 4 no exponentials, 8 half the Vᵀ fragment
-// reads (profiles/r5_abl_fwd.txt).
+// reads (profiles/r5_abl_fwd.txt), 16 no O stores (the epilogue's store tail, round 6).
 #ifndef V6ABL
 #define V6ABL 0
 #endif
@@ -792,6 +792,18 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
       const float m = blk ? mB[qh] : mA[qh];
       const float inv = 1.f / l;
       const f32x4(&O)[4][2] = blk ? OB : OA;
+      if (V6ABL & 16) {  // timing-only: no O stores (kept live through an improbable store)
+        float t = 0.f;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) t += O[db][qh][0] * inv + O[db][qh][1] + O[db][qh][2] + O[db][qh][3];
+        if (t == 1.2345e-30f) p.l[0] = t;
+        if (q < N && g == 0) {
+          const int64_t row = (int64_t)bh * N + q;
+          if (p.m) p.m[row] = m * p.scale;
+          if (p.l) p.l[row] = l;
+        }
+        continue;
+      }
       if (WIDE && !p.o_f32) {
         // Widened store (cdna_hip_programming.md T21): lane (i, g) holds d 16db + 4g .. + 3;
         // one v_permlane16_swap per dword pairs the 16-lane rows g, g + 1 (even g keeps d block
@@ -858,6 +870,10 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
 // the 31-bit buffer range.
 hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled) {
   *handled = false;
+  // diagnostics (launch bit 1 << 20): the workgroup's LDS padded to 96 KiB, so one workgroup
+  // fits a CU: with W4 that is one wave per SIMD (round 6 A/B of the one-wave form)
+  const bool one_wg = (var & (1 << 20)) != 0;
+  var &= ~(1 << 20);
   const bool split = (var & 16) != 0;  // (var & 64: the widened epilogue stores)
   const bool dual = (var & 256) != 0;   // causal, two 4-wave halves with a pair each
   const bool rg = (var & 65536) != 0;  // any N >= 128
@@ -870,12 +886,13 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
   *handled = true;
   const size_t smem = (size_t)(split || dual ? 2 : 1) * (kKSlots + (var & 512 ? 4 : kVSlots)) * TILE * sizeof(bf16);
   void (*kern)(AttnArgs, int) = nullptr;
-  switch (var) {  // product build: the defaults 66 / 18 / 98 / 610 / 16482; the rest are A/B policies
+  switch (var) {  // product build: the defaults 16450 / 66 / 18 / 98 / 610 / 16482; the rest are A/B policies
     case 66: kern = fa_fwd_bf16_v6<66>; break;
     case 18: kern = fa_fwd_bf16_v6<18>; break;
     case 98: kern = fa_fwd_bf16_v6<98>; break;
     case 610: kern = fa_fwd_bf16_v6<610>; break;  // 98 with fp16 PV (the fp32-output causal default)
     case 16482: kern = fa_fwd_bf16_v6<16482>; break;  // 98 with 4-wave workgroups (the causal default)
+    case 16450: kern = fa_fwd_bf16_v6<16450>; break;  // 66 with 4-wave workgroups (the non-causal default, round 6)
     case 65602: kern = fa_fwd_bf16_v6<65602>; break;  // 66 for any N (the non-causal default for N % 64 != 0)
     case 65634: kern = fa_fwd_bf16_v6<65634>; break;  // 98 for any N
     case 82018: kern = fa_fwd_bf16_v6<82018>; break;  // 16482 for any N (the causal default for N % 64 != 0)
@@ -887,7 +904,6 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
     case 4162: kern = fa_fwd_bf16_v6<4162>; break;  // 66, waves 4-7 at priority 1 for P1-P2
     case 8258: kern = fa_fwd_bf16_v6<8258>; break;  // 66, waves 4-7 at priority 1 for P1
     case 5186: kern = fa_fwd_bf16_v6<5186>; break;  // 4162 with stamps
-    case 16450: kern = fa_fwd_bf16_v6<16450>; break;  // 66 with 4-wave workgroups, two per CU
     case 32834: kern = fa_fwd_bf16_v6<32834>; break;  // 66 with packed scale-and-shift
     case 102: kern = fa_fwd_bf16_v6<102>; break;  // 98 without the Vᵀ reuse (32 VGPRs fewer)
     case 16994: kern = fa_fwd_bf16_v6<16994>; break;  // 610 with 4-wave workgroups
@@ -905,14 +921,15 @@ hipError_t launch_fwd_v6(const AttnArgs& a, bool causal, int var, hipStream_t st
 #endif
     default: return hipErrorInvalidValue;
   }
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  const size_t smem_launch = one_wg && smem < 96 * 1024 ? (size_t)96 * 1024 : smem;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_launch);
   if (e != hipSuccess) return e;
   const bool w4 = (var & 16384) != 0;
   const int bq = split || dual || w4 ? kBQ / 2 : kBQ;
   const int nqb = (a.N + bq - 1) / bq;
   const int64_t nblk = (int64_t)(dual ? nqb / 4 : causal ? (nqb + 1) / 2 : nqb) * a.B * a.H;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(w4 ? 32 * kNW : 64 * kNW), smem, st, a, nqb);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(w4 ? 32 * kNW : 64 * kNW), smem_launch, st, a, nqb);
   return hipGetLastError();
 }
 

@@ -11,7 +11,8 @@ _DIAG = os.path.join(os.path.dirname(_hip.LIB_PATH), "diag", "libminitorch_hip_d
 if os.environ.get("MT_DIAG") == "1":
     assert os.path.exists(_DIAG), "make -C llmsys-project-flashattn_amd DIAG=1"
     _hip.use_library(_DIAG)
-pols = [int(x) for x in sys.argv[1].split(",")]
+# an arm is POL or POL:KNOB (the policy with MT_KNOB=KNOB, read per launch by the diagnostics build)
+pols = [x for x in sys.argv[1].split(",")]
 env_name, env_vals = None, None
 if os.environ.get("ENVAB"):
     env_name, _v = os.environ["ENVAB"].split(":")
@@ -36,9 +37,14 @@ for rnd in range(rounds):
     for p in arms:
         if env_vals:
             os.environ[env_name] = p
-            _hip.set_policy(pols[0])
+            _hip.set_policy(int(pols[0]))
         else:
-            _hip.set_policy(p)
+            pol, _, knob = p.partition(":")
+            if knob:
+                os.environ["MT_KNOB"] = knob
+            else:
+                os.environ.pop("MT_KNOB", None)
+            _hip.set_policy(int(pol))
         for _ in range(2): _hip.flash_fwd(q, k, v, causal, out=o, m=m, l=l)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize(); e0.record()
@@ -49,4 +55,4 @@ _hip.set_policy(0)
 print(f"shape {(B, H, N, d)} {dt} causal={causal} reps={reps} rounds={rounds}")
 for p in arms:
     t = sorted(res[p]); med = t[len(t) // 2]
-    print(f"{(env_name + '=' + p) if env_vals else 'policy %3d' % p}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s", flush=True)
+    print(f"{(env_name + '=' + p) if env_vals else 'policy %6s' % p}: median {med:.4f} ms  min {t[0]:.4f}  -> {flops / med / 1e9:.1f} TF/s", flush=True)
