@@ -548,20 +548,25 @@ static hipError_t fwd_bf16_dispatch(const AttnArgs& a, bool causal, int pol, hip
       else if ((int64_t)((N + 511) / 512) * bh >= 256)
         e = launch_fwd_v6(a, false, N % 64 ? 66 | 65536 : 66, st, handled);
       if (!*handled) e = launch_fwd_v6(a, false, 18, st, handled);
-    } else if ((int64_t)((N + 511) / 512 + 1) / 2 * bh >= 256) {
-      // causal with at least one 8-wave workgroup per CU: paired light / heavy query blocks
-      // with each wave's diagonal inside the pipeline, v6 with the widened epilogue stores
-      // (policy 142: +1.8 % over 106, r3_ab_v6_wide.txt). An fp32 O (MT_BF16_F32OUT) takes the
-      // fp16-PV form (610): P rounded to 11 bits instead of 8, within north_star's flat 1e-3 on
-      // the causal heads. The bf16 output takes 4-wave workgroups (W4, 256
-      // queries, two per CU) where that grid keeps two workgroups per CU: the two waves of a
-      // SIMD then share no barrier (0.2544 vs 0.2598 ms at C3 causal, profiles/r4_ab_fwd_w4.txt).
-      // N % 64 != 0 (round 5): the same forms with the partial last key tile staged (VAR
-      // 65536; its keys past N are past every query, so the diagonal mask hides them), except
-      // the fp32 output's fp16-PV form
-      const bool w4 = !a.o_f32 && (int64_t)((N + 255) / 256 + 1) / 2 * bh >= 512;
+    } else {
+      // causal: paired light / heavy query blocks with each wave's diagonal inside the
+      // pipeline, v6 with the widened epilogue stores (policy 142: +1.8 % over 106,
+      // r3_ab_v6_wide.txt). An fp32 O (MT_BF16_F32OUT) takes the fp16-PV form (610): P rounded
+      // to 11 bits instead of 8, within north_star's flat 1e-3 on the causal heads (DESIGN.md
+      // §4), on grids of at least one 8-wave workgroup per CU. The bf16 output takes 4-wave
+      // workgroups (W4, 256 queries, the two waves of a SIMD share no barrier: 0.2544 vs 0.2598
+      // ms at C3 causal, profiles/r4_ab_fwd_w4.txt) wherever that grid has a workgroup per CU:
+      // round 6 moved that bound from two per CU to one, taking (4,16,2048,64) 666 -> 711,
+      // (2,16,4096,64) 791 -> 838, (1,16,8192,64) 864 -> 927, (8,16,1024,64) 511 -> 519 TF/s
+      // from v4 (profiles/r6_ab_fwd_small_causal.txt). Below that v4's blocks stay ahead
+      // ((1,16,4096,64): 603 vs 443 TF/s). N % 64 != 0 (round 5): the same forms with the
+      // partial last key tile staged (VAR 65536; its keys past N are past every query, so the
+      // diagonal mask hides them), except the fp32 output's fp16-PV form.
+      const int64_t w4grid = (int64_t)((N + 255) / 256 + 1) / 2 * bh;
+      const int64_t w8grid = (int64_t)((N + 511) / 512 + 1) / 2 * bh;
       const int rg = N % 64 ? 65536 : 0;
-      if (!rg || !a.o_f32) e = launch_fwd_v6(a, true, a.o_f32 ? 610 : (w4 ? (98 | 16384) : 98) | rg, st, handled);
+      if (!a.o_f32 && w4grid >= 256) e = launch_fwd_v6(a, true, (98 | 16384) | rg, st, handled);
+      else if (a.o_f32 && !rg && w8grid >= 256) e = launch_fwd_v6(a, true, 610, st, handled);
     }
     // ragged N, short N, small causal grids: v4 (causal: paired, light block first, 8 waves
     // from N = 8192; profiles/r1_ab_causal_pair.txt)

@@ -723,6 +723,27 @@ def test_bf16_bwd_fused_head_groups(torch_dev, causal):
                 f"(2,72,4096,64) causal={causal}")
 
 
+@pytest.mark.parametrize("shape", [(4, 16, 2048, 64), (8, 16, 1024, 64), (2, 16, 4032, 64), (1, 16, 8192, 64)])
+def test_causal_w4_small_grids(torch_dev, shape, parity_record):
+    """Round 6: the bf16 causal default takes W4 (4-wave workgroups, paired light / heavy
+    256-query blocks) down to one workgroup per CU, where v4 ran before: heads at both ends of
+    the grid against the C oracle at the elementwise bf16 bound, (m, l) included; N = 4032 has a
+    partial last key tile."""
+    from minitorch import _hip
+    torch = torch_dev
+    B, H, N, d = shape
+    g = torch.Generator(device="cuda").manual_seed(N + B)
+    q, k, v = (torch.randn(shape, device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
+    o, m, l = _hip.flash_fwd(q, k, v, True)
+    torch.cuda.synchronize()
+    heads = [(0, 0), (B - 1, H - 1)]
+    err, _ = _subset_check_fwd(torch, q, k, v, o, True, heads, 1e-3, 2.0 ** -7)
+    for (b, h) in heads:
+        _, m_ref, l_ref = cref.attn_fwd(_np(q[b, h])[None], _np(k[b, h])[None], _np(v[b, h])[None], True)
+        _check_ml(_np(m[b, h]), _np(l[b, h]), m_ref[0], l_ref[0], exact=False)
+    parity_record("test_causal_w4_small_grids", f"{shape} bf16 causal O (bf16 out)", max_abs=err)
+
+
 @pytest.mark.parametrize("d", [64, 128])
 def test_long_causal_paired_default(torch_dev, d):
     """Causal default at long N (d = 64: 8-wave v4 from N = 8192; d = 128: 8-wave d128),
