@@ -5,7 +5,11 @@
     python bench.py --gpus N --steps K --warmup W [--config c3|c4] [--split strong|weak]
 
 One "step" = one pass of the hot path (the bf16 MFMA forward kernel) over this rank's
-shard of the workload, with synthetic Q/K/V already resident in HBM. Multi-GPU: one
+shard of the workload, with synthetic Q/K/V already resident in HBM. Since round 6 the timed
+form writes an fp32 O (bf16 Q/K/V, bf16 MFMAs with fp32 accumulation, O without a final
+bf16 rounding: MT_BF16_F32OUT), the form that meets north_star's flat 1e-3 max-abs against
+the CPU reference on every head; --out bf16 times the bf16-O form, whose rounding of O alone
+is up to 9.8e-4 where |O| reaches 0.5 (its throughput is in "extra"). Multi-GPU: one
 process per GPU (torch.distributed.run, RCCL). The flattened batch x heads axis is
 sharded into contiguous per-rank ranges (every (b,h) head is
 independent, so there is no collective on the data path):
@@ -68,9 +72,11 @@ def fwd_flops(B, H, N, d, causal=False):
     return f / 2 if causal else f
 
 
-def fwd_bytes(B, H, N, d, esize=2):
-    # read Q, K, V + write O, plus the fp32 row statistics m and l
-    return 4.0 * B * H * N * d * esize + 2.0 * B * H * N * 4
+def fwd_bytes(B, H, N, d, esize=2, out_esize=None):
+    # read Q, K, V + write O (out_esize bytes per element; default: the input size), plus the
+    # fp32 row statistics m and l
+    oe = esize if out_esize is None else out_esize
+    return (3.0 * esize + oe) * B * H * N * d + 2.0 * B * H * N * 4
 
 
 # ---- sharding plan -------------------------------------------------------------------
@@ -161,16 +167,18 @@ def _timed_region(torch, clock, dist, world, fn, steps):
     return wall, dev_ms, own_ms
 
 
-def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2):
+def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2, out_esize=None):
     """The bench's timed legs for this rank. attn_fwd(q, k, v, causal, out) runs the hot
-    path on a shard. Returns the result dict (rank 0 prints it) and, for tests, the
-    gathered output (N > 1) or this rank's output."""
+    path on a shard; out_esize 4 with bf16 inputs: an fp32 O (the headline form since round
+    6, MT_BF16_F32OUT: the one that meets north_star's flat 1e-3). Returns the result dict
+    (rank 0 prints it) and, for tests, the gathered output (N > 1) or this rank's output."""
+    out_esize = esize if out_esize is None else out_esize
     base = CONFIGS[args.config] if args.shape is None else tuple(args.shape)
     split = "strong" if args.config == "c4" else args.split
     plan = shard_plan(base, world, rank, split)
     gshape, sshape = plan["global_shape"], plan["shard_shape"]
     q, k, v = (make_shard(torch, sshape, plan["bh_lo"], dtype, s, device) for s in (1, 2, 3))
-    o = torch.empty_like(q)
+    o = torch.empty_like(q, dtype=torch.float32 if out_esize == 4 else dtype)
     clock = Clock(torch, device)
 
     def step():
@@ -196,8 +204,9 @@ def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2):
     value = total_flops / wall / 1e12
     flops_rank = fwd_flops(*sshape, args.causal)
     achieved = flops_rank / (kern_ms * 1e-3) / 1e12
-    alg_bytes = fwd_bytes(*sshape, esize=esize)
-    tag = ("fwd_bf16_c4" if args.config == "c4" else "fwd_bf16_c3") + ("_causal" if args.causal else "")
+    alg_bytes = fwd_bytes(*sshape, esize=esize, out_esize=out_esize)
+    tag = (("fwd_bf16_c4" if args.config == "c4" else "fwd_bf16_c3") + ("_causal" if args.causal else "")
+           + ("_f32out" if esize == 2 and out_esize == 4 else ""))
     traffic, traffic_src, pmc_extra = load_pmc_traffic(tag) if world == 1 else (None, None, {})
 
     result = {
@@ -216,8 +225,9 @@ def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2):
         "data": "synthetic N(0,1) Q/K/V (counter-seeded per global head), resident in HBM",
         "config": {"workload": f"flash_attention_fwd {args.config}", "B": B, "H": H, "N": N,
                    "d": d, "per_gpu_shape": list(sshape), "causal": bool(args.causal),
+                   "output": "fp32 O" if out_esize == 4 else ("bf16 O" if esize == 2 else "fp32 O"),
                    "parallelism": f"bh-shard x{world} ({split})"},
-        "hbm_gbps": round(fwd_bytes(B, H, N, d, esize) * args.steps / wall / 1e9, 2),
+        "hbm_gbps": round(fwd_bytes(B, H, N, d, esize, out_esize) * args.steps / wall / 1e9, 2),
         "roofline": {
             "bound": "mfma",
             "achieved": round(achieved, 2),
@@ -381,28 +391,31 @@ def cpu_baseline(shape, seconds=12.0):
 
 def timed_parity(torch, _hip, q, k, v, o, causal, heads=8):
     """Part of the CPU leg (rank 0, N = 1): the max-abs error of the output the timed region
-    wrote (o, the bf16 forward) and of the fp32-output form of the same forward, on a sample of
-    heads spread over B*H, against the C restatement of the reference's CPU attention
-    (oracle/attn_ref.c, fp32) fed the same bf16 inputs. north_star's bound is a flat 1e-3."""
+    wrote (o: the fp32-output forward by default) and of the other output form of the same
+    forward (bf16 O), on `heads` heads spread over B*H (C3: all 128), against the C
+    restatement of the reference's CPU attention (oracle/attn_ref.c, fp32) fed the same bf16
+    inputs. north_star's bound is a flat 1e-3."""
     import numpy as np
     from oracle import cref
     B, H, N, d = q.shape
     BH = B * H
     pick = sorted({int(round(i * (BH - 1) / max(heads - 1, 1))) for i in range(heads)})
-    o32 = torch.empty(q.shape, dtype=torch.float32, device=q.device)
-    _hip.flash_fwd(q, k, v, causal, out=o32)
+    other_dtype = torch.bfloat16 if o.dtype == torch.float32 else torch.float32
+    o2 = torch.empty(q.shape, dtype=other_dtype, device=q.device)
+    _hip.flash_fwd(q, k, v, causal, out=o2)
     torch.cuda.synchronize()
     flat = lambda t: t.reshape(BH, N, d)  # noqa: E731
     idx = torch.tensor(pick, device=q.device)
     qs, ks, vs = (flat(t).index_select(0, idx).float().cpu().numpy() for t in (q, k, v))
     ref, _, _ = cref.attn_fwd(qs, ks, vs, causal=causal, nthreads=_cpu_cores()[0])
-    err_bf16 = float(np.abs(flat(o).index_select(0, idx).float().cpu().numpy() - ref).max())
-    err_f32 = float(np.abs(flat(o32).index_select(0, idx).cpu().numpy() - ref).max())
-    del o32
-    return {"bound": 1e-3, "heads": pick, "of_heads": BH,
+    err = float(np.abs(flat(o).index_select(0, idx).float().cpu().numpy() - ref).max())
+    err2 = float(np.abs(flat(o2).index_select(0, idx).float().cpu().numpy() - ref).max())
+    del o2
+    name = lambda t: "fp32 O" if t == torch.float32 else "bf16 O"  # noqa: E731
+    return {"bound": 1e-3, "heads_checked": len(pick), "of_heads": BH,
             "reference": "oracle/attn_ref.c fp32 on the same bf16 Q/K/V (C restatement of fast_ops attention)",
-            "timed_bf16_out_max_abs": err_bf16, "timed_bf16_out_within_bound": err_bf16 <= 1e-3,
-            "f32_out_max_abs": err_f32, "f32_out_within_bound": err_f32 <= 1e-3}
+            "timed_form": name(o.dtype), "timed_max_abs": err, "timed_within_bound": err <= 1e-3,
+            "other_form": name(other_dtype), "other_max_abs": err2, "other_within_bound": err2 <= 1e-3}
 
 
 def load_pmc_traffic(tag):
@@ -431,6 +444,10 @@ def extra_legs(torch, _hip, time_fn):
     l = torch.empty_like(m)
     extra["fwd_causal_tflops"] = round(fwd_flops(B, H, N, d, True) / (time_fn(
         lambda: _hip.flash_fwd(q, k, v, True, out=o, m=m, l=l), 20, 3) * 1e-3) / 1e12, 2)
+    # the bf16-output form of the headline (O rounded to bf16: half an ulp of |O| up to 0.5 is
+    # already 9.8e-4, so it cannot meet north_star's flat 1e-3 on every head)
+    extra["fwd_bf16out_tflops"] = round(fwd_flops(B, H, N, d) / (time_fn(
+        lambda: _hip.flash_fwd(q, k, v, False, out=o, m=m, l=l), 20, 3) * 1e-3) / 1e12, 2)
     # the fp32-output forms (MT_BF16_F32OUT: bf16 Q/K/V, O without its final bf16 rounding),
     # the configuration that meets north_star's flat 1e-3 on every C3 head, causal included
     o32 = torch.empty(q.shape, dtype=torch.float32, device="cuda")
@@ -639,6 +656,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra (bwd, fp32) legs")
     ap.add_argument("--policy", type=int, default=0, help="kernel policy (0 default)")
+    ap.add_argument("--out", choices=("f32", "bf16"), default="f32",
+                    help="the timed forward's O: f32 (default, MT_BF16_F32OUT: within north_star's "
+                         "flat 1e-3) or bf16")
     ap.add_argument("--chunks", type=int, default=None,
                     help="end-to-end leg: chunks of the rank's rows whose all-gather overlaps "
                          "the next chunk's forward (default: minitorch.shard.occupancy_chunks, "
@@ -677,7 +697,8 @@ def main():
         m, l = ml[key]
         _hip.flash_fwd(q, k, v, causal, out=out, m=m, l=l)
 
-    result, o_timed, qkv = run(args, attn_ml, torch, dist, world, rank, f"cuda:{local}", torch.bfloat16)
+    result, o_timed, qkv = run(args, attn_ml, torch, dist, world, rank, f"cuda:{local}", torch.bfloat16,
+                               esize=2, out_esize=4 if args.out == "f32" else 2)
 
     if rank == 0 and world == 1 and not args.no_extra and args.config == "c3":
         clock = Clock(torch, "cuda")
