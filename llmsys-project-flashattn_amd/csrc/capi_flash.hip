@@ -171,7 +171,7 @@ namespace v5 {
 [[maybe_unused]] constexpr int kUnroll = 4, kDma = 1024, kW8 = 2048, kPrio = 4096, kScalar = 8192,
               kStagger = 16384, kVKeep = 32768, kDefer = 65536, kSplit = 131072, kRowSumMfma = 262144,
               kAsmDma = 524288;
-constexpr int kDefault = kW8 | kDefer | kVKeep | kDma | kUnroll;
+[[maybe_unused]] constexpr int kDefault = kW8 | kDefer | kVKeep | kDma | kUnroll;
 }  // namespace v5
 
 int set_error(const char* fmt, ...) {

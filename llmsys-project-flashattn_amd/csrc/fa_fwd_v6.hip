@@ -33,6 +33,14 @@
 #ifndef V6ABL
 #define V6ABL 0
 #endif
+// The epilogue's O stores are non-temporal (round 6): O is written once and never read by
+// this kernel, and the 'nt' policy keeps it from displacing the K/V tiles other workgroups of
+// the XCD are still streaming through L2. Same-process A/B against the plain stores
+// (profiles/r6_ab_fwd_nt_store.txt): C3 fp32 O 1121 -> 1142 TF/s, (16,16,2048,64) fp32 O
+// 1049 -> 1062, bf16 O +0.3 % / +1.1 %.
+#ifndef V6NT
+#define V6NT 1
+#endif
 
 namespace mt {
 
@@ -818,12 +826,22 @@ __global__ __launch_bounds__(64 * kNW, 1) void fa_fwd_bf16_v6(AttnArgs p, int nq
           const uint2 uy = __builtin_bit_cast(uint2, bf16x4{(bf16)(y[0] * inv), (bf16)(y[1] * inv), (bf16)(y[2] * inv), (bf16)(y[3] * inv)});
           const auto rx = __builtin_amdgcn_permlane16_swap(ux.x, uy.x, false, false);
           const auto ry = __builtin_amdgcn_permlane16_swap(ux.y, uy.y, false, false);
-          if (q < N) *(uint4*)(Ob + 32 * k + 16 * (g & 1) + 4 * (g & 2)) = uint4{rx[0], ry[0], rx[1], ry[1]};
+          if (q < N) {
+            u32x4* dst = (u32x4*)(Ob + 32 * k + 16 * (g & 1) + 4 * (g & 2));
+            const u32x4 val = {rx[0], ry[0], rx[1], ry[1]};
+            if (V6NT) __builtin_nontemporal_store(val, dst);
+            else *dst = val;
+          }
         }
       }
       if (q < N) {
         const ORow Og = o_row(p, b, hh, q);
-        if (!WIDE || p.o_f32) {
+        if (V6NT && p.o_f32) {
+#pragma unroll
+          for (int db = 0; db < 4; ++db)
+            __builtin_nontemporal_store(f32x4{O[db][qh][0] * inv, O[db][qh][1] * inv, O[db][qh][2] * inv,
+                                              O[db][qh][3] * inv}, (f32x4*)((float*)Og.p + 16 * db + 4 * g));
+        } else if (!WIDE || p.o_f32) {
 #pragma unroll
           for (int db = 0; db < 4; ++db)
             store4(Og, 16 * db + 4 * g, O[db][qh][0] * inv, O[db][qh][1] * inv, O[db][qh][2] * inv,
