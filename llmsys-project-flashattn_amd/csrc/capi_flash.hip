@@ -335,7 +335,7 @@ static hipError_t fwd_bf16_dispatch_ab(const AttnArgs& a, bool causal, int pol, 
     case kPolV6RowSumEven: e = launch_fwd_v6(a, causal, 10, st, handled); break;
     case kPolV6Split: e = launch_fwd_v6(a, causal, 18, st, handled); break;
     case kPolV6Wide:  // diagnostics knobs: 1 the older half's DMA, 2 / 3 priority flips
-      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : a.knob == 4 ? 16384 : a.knob == 7 ? 32768 : a.knob == 8 ? (16384 | (1 << 20)) : 0), st, handled);
+      e = launch_fwd_v6(a, causal, 66 | (a.knob == 1 ? 2048 : a.knob == 2 ? 4096 : a.knob == 3 ? 8192 : a.knob == 4 ? 16384 : a.knob == 7 ? 32768 : a.knob == 8 ? (16384 | (1 << 20)) : a.knob == 9 ? 65536 : 0), st, handled);
       break;
     case kPolV6Stamp: {
       AttnArgs as = a;
