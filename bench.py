@@ -287,7 +287,7 @@ def run(args, attn_fwd, torch, dist, world, rank, device, dtype, esize=2, out_es
             for c in range(chunks):
                 lo = chunk_rows(BHg, world, rank, chunks, c)[0]
                 qc, kc, vc = (make_shard(torch, (1, rc, N, d), lo, dtype, s_, device) for s_ in (1, 2, 3))
-                pieces.append((qc, kc, vc, torch.empty_like(qc)))
+                pieces.append((qc, kc, vc, torch.empty_like(qc, dtype=o.dtype)))
             gathered_c = torch.empty_like(gathered)
 
             def step_overlap():

@@ -50,18 +50,20 @@ def test_make_shard_is_slice_of_global():
 
 def _oracle_attn(q, k, v, causal, out):
     from oracle import attention as A
-    o, _, _ = A.attention_fwd(q.numpy(), k.numpy(), v.numpy(), causal)
+    o, _, _ = A.attention_fwd(q.float().numpy(), k.float().numpy(), v.float().numpy(), causal)
     out.copy_(torch.from_numpy(o))
 
 
-def _worker(rank, world, port, argv, q_out):
+def _worker(rank, world, port, argv, q_out, bf16_in=False):
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=world)
         args = bench.parse_args(argv)
+        # bf16_in: the headline's types (bf16 Q/K/V, fp32 O); else fp32 throughout
         res, gathered, _ = bench.run(args, _oracle_attn, torch, dist, world, rank, "cpu",
-                                     torch.float32, esize=4)
-        q_out.put((rank, res, gathered.numpy()))
+                                     torch.bfloat16 if bf16_in else torch.float32,
+                                     esize=2 if bf16_in else 4, out_esize=4)
+        q_out.put((rank, res, gathered.float().numpy()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # surface the failure in the parent
@@ -69,11 +71,11 @@ def _worker(rank, world, port, argv, q_out):
         q_out.put((rank, "error", traceback.format_exc() + repr(e)))
 
 
-def _run_world(world, argv):
+def _run_world(world, argv, bf16_in=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, argv, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, argv, q, bf16_in)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -180,3 +182,17 @@ def test_bench_world8_chunked_and_unchunked_bitwise():
             assert res["end_to_end"]["chunks"] == chunks
         for r in range(8):
             np.testing.assert_array_equal(out[r][1].reshape(ref.shape), ref)
+
+
+def test_bench_bf16_in_fp32_out_chunked_world2():
+    """The headline's types through the N > 1 legs: bf16 Q/K/V shards, fp32 O, the overlapped
+    chunked all-gather (its pieces' O must be fp32 like the gathered tensor) and the serial one;
+    the gathered output equals world 1's bitwise."""
+    shape = (2, 4, 48, 16)
+    argv = ["--gpus", "2", "--steps", "2", "--warmup", "1", "--chunks", "2", "--shape", *map(str, shape)]
+    out2 = _run_world(2, argv, bf16_in=True)
+    res, gathered = out2[0]
+    assert res["end_to_end"]["chunks"] == 2 and res["config"]["output"] == "fp32 O"
+    assert res["roofline"]["algorithmic_bytes"] == bench.fwd_bytes(1, 4, 48, 16, 2, 4)
+    out1 = _run_world(1, ["--gpus", "1", "--steps", "2", "--warmup", "1", "--shape", *map(str, shape)], bf16_in=True)
+    np.testing.assert_array_equal(gathered.reshape(-1), out1[0][1].reshape(-1))
