@@ -1177,6 +1177,14 @@ static hipError_t launch_bwd_bf16_t(const AttnArgs& a, int variant, hipStream_t 
 
 hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st);
 
+// the d = 128 prep as its own launch (the passes' forms that do not form the row constants)
+hipError_t launch_prep_d128(const AttnArgs& a, hipStream_t st) {
+  constexpr int rpp = 256 / 16;
+  hipLaunchKernelGGL(fa_bwd_prep_bf16<128>, dim3((unsigned)((a.N + rpp * kPrepRows - 1) / (rpp * kPrepRows)), (unsigned)(a.B * a.H)),
+                     dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 // bf16, d = 64 / 128, every per-head row offset of Q/K/V/dO (plus one tile past N) inside the
 // 31-bit buffer range; otherwise the caller falls back to the generic kernels. d = 128: the
 // split form on the 16x16x32 MFMA (fa_bwd_d128.hip; no key padding).
@@ -1188,11 +1196,6 @@ hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStrea
       if (((int64_t)a.N + 64) * s * 2 >= lim) return hipSuccess;
     if ((int64_t)a.B * a.H > 65535 || (int64_t)a.B * a.H * a.N * 4 >= lim) return hipSuccess;
     *handled = true;
-    constexpr int rpp = 256 / 16;
-    hipLaunchKernelGGL(fa_bwd_prep_bf16<128>, dim3((unsigned)((a.N + rpp * kPrepRows - 1) / (rpp * kPrepRows)), (unsigned)(a.B * a.H)),
-                       dim3(256), 0, st, a);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
     return launch_bwd_d128_passes(a, causal, st);
   }
   if (a.d != 64) return hipSuccess;

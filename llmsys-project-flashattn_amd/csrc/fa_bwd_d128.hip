@@ -411,7 +411,11 @@ __global__ __launch_bounds__(512, 2) void fa_bwd_d128_bf16(AttnArgs p, int nblk_
 // 2 no softmax (scores packed as they are), 4 no staging in the tile loop
 // NWV: waves per workgroup (4: one per SIMD; 8: two per SIMD, 256 stationary rows, for a
 // kernel that fits 256 registers)
-template <int MODE, bool CAUSAL, bool PAIR = false, bool PK = true, int ABL = 0, int AH = 7, int NWV = 4>
+// PREP (MODE 1): the pass forms the row constants of its stationary queries itself (the prep
+// kernel's −lse2/c2 and −δ = −rowsum(dO ∘ O)) and writes them for the dK/dV pass, which then
+// runs second; no prep launch
+template <int MODE, bool CAUSAL, bool PAIR = false, bool PK = true, int ABL = 0, int AH = 7, int NWV = 4,
+          bool PREP = false>
 __global__ __launch_bounds__(64 * NWV, NWV / 4) void fa_bwd_d128w_bf16(AttnArgs p, int nblk_head) {
   constexpr int kImgB = img_bytes(kT), kSlotB = slot_bytes(kT);
   constexpr int kWw = 32;     // stationary rows per wave
@@ -499,9 +503,24 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void fa_bwd_d128w_bf16(AttnArgs 
       xf1[sg][ks] = *(const bf16x8*)(X1 + (int64_t)rr * sx1 + 32 * ks + 8 * g);
       xf2[sg][ks] = *(const bf16x8*)(X2 + (int64_t)rr * sx2 + 32 * ks + 8 * g);
     }
-    if (MODE == 1 && my[sg] < N) {
+    if (MODE == 1 && !PREP && my[sg] < N) {
       nl[sg] = p.lse2[(int64_t)bh * N + my[sg]];
       nd[sg] = p.delta[(int64_t)bh * N + my[sg]];
+    }
+  }
+  // PREP: the forward's O rows and (m, l) of the stationary queries, in flight across the first
+  // tiles' staging; the row constants are formed after it (below)
+  bf16x8 of[2][4];
+  float pm[2] = {0.f, 0.f}, pl[2] = {1.f, 1.f};
+  if (MODE == 1 && PREP) {
+    const bf16* Og = (const bf16*)p.o + b * p.so[0] + hh * p.so[1];
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+      const int rr = min(my[sg], N - 1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) of[sg][ks] = *(const bf16x8*)(Og + (int64_t)rr * p.so[2] + 32 * ks + 8 * g);
+      pm[sg] = p.m[(int64_t)bh * N + rr];
+      pl[sg] = p.l[(int64_t)bh * N + rr];
     }
   }
   // (waited here, not at first use inside the loop: see the form above)
@@ -509,7 +528,7 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void fa_bwd_d128w_bf16(AttnArgs 
   for (int sg = 0; sg < 2; ++sg) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(xf1[sg][ks]), "v"(xf2[sg][ks]));
-    asm volatile("" ::"v"(nl[sg]), "v"(nd[sg]));
+    if (!PREP) asm volatile("" ::"v"(nl[sg]), "v"(nd[sg]));
   }
 
   const int ntile_all = (N + kT - 1) / kT;
@@ -528,6 +547,30 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void fa_bwd_d128w_bf16(AttnArgs 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  if (MODE == 1 && PREP) {
+    // the prep kernel's row constants from the stationary dO fragments: the four lanes g of a
+    // row hold its columns 32 ks + 8 g .. + 7, so δ is their sum over ks, then across g; written
+    // for the dK/dV pass, which runs after this one
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+      float acc = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += (float)of[sg][ks][j] * (float)xf2[sg][ks][j];
+      acc += __shfl_xor(acc, 16);
+      acc += __shfl_xor(acc, 32);
+      if (my[sg] < N) {
+        nd[sg] = -acc;
+        nl[sg] = -(pm[sg] * kLog2e + log2f(pl[sg])) / p.scale_log2;
+        if (g == 0) {
+          const int64_t row = (int64_t)bh * N + my[sg];
+          p.delta[row] = nd[sg];
+          p.lse2[row] = nl[sg];
+        }
+      }
+    }
+  }
 
   constexpr int kNA = MODE == 0 ? 16 : 8;
   constexpr int kL = 32 + 2 * kNA;
@@ -979,8 +1022,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_d128x_bf16(AttnArgs p, int nblk
   }  // pass
 }
 
-// The two passes after the d = 128 prep (fa_bwd_prep_bf16<128>). bf16, d = 128, 16-B rows,
-// every per-head row offset (plus one tile past N) inside the 31-bit buffer range.
+hipError_t launch_prep_d128(const AttnArgs& a, hipStream_t st);  // fa_bwd_bf16.hip
+
+// The d = 128 backward: the dQ pass (forming the row constants) then the dK/dV pass, or, for the
+// diagnostics forms without PREP, the prep kernel (fa_bwd_prep_bf16<128>) and the two passes.
+// bf16, d = 128, 16-B rows, every per-head row offset (plus one tile past N) inside the 31-bit
+// buffer range.
 hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st) {
   const int nbh = (a.N + kBR - 1) / kBR;
   // causal: light / heavy pairs while the paired grid keeps a workgroup per CU
@@ -1003,14 +1050,24 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
   const int nbh8 = (a.N + 255) / 256;
   bool q8 = !causal && (int64_t)nbh8 * a.B * a.H >= 256;
   bool q8p = causal && (int64_t)((nbh8 + 1) / 2) * a.B * a.H >= 256;
-  void (*kq)(AttnArgs, int) = q8p ? fa_bwd_d128w_bf16<1, true, true, true, 0, 2, 8>
-                              : pair ? fa_bwd_d128w_bf16<1, true, true>
-                              : causal ? fa_bwd_d128w_bf16<1, true>
-                              : q8 ? fa_bwd_d128w_bf16<1, false, false, true, 0, 3, 8> : fa_bwd_d128w_bf16<1, false>;
+  // the product's dQ pass forms the row constants itself (PREP) and runs first, the dK/dV pass
+  // reads them second: no prep launch (its 51 µs at (8,16,4096,128) read O and dO once more)
+  void (*kq)(AttnArgs, int) = q8p ? fa_bwd_d128w_bf16<1, true, true, true, 0, 2, 8, true>
+                              : pair ? fa_bwd_d128w_bf16<1, true, true, true, 0, 7, 4, true>
+                              : causal ? fa_bwd_d128w_bf16<1, true, false, true, 0, 7, 4, true>
+                              : q8 ? fa_bwd_d128w_bf16<1, false, false, true, 0, 3, 8, true>
+                                   : fa_bwd_d128w_bf16<1, false, false, true, 0, 7, 4, true>;
+  void (*const kq_prep)(AttnArgs, int) = kq;
   bool wd = true, wq = true;
   int kt_d = 64, kt_q = 64;
 #ifdef MT_DIAGNOSTICS
-  void (*const kq_product)(AttnArgs, int) = kq;
+  // knob 54: the round-4 order (prep kernel, dK/dV pass, dQ pass without PREP)
+  if (a.knob == 54)
+    kq = q8p ? fa_bwd_d128w_bf16<1, true, true, true, 0, 2, 8>
+         : pair ? fa_bwd_d128w_bf16<1, true, true>
+         : causal ? fa_bwd_d128w_bf16<1, true>
+         : q8 ? fa_bwd_d128w_bf16<1, false, false, true, 0, 3, 8> : fa_bwd_d128w_bf16<1, false>;
+  void (*const kq_product)(AttnArgs, int) = a.knob == 54 ? kq : kq_prep;
   // knob 50: the dQ pass in the 4-wave form at any grid
   if (a.knob == 50) kq = pair ? fa_bwd_d128w_bf16<1, true, true> : causal ? fa_bwd_d128w_bf16<1, true> : fa_bwd_d128w_bf16<1, false>;
   // the two-wave form (knob 34: both passes; 12 / 14 / 15: with operand reads 2 / 4 / 5 MFMA
@@ -1098,7 +1155,13 @@ hipError_t launch_bwd_d128_passes(const AttnArgs& a, bool causal, hipStream_t st
 #endif
   const int nbh_q = (q8 || q8p) ? nbh8 : nbh;
   const int64_t nblk_q = q8 ? (int64_t)nbh8 * a.B * a.H : q8p ? (int64_t)((nbh8 + 1) / 2) * a.B * a.H : nblk;
-  for (int pass = 0; pass < 2; ++pass) {
+  const bool prep_in_dq = kq == kq_prep;
+  if (!prep_in_dq) {
+    const hipError_t e = launch_prep_d128(a, st);
+    if (e != hipSuccess) return e;
+  }
+  for (int step = 0; step < 2; ++step) {
+    const int pass = prep_in_dq ? 1 - step : step;  // 1 = the dQ pass
     void (*k)(AttnArgs, int) = pass ? kq : kd;
     const bool w = pass ? wq : wd;
     const int smem = w ? 3 * slot_bytes(kT) : smem_bytes(pass ? kt_q : kt_d);
