@@ -31,8 +31,9 @@ hipError_t launch_fwd_d128(const AttnArgs& a, bool causal, int nw, bool dma, hip
 hipError_t launch_fwd_d128v2(const AttnArgs& a, bool causal, int var, hipStream_t st, bool* handled);
 hipError_t launch_bwd_bf16(const AttnArgs& a, bool causal, int variant, hipStream_t st, bool* handled);
 hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool causal,
-                              hipStream_t st, int pair, bool ring);
+                              hipStream_t st, int pair, bool ring, int64_t fused_slab);
 int64_t bwd_fused_ws_bytes(int64_t B, int64_t H, int64_t N);
+int64_t ring_fused_ws_bytes(int64_t B, int64_t H, int64_t N);
 int64_t bwd_fused_abi2_bytes(int64_t B, int64_t H, int64_t N);
 #ifdef MT_DIAGNOSTICS
 hipError_t launch_fwd_v4_deep(const AttnArgs& a, bool causal, bool pk, hipStream_t st);
@@ -712,10 +713,17 @@ static int64_t bwd_rows_bytes(int64_t B, int64_t H, int64_t N) {
   return (2 * B * H * N * (int64_t)sizeof(float) + 255) / 256 * 256;
 }
 
+// the workspace region after the rows where d = 64 (or a padded width 64) runs a fused pass: the
+// bf16 pass's counters and partials, or the fp32 ring pass's partials (fa_bwd_ring.hip), whichever
+// is larger (the size function does not know the dtype)
+static int64_t bwd_fused_region_bytes(int64_t B, int64_t H, int64_t N) {
+  return std::max(bwd_fused_ws_bytes(B, H, N), ring_fused_ws_bytes(B, H, N));
+}
+
 int64_t mt_flash_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t d) {
   // a padded head dim (pad_dim) runs the kernels of its padded width
   const int64_t de = pad_dim(d) ? pad_dim(d) : d;
-  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(B, H, N, de) ? bwd_fused_ws_bytes(B, H, N) : 0);
+  return bwd_rows_bytes(B, H, N) + (fused_bwd_applies(B, H, N, de) ? bwd_fused_region_bytes(B, H, N) : 0);
 }
 
 static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void* k, const void* v,
@@ -766,6 +774,16 @@ static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void*
   const bool slab_ok = fused_bwd_applies(B, H, N, d) &&
                        (checked || (N <= 8192 && bwd_fused_ws_bytes(B, H, N) <= bwd_fused_abi2_bytes(B, H, N)));
   a.slab = slab_ok ? (char*)workspace + bwd_rows_bytes(B, H, N) : nullptr;
+  // fp32, 32 < d <= 64: the same region holds the fused ring backward's dQ partials (the
+  // workspace size reserves it for the padded width 64; the legacy unchecked entries only at
+  // d = 64, as above)
+  int64_t f32_slab = 0;
+  if (dtype == MT_F32 && d > 32 && d <= 64 && (d == 64 || (checked && pad_dim(d) == 64)) &&
+      fused_bwd_applies(B, H, N, 64) &&
+      (checked || (N <= 8192 && bwd_fused_ws_bytes(B, H, N) <= bwd_fused_abi2_bytes(B, H, N)))) {
+    a.slab = (char*)workspace + bwd_rows_bytes(B, H, N);
+    f32_slab = checked ? bwd_fused_region_bytes(B, H, N) : bwd_fused_abi2_bytes(B, H, N);
+  }
   int64_t* dst[8] = {a.sq, a.sk, a.sv, a.so, a.sdo, a.sdq, a.sdk, a.sdv};
   for (int i = 0; i < 8; ++i) fill_strides(dst[i], strides ? strides + 3 * i : nullptr, H, N, d);
   a.B = (int)B; a.H = (int)H; a.N = (int)N; a.d = (int)d;
@@ -864,9 +882,15 @@ static int flash_attn_bwd_impl(int dtype, int causal, const void* q, const void*
     const hipError_t e = launch_bwd_bf16(a, causal != 0, variant, (hipStream_t)stream, &handled);
     if (handled) return check_hip(e, "mt_flash_attn_bwd(bf16)");
   }
+  // the fused fp32 ring backward (dQ in the dK/dV pass) only under the default policy: the
+  // pairing / LDS-row policies keep selecting the split kernels they name
+  bool f32_fused = pol == kPolDefault && f32_slab > 0;
+#ifdef MT_DIAGNOSTICS
+  if (a.knob == 60) f32_fused = false;  // A/B: the split ring backward
+#endif
   return check_hip(launch_bwd_generic(a, dtype == MT_BF16, vec, causal != 0, (hipStream_t)stream,
                                       pol == kPolBwdGenNoPair ? 0 : pol == kPolBwdGenPair ? 1 : 2,
-                                      pol != kPolBwdF32Lds && pol != kPolGeneric),
+                                      pol != kPolBwdF32Lds && pol != kPolGeneric, f32_fused ? f32_slab : 0),
                    "mt_flash_attn_bwd");
 }
 

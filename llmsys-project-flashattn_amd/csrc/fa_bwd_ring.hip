@@ -14,6 +14,8 @@
 // MultiHeadAttention runs.
 #include "fa_common.h"
 
+#include <algorithm>
+
 namespace mt {
 
 namespace {
@@ -319,6 +321,269 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
         }
     }
   }
+}
+
+// The fp32 backward with dQ in the dK/dV pass (fp32, 32 < d <= 64): 5 products per tile
+// instead of the split's 7. The dK/dV half is fa_bwd_dkv_ring's (key on the lane, register-row
+// K / V, Q / dO tiles of 32 queries through a two-slot ring) with 8 waves x 32 keys = 256 keys
+// per workgroup, one workgroup per CU (two waves per SIMD); the dQ half needs the query on the
+// lane, so each wave writes its dSᵀ values into an LDS image dS[query][key] (the transpose) and,
+// after a barrier, wave w computes one 16 x 16 tile (query half w & 1, d quarter w >> 1) of
+//     dQpart(tile) = dS(32 x 256) · K(256 x 64)
+// on v_mfma_f32_16x16x4_f32 from that image and a Kᵀ image [d][key] staged once per block (the
+// 256-key contraction in the permuted order key = 64 (lane >> 4) + s, so both operands are
+// 16-B LDS reads), and stores it to the slab [head][key block][query][64]. fa_bwd_ring_dq_sum
+// then sums each row's key blocks in block order: deterministic, no atomics (the reference
+// accumulates dQ serially inside its single pass, src/flashattention_kernel.cu:226-235).
+// LDS: ring 2 x 17.25 KiB + Kᵀ 65 KiB + dS 32.5 KiB = 132 KiB.
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+constexpr int kFrBKV = 256, kFrTL = kFrBKV + 4;  // keys per workgroup; image row (floats)
+constexpr int kFrSlot = 2 * 32 * 68 * 4 + 2 * 32 * 4;
+constexpr int kFrSmem = 2 * kFrSlot + (64 + 32) * kFrTL * 4;
+
+template <bool CAUSAL, bool PAIR>
+__global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* slab, int bh0) {
+  using T = float;
+  constexpr int DT = 64, EPC = 4, kLD = DT + EPC, kCPR = DT / EPC, KS = DT / 16, NDB = DT / 32;
+  constexpr int BKV = kFrBKV, BQ = 32, SLOT = kFrSlot, TL = kFrTL;
+  extern __shared__ __attribute__((aligned(16))) char smem_fr[];
+  char* ring = smem_fr;
+  float* KT = (float*)(smem_fr + 2 * SLOT);  // [64 d][TL]: Kᵀ of the block's 256 keys
+  float* dSi = KT + DT * TL;                 // [32 queries][TL]: the tile's dS
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int N = p.N, d = p.d;
+  int ublk, bhl;
+  xcd_order(ublk, bhl);
+  const int bh = bh0 + bhl;
+  const int b = bh / p.H, hh = bh % p.H;
+  const int nkb = (N + BKV - 1) / BKV;
+  const T* Qg = (const T*)p.q + b * p.sq[0] + hh * p.sq[1];
+  const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
+  const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
+  const T* dOg = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const float* lse2 = p.lse2 + (int64_t)bh * N;
+  const float* delta = p.delta + (int64_t)bh * N;
+  const float c2 = p.scale_log2;
+  // this wave's dQ tile: queries 16 qh .. + 15 of a 32-query tile, d columns 16 d4 .. + 15
+  const int qh = wave & 1, d4 = wave >> 1;
+  const int ia = (16 * qh + (lane & 15)) * TL + 64 * (lane >> 4);
+  const int ib = (16 * d4 + (lane & 15)) * TL + 64 * (lane >> 4);
+
+#pragma nounroll
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+    const int kblk = !PAIR ? ublk : pass == 0 ? nkb - 1 - ublk : ublk;
+    if (PAIR && pass == 1) {
+      if (kblk == nkb - 1 - ublk) break;  // odd nkb: the middle block runs alone
+      __syncthreads();                     // the first block's LDS reads are done
+    }
+    const int k0 = kblk * BKV;
+    const int my_k = k0 + wave * 32 + c32;
+    const int wave_kmin = k0 + wave * 32;
+    const int Nk = kv_keys(p, b);  // keys >= Nk are padding: zero gradients
+    const int kval = min(N, Nk);
+    Frag<T> bk[KS], bv[KS];
+    {
+      const int kr = min(my_k, N - 1);
+      row_frags(bk, Kg + (int64_t)kr * p.sk[2], d, hf);
+      row_frags(bv, Vg + (int64_t)kr * p.sv[2], d, hf);
+    }
+    // Kᵀ image: key r fastest across the lanes (conflict-free column stores), zero past the
+    // valid keys and past d
+#pragma unroll
+    for (int i = 0; i < (BKV * kCPR) / 512; ++i) {
+      const int ch = tid + 512 * i, r = ch % BKV, cc = (ch / BKV) * EPC, gr = k0 + r;
+      float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gr < kval && cc < d) v4 = *(const float4*)(Kg + (int64_t)gr * p.sk[2] + cc);
+      KT[(cc + 0) * TL + r] = v4.x;
+      KT[(cc + 1) * TL + r] = v4.y;
+      KT[(cc + 2) * TL + r] = v4.z;
+      KT[(cc + 3) * TL + r] = v4.w;
+    }
+    f32x16 dK[NDB], dV[NDB];
+#pragma unroll
+    for (int i = 0; i < NDB; ++i) { dK[i] = f32x16{}; dV[i] = f32x16{}; }
+
+    const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of BQ
+    const int ntile = N > qstart && k0 < Nk ? (N - qstart + BQ - 1) / BQ : 0;
+    uint4 pq, po;
+    float pl = 0.f, pd = 0.f;
+    auto pre_load = [&](int qt) __attribute__((always_inline)) {
+      const int r = tid / kCPR, cc = (tid % kCPR) * EPC, gr = qt + r;
+      pq = po = make_uint4(0, 0, 0, 0);
+      if (gr < N && cc < d) {
+        pq = *(const uint4*)(Qg + (int64_t)gr * p.sq[2] + cc);
+        po = *(const uint4*)(dOg + (int64_t)gr * p.sdo[2] + cc);
+      }
+      if (tid < BQ) {
+        const int q = qt + tid;
+        pl = q < N ? lse2[q] : 0.f;
+        pd = q < N ? delta[q] : 0.f;
+      }
+    };
+    auto pre_store = [&](int s) __attribute__((always_inline)) {
+      T* sQ = (T*)(ring + s * SLOT);
+      T* sO = sQ + BQ * kLD;
+      const int r = tid / kCPR, cc = (tid % kCPR) * EPC;
+      *(uint4*)(sQ + r * kLD + cc) = pq;
+      *(uint4*)(sO + r * kLD + cc) = po;
+      if (tid < BQ) {
+        float* sRow = (float*)(sO + BQ * kLD);
+        sRow[tid] = pl;
+        sRow[BQ + tid] = pd;
+      }
+    };
+    if (ntile > 0) {
+      pre_load(qstart);
+      pre_store(0);
+      if (ntile > 1) pre_load(qstart + BQ);
+    }
+    __syncthreads();
+    float* dst_base = slab + ((int64_t)bhl * nkb + kblk) * N * DT;
+
+    for (int t = 0; t < ntile; ++t) {
+      const int qt = qstart + t * BQ;
+      const T* sQ = (const T*)(ring + (t & 1) * SLOT);
+      const T* sO = sQ + BQ * kLD;
+      const float* sLse = (const float*)(sO + BQ * kLD);
+      const float* sDel = sLse + BQ;
+      if (!(CAUSAL && qt + BQ - 1 < wave_kmin)) {
+        f32x16 S = f32x16{}, dP = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int col = ks * 16 + 8 * hf;
+          mma(S, row_frag<T>(sQ + c32 * kLD + col), bk[ks]);
+          mma(dP, row_frag<T>(sO + c32 * kLD + col), bv[ks]);
+        }
+        const bool msk = qt + BQ > N || k0 + BKV > Nk || (CAUSAL && qt < wave_kmin + 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = acc_row(r, hf);
+          const int q = qt + ql;
+          float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(S[r], c2, -sLse[ql]));
+          if (msk && (q >= N || my_k >= Nk || (CAUSAL && my_k > q))) pv = 0.f;
+          S[r] = pv;
+          dP[r] = pv * (dP[r] - sDel[ql]);
+          dSi[ql * TL + wave * 32 + c32] = dP[r];
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const Frag<T> bp = acc_frag<T>(S, s), bs = acc_frag<T>(dP, s);
+#pragma unroll
+          for (int db = 0; db < NDB; ++db) {
+            mma(dV[db], col_frag<T>(sO, kLD, 16 * s + 4 * hf, db * 32, lane), bp);
+            mma(dK[db], col_frag<T>(sQ, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dSi[acc_row(r, hf) * TL + wave * 32 + c32] = 0.f;
+      }
+      __syncthreads();  // the tile's dS image is complete
+      {
+        f32x4 qa = f32x4{}, qb = f32x4{};
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+          const float4 a4 = *(const float4*)(dSi + ia + 4 * s4);
+          const float4 b4 = *(const float4*)(KT + ib + 4 * s4);
+          qa = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, qa, 0, 0, 0);
+          qb = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, qb, 0, 0, 0);
+          qa = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, qa, 0, 0, 0);
+          qb = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4.w, qb, 0, 0, 0);
+        }
+        const int col = 16 * d4 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = qt + 16 * qh + 4 * (lane >> 4) + j;
+          if (q < N) dst_base[(int64_t)q * DT + col] = qa[j] + qb[j];
+        }
+      }
+      if (t + 1 < ntile) {
+        pre_store((t + 1) & 1);
+        if (t + 2 < ntile) pre_load(qt + 2 * BQ);
+      }
+      __syncthreads();
+    }
+
+    if (my_k < N) {
+      T* dKg = (T*)p.dk + b * p.sdk[0] + hh * p.sdk[1] + (int64_t)my_k * p.sdk[2];
+      T* dVg = (T*)p.dv + b * p.sdv[0] + hh * p.sdv[1] + (int64_t)my_k * p.sdv[2];
+      const float sc = p.scale;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int col = db * 32 + 8 * g + 4 * hf;
+          if (col < d) {
+            store4(dKg + col, dK[db][4 * g] * sc, dK[db][4 * g + 1] * sc, dK[db][4 * g + 2] * sc,
+                   dK[db][4 * g + 3] * sc, true);
+            store4(dVg + col, dV[db][4 * g], dV[db][4 * g + 1], dV[db][4 * g + 2], dV[db][4 * g + 3],
+                   true);
+          }
+        }
+    }
+  }
+}
+
+// dQ = scale · Σ_kb slab[head][kb][q][:] over the key blocks that wrote row q (kb below the valid
+// keys' block count; causal: kb·256 <= q), in kb order. One thread per 16-B chunk of a row.
+__global__ __launch_bounds__(256) void fa_bwd_ring_dq_sum(AttnArgs p, const float* slab, int bh0, int ng,
+                                                          int causal) {
+  const int N = p.N, nkb = (N + kFrBKV - 1) / kFrBKV;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)ng * N * 16) return;
+  const int c = (int)(i & 15);
+  const int64_t rq = i >> 4;
+  const int bhl = (int)(rq / N), q = (int)(rq % N);
+  if (4 * c >= p.d) return;
+  const int bh = bh0 + bhl, b = bh / p.H, hh = bh % p.H;
+  int kb1 = (min(N, kv_keys(p, b)) + kFrBKV - 1) / kFrBKV;
+  if (causal) kb1 = min(kb1, q / kFrBKV + 1);
+  const float* src = slab + ((int64_t)bhl * nkb * N + q) * 64 + 4 * c;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int kb = 0; kb < kb1; ++kb) {
+    const float4 v = *(const float4*)(src + (int64_t)kb * N * 64);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  const float sc = p.scale;
+  float* dst = (float*)p.dq + b * p.sdq[0] + hh * p.sdq[1] + (int64_t)q * p.sdq[2] + 4 * c;
+  store4(dst, acc.x * sc, acc.y * sc, acc.z * sc, acc.w * sc, true);
+}
+
+// fp32 bytes of one head's dQ slab in the fused ring backward
+int64_t ring_fused_head_slab(int64_t N) { return ((N + kFrBKV - 1) / kFrBKV) * N * 64 * 4; }
+// the workspace region it asks for: the slab of one group of heads, at most 1 GiB per launch (0
+// when one head's slab is larger: the split ring runs)
+int64_t ring_fused_ws_bytes(int64_t B, int64_t H, int64_t N) {
+  constexpr int64_t cap = (int64_t)1 << 30;
+  const int64_t per = ring_fused_head_slab(N);
+  return per > cap ? 0 : std::min<int64_t>(B * H, cap / per) * per;
+}
+
+// The fused fp32 backward after the prep kernel: heads in groups whose slab fits slab_bytes
+// (the workspace's fused region), each group one pass and one ordered sum.
+hipError_t launch_bwd_ring_fused(const AttnArgs& a, bool causal, bool pair, int64_t slab_bytes, hipStream_t st) {
+  const int64_t per = ring_fused_head_slab(a.N), BH = (int64_t)a.B * a.H;
+  const int64_t grp = std::min<int64_t>(BH, slab_bytes / per);
+  if (grp < 1 || a.N < 1) return hipErrorInvalidValue;
+  const int nkb = (a.N + kFrBKV - 1) / kFrBKV;
+  auto kfn = causal ? (pair ? fa_bwd_fused_ring<true, true> : fa_bwd_fused_ring<true, false>)
+                    : fa_bwd_fused_ring<false, false>;
+  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kFrSmem);
+  if (e != hipSuccess) return e;
+  for (int64_t bh0 = 0; bh0 < BH; bh0 += grp) {
+    const int64_t ng = std::min<int64_t>(grp, BH - bh0);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)(pair ? (nkb + 1) / 2 : nkb), (unsigned)ng), dim3(512), kFrSmem, st, a,
+                       (float*)a.slab, (int)bh0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t nthr = ng * a.N * 16;
+    hipLaunchKernelGGL(fa_bwd_ring_dq_sum, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st, a,
+                       (const float*)a.slab, (int)bh0, (int)ng, causal ? 1 : 0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 template <typename T, int DT, bool CAUSAL, bool PAIR>

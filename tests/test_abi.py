@@ -51,6 +51,14 @@ def test_python_binding_covers_header():
         cnt = -(-(B * H * -(-N // 64) * 4) // 256) * 256
         return cnt + min(B * H, 2 ** 30 // head) * head
     assert lib.mt_flash_attn_bwd_workspace_bytes(2, 3, 5, 7) == 256
+    # ... or, when larger, the fp32 fused ring backward's partials (fa_bwd_fused_ring): one group
+    # of at most 1 GiB of ceil(N/256) * N * 64 fp32 per head (C2: 128 MiB, above the bf16 64 MiB)
+    def ring(B, H, N):
+        head = -(-N // 256) * N * 256
+        return min(B * H, 2 ** 30 // head) * head
+    assert lib.mt_flash_attn_bwd_workspace_bytes(8, 16, 1024, 64) == 2 * 128 * 1024 * 4 + ring(8, 16, 1024)
+    assert ring(8, 16, 1024) == 2 ** 27 > fused(8, 16, 1024)
+    assert lib.mt_flash_attn_bwd_workspace_bytes(2, 3, 300, 48) == 2 * 6 * 300 * 4 + 256 - (2 * 6 * 300 * 4) % 256 + ring(2, 3, 300)
     assert lib.mt_flash_attn_bwd_workspace_bytes(8, 16, 4096, 64) == 2 * 128 * 4096 * 4 + fused(8, 16, 4096)
     assert fused(8, 16, 4096) == 128 * 64 * 4 + 2 ** 30  # C3: one launch, 1 GiB of partials
     # longer sequences: head groups that reuse a slab of at most 1 GiB (N = 16384: 8 heads)

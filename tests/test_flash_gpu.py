@@ -1167,6 +1167,40 @@ def test_generic_causal_bwd_pairing_vs_oracle(torch_dev, policy, dtype, causal):
         _hip.set_policy(0)
 
 
+@pytest.mark.parametrize("causal", [False, True])
+def test_fp32_bwd_fused_ring_vs_oracle(torch_dev, causal, parity_record):
+    """The fp32 backward with dQ inside the dK/dV pass (fa_bwd_fused_ring: 256-key blocks, the
+    dQ partials summed per row in key-block order), which the default policy takes for 32 < d
+    <= 64 once its grid fills a workgroup per CU: BASELINE config 2 (8,16,1024,64) on all 128
+    heads, ragged N with d = 48, an odd block count (N = 640: the middle causal block alone) and
+    key padding, every head against the C oracle at the fp32 gradient bound 2e-5 x max|ref|;
+    and a bitwise-equal rerun (no atomics)."""
+    from minitorch import _hip
+    torch = torch_dev
+    rng = np.random.default_rng(61)
+    worst = 0.0
+    for (B, H, N, d, kv) in ((8, 16, 1024, 64, None), (2, 128, 300, 48, None), (1, 256, 640, 64, None),
+                             (2, 128, 300, 64, [300, 171])):
+        q, k, v, do = (rng.standard_normal((B, H, N, d)).astype(np.float32) for _ in range(4))
+        tq, tk, tv, tdo = (_dev(torch, x, torch.float32) for x in (q, k, v, do))
+        kvl = None if kv is None else torch.tensor(kv, dtype=torch.int32, device="cuda")
+        o, m, l = _hip.flash_fwd(tq, tk, tv, causal, kv_len=kvl)
+        grads = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, causal, kv_len=kvl)
+        again = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, causal, kv_len=kvl)
+        torch.cuda.synchronize()
+        for g1, g2 in zip(grads, again):
+            assert torch.equal(g1, g2)
+        o_ref, m_ref, l_ref = cref.attn_fwd(q, k, v, causal, kv_len=kv)
+        refs = cref.attn_bwd(q, k, v, do, m_ref, l_ref, causal, kv_len=kv)
+        scale = max(1.0, *(float(np.abs(r).max()) for r in refs))
+        for got, ref, name in zip(grads, refs, ("dq", "dk", "dv")):
+            err = float(np.abs(_np(got) - ref).max())
+            worst = max(worst, err / scale)
+            assert err <= 2e-5 * scale, f"{name} {(B, H, N, d)} kv={kv} max-abs {err:.3e} > {2e-5 * scale:.3e}"
+    parity_record("test_fp32_bwd_fused_ring_vs_oracle", f"causal={causal} C2 + ragged/odd/kv_len",
+                  max_err_over_bound=worst / 2e-5, bound="2e-5 x max|ref|")
+
+
 @pytest.mark.parametrize("policy", _shipped((0, 109, 110, 111)))
 @pytest.mark.parametrize("causal", [False, True])
 def test_fp32_fwd_policies_vs_oracle(torch_dev, policy, causal):
