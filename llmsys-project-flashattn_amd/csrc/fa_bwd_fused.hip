@@ -687,7 +687,12 @@ hipError_t launch_bwd_fused(const AttnArgs& a0, bool causal, void* ws, hipStream
     return hipErrorInvalidValue;
   a.dq_cnt = (unsigned*)ws;
   const int nkb = (a.N + kKB - 1) / kKB, nsa = (a.N + kStep - 1) / kStep;
-  const int64_t grp = fused_group_heads(B, H, N);
+  int64_t grp = fused_group_heads(B, H, N);
+#ifdef MT_DIAGNOSTICS
+  // A/B: smaller head groups (MT_FUSED_GROUP heads per launch), so a group's partials stay in
+  // the Infinity Cache between their store and the last arriver's read
+  if (const char* e = getenv("MT_FUSED_GROUP")) grp = std::max<int64_t>(1, std::min<int64_t>(grp, atoll(e)));
+#endif
   // causal: light/heavy pairs while the paired grid still has a workgroup per CU
   const bool pair = causal && (int64_t)((nkb + 1) / 2) * grp >= 256;
   // the product form (an A/B form of the kernel's VAR, see kFormRot)
