@@ -510,7 +510,8 @@ static hipError_t dispatch_bwd(const AttnArgs& a, bool vec, bool causal, bool pa
 }
 
 hipError_t launch_bwd_ring(const AttnArgs& a, bool bf16_io, bool causal, bool pair, hipStream_t st);
-hipError_t launch_bwd_ring_fused(const AttnArgs& a, bool causal, bool pair, int64_t slab_bytes, hipStream_t st);
+hipError_t launch_bwd_ring_fused(const AttnArgs& a, bool causal, bool pair, int64_t slab_bytes, bool prep,
+                                 hipStream_t st);
 int64_t ring_fused_head_slab(int64_t N);
 
 // pair: 0 never, 1 always (causal), 2 when the paired grid keeps >= 2 workgroups per CU.
@@ -522,16 +523,20 @@ hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
                               hipStream_t st, int pair, bool ring, int64_t fused_slab) {
   const bool pr = pair == 1 || (pair == 2 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
   if (ring && vec && (bf16_io ? a.d < 64 : a.d <= 64)) {
-    const hipError_t e = bf16_io ? launch_prep<bf16>(a, st) : launch_prep<float>(a, st);
-    if (e != hipSuccess) return e;
     const int64_t nkb = (a.N + 255) / 256;
     bool fpair = causal && nkb > 1;
+    bool fprep = prep_vec(a, 4);  // the fused kernel's own row constants need 16-B O chunks
 #ifdef MT_DIAGNOSTICS
     if (a.knob == 61) fpair = false;  // A/B: the causal fused ring backward unpaired
+    if (a.knob == 62) fprep = false;  // A/B: the prep kernel ahead of the fused pass
 #endif
-    if (!bf16_io && a.d > 32 && a.slab && fused_slab >= ring_fused_head_slab(a.N) &&
-        (fpair ? (nkb + 1) / 2 : nkb) * a.B * a.H >= 256)
-      return launch_bwd_ring_fused(a, causal, fpair, fused_slab, st);
+    const bool fused = !bf16_io && a.d > 32 && a.slab && fused_slab >= ring_fused_head_slab(a.N) &&
+                       (fpair ? (nkb + 1) / 2 : nkb) * a.B * a.H >= 256;
+    if (!(fused && fprep)) {
+      const hipError_t e = bf16_io ? launch_prep<bf16>(a, st) : launch_prep<float>(a, st);
+      if (e != hipSuccess) return e;
+    }
+    if (fused) return launch_bwd_ring_fused(a, causal, fpair, fused_slab, fprep, st);
     return launch_bwd_ring(a, bf16_io, causal, pr, st);
   }
   if (bf16_io) {

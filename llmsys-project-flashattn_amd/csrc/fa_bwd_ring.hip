@@ -341,7 +341,10 @@ constexpr int kFrBKV = 256, kFrTL = kFrBKV + 4;  // keys per workgroup; image ro
 constexpr int kFrSlot = 2 * 32 * 68 * 4 + 2 * 32 * 4;
 constexpr int kFrSmem = 2 * kFrSlot + (64 + 32) * kFrTL * 4;
 
-template <bool CAUSAL, bool PAIR>
+// PREP: the tile's row constants are formed here (lse2 = m·log2e + log2 l from the forward's
+// (m, l); δ = rowsum(dO ∘ O) from the staged dO chunks and the O chunks loaded beside them, the
+// 16 lanes of a row summed by xor shuffles: the prep kernel's arithmetic), no prep launch
+template <bool CAUSAL, bool PAIR, bool PREP = true>
 __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* slab, int bh0) {
   using T = float;
   constexpr int DT = 64, EPC = 4, kLD = DT + EPC, kCPR = DT / EPC, KS = DT / 16, NDB = DT / 32;
@@ -362,6 +365,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* s
   const T* Kg = (const T*)p.k + b * p.sk[0] + hh * p.sk[1];
   const T* Vg = (const T*)p.v + b * p.sv[0] + hh * p.sv[1];
   const T* dOg = (const T*)p.dout + b * p.sdo[0] + hh * p.sdo[1];
+  const T* Og = (const T*)p.o + b * p.so[0] + hh * p.so[1];
   const float* lse2 = p.lse2 + (int64_t)bh * N;
   const float* delta = p.delta + (int64_t)bh * N;
   const float c2 = p.scale_log2;
@@ -406,19 +410,25 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* s
 
     const int qstart = CAUSAL ? k0 : 0;  // k0 is a multiple of BQ
     const int ntile = N > qstart && k0 < Nk ? (N - qstart + BQ - 1) / BQ : 0;
-    uint4 pq, po;
+    uint4 pq, po, pa;
     float pl = 0.f, pd = 0.f;
     auto pre_load = [&](int qt) __attribute__((always_inline)) {
       const int r = tid / kCPR, cc = (tid % kCPR) * EPC, gr = qt + r;
-      pq = po = make_uint4(0, 0, 0, 0);
+      pq = po = pa = make_uint4(0, 0, 0, 0);
       if (gr < N && cc < d) {
         pq = *(const uint4*)(Qg + (int64_t)gr * p.sq[2] + cc);
         po = *(const uint4*)(dOg + (int64_t)gr * p.sdo[2] + cc);
+        if (PREP) pa = *(const uint4*)(Og + (int64_t)gr * p.so[2] + cc);
       }
       if (tid < BQ) {
         const int q = qt + tid;
-        pl = q < N ? lse2[q] : 0.f;
-        pd = q < N ? delta[q] : 0.f;
+        if (PREP) {  // (m, l) here, lse2 at the store
+          pl = q < N ? p.m[(int64_t)bh * N + q] : 0.f;
+          pd = q < N ? p.l[(int64_t)bh * N + q] : 1.f;
+        } else {
+          pl = q < N ? lse2[q] : 0.f;
+          pd = q < N ? delta[q] : 0.f;
+        }
       }
     };
     auto pre_store = [&](int s) __attribute__((always_inline)) {
@@ -427,8 +437,19 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* s
       const int r = tid / kCPR, cc = (tid % kCPR) * EPC;
       *(uint4*)(sQ + r * kLD + cc) = pq;
       *(uint4*)(sO + r * kLD + cc) = po;
-      if (tid < BQ) {
-        float* sRow = (float*)(sO + BQ * kLD);
+      float* sRow = (float*)(sO + BQ * kLD);
+      if (PREP) {
+        const float4 x = __builtin_bit_cast(float4, pa), y = __builtin_bit_cast(float4, po);
+        float a = 0.f;
+        a += x.x * y.x;
+        a += x.y * y.y;
+        a += x.z * y.z;
+        a += x.w * y.w;
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) a += __shfl_xor(a, off);
+        if ((tid & 15) == 0) sRow[BQ + r] = a;
+        if (tid < BQ) sRow[tid] = pl * kLog2e + log2f(pd);
+      } else if (tid < BQ) {
         sRow[tid] = pl;
         sRow[BQ + tid] = pd;
       }
@@ -562,13 +583,18 @@ int64_t ring_fused_ws_bytes(int64_t B, int64_t H, int64_t N) {
 
 // The fused fp32 backward after the prep kernel: heads in groups whose slab fits slab_bytes
 // (the workspace's fused region), each group one pass and one ordered sum.
-hipError_t launch_bwd_ring_fused(const AttnArgs& a, bool causal, bool pair, int64_t slab_bytes, hipStream_t st) {
+// prep: the kernel forms the row constants (PREP; the caller skipped the prep kernel), else
+// the caller ran fa_bwd_prep.
+hipError_t launch_bwd_ring_fused(const AttnArgs& a, bool causal, bool pair, int64_t slab_bytes, bool prep,
+                                 hipStream_t st) {
   const int64_t per = ring_fused_head_slab(a.N), BH = (int64_t)a.B * a.H;
   const int64_t grp = std::min<int64_t>(BH, slab_bytes / per);
   if (grp < 1 || a.N < 1) return hipErrorInvalidValue;
   const int nkb = (a.N + kFrBKV - 1) / kFrBKV;
-  auto kfn = causal ? (pair ? fa_bwd_fused_ring<true, true> : fa_bwd_fused_ring<true, false>)
-                    : fa_bwd_fused_ring<false, false>;
+  auto kfn = prep ? (causal ? (pair ? fa_bwd_fused_ring<true, true> : fa_bwd_fused_ring<true, false>)
+                            : fa_bwd_fused_ring<false, false>)
+                  : (causal ? (pair ? fa_bwd_fused_ring<true, true, false> : fa_bwd_fused_ring<true, false, false>)
+                            : fa_bwd_fused_ring<false, false, false>);
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kFrSmem);
   if (e != hipSuccess) return e;
   for (int64_t bh0 = 0; bh0 < BH; bh0 += grp) {

@@ -1197,7 +1197,23 @@ def test_fp32_bwd_fused_ring_vs_oracle(torch_dev, causal, parity_record):
             err = float(np.abs(_np(got) - ref).max())
             worst = max(worst, err / scale)
             assert err <= 2e-5 * scale, f"{name} {(B, H, N, d)} kv={kv} max-abs {err:.3e} > {2e-5 * scale:.3e}"
-    parity_record("test_fp32_bwd_fused_ring_vs_oracle", f"causal={causal} C2 + ragged/odd/kv_len",
+    # permuted views (minitorch's MHA hands over [B,N,H,d] buffers as [B,H,N,d] views)
+    B, H, N, d = 2, 128, 300, 64
+    base = [rng.standard_normal((B, N, H, d)).astype(np.float32) for _ in range(4)]
+    q, k, v, do = (np.ascontiguousarray(x.transpose(0, 2, 1, 3)) for x in base)
+    tq, tk, tv, tdo = (_dev(torch, x, torch.float32).permute(0, 2, 1, 3) for x in base)
+    assert not tq.is_contiguous()
+    o, m, l = _hip.flash_fwd(tq, tk, tv, causal)
+    grads = _hip.flash_bwd(tq, tk, tv, o, tdo, m, l, causal)
+    torch.cuda.synchronize()
+    o_ref, m_ref, l_ref = cref.attn_fwd(q, k, v, causal)
+    refs = cref.attn_bwd(q, k, v, do, m_ref, l_ref, causal)
+    scale = max(1.0, *(float(np.abs(r).max()) for r in refs))
+    for got, ref, name in zip(grads, refs, ("dq", "dk", "dv")):
+        err = float(np.abs(_np(got) - ref).max())
+        worst = max(worst, err / scale)
+        assert err <= 2e-5 * scale, f"{name} strided max-abs {err:.3e} > {2e-5 * scale:.3e}"
+    parity_record("test_fp32_bwd_fused_ring_vs_oracle", f"causal={causal} C2 + ragged/odd/kv_len/strided",
                   max_err_over_bound=worst / 2e-5, bound="2e-5 x max|ref|")
 
 
