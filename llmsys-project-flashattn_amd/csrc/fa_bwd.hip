@@ -525,7 +525,10 @@ hipError_t launch_bwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
   if (ring && vec && (bf16_io ? a.d < 64 : a.d <= 64)) {
     const int64_t nkb = (a.N + 255) / 256;
     bool fpair = causal && nkb > 1;
-    bool fprep = prep_vec(a, 4);  // the fused kernel's own row constants need 16-B O chunks
+    // the fused kernel's own row constants need 16-B O chunks; the paired causal X3 form keeps
+    // the prep kernel (forming them in the pass spilled 47 VGPRs there: C2 causal 0.377 against
+    // 0.360 ms, profiles/r6_ab_fp32_x3.txt)
+    bool fprep = prep_vec(a, 4) && !(causal && fpair);
 #ifdef MT_DIAGNOSTICS
     if (a.knob == 61) fpair = false;  // A/B: the causal fused ring backward unpaired
     if (a.knob == 62) fprep = false;  // A/B: the prep kernel ahead of the fused pass

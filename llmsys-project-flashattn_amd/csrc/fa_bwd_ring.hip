@@ -340,15 +340,24 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int kFrBKV = 256, kFrTL = kFrBKV + 4;  // keys per workgroup; image row (floats)
 constexpr int kFrSlot = 2 * 32 * 68 * 4 + 2 * 32 * 4;
 constexpr int kFrSmem = 2 * kFrSlot + (64 + 32) * kFrTL * 4;
+// X3: the Q and dO tiles as three bf16 planes each ([32][72]), then the row constants
+constexpr int kFrLDB = 72, kFrPlane = 32 * kFrLDB;
+constexpr int kFrSlotX3 = 6 * kFrPlane * 2 + 2 * 32 * 4;
+constexpr int kFrSmemX3 = 2 * kFrSlotX3 + (64 + 32) * kFrTL * 4;
 
 // PREP: the tile's row constants are formed here (lse2 = m·log2e + log2 l from the forward's
 // (m, l); δ = rowsum(dO ∘ O) from the staged dO chunks and the O chunks loaded beside them, the
 // 16 lanes of a row summed by xor shuffles: the prep kernel's arithmetic), no prep launch
-template <bool CAUSAL, bool PAIR, bool PREP = true>
+// X3: the four key-on-the-lane products (S, dP, dVᵀ, dKᵀ) on the bf16 MFMA with every fp32
+// operand in three bf16 pieces (fa_common.h mma_x3, fp32 accuracy): Q / dO tiles split once when
+// written to the ring, K / V once per block, P and dS per tile; the dQ product stays on
+// v_mfma_f32_16x16x4_f32 (its Kᵀ image as three planes would not fit the LDS)
+template <bool CAUSAL, bool PAIR, bool PREP = true, bool X3 = true>
 __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* slab, int bh0) {
   using T = float;
   constexpr int DT = 64, EPC = 4, kLD = DT + EPC, kCPR = DT / EPC, KS = DT / 16, NDB = DT / 32;
-  constexpr int BKV = kFrBKV, BQ = 32, SLOT = kFrSlot, TL = kFrTL;
+  constexpr int BKV = kFrBKV, BQ = 32, SLOT = X3 ? kFrSlotX3 : kFrSlot, TL = kFrTL;
+  constexpr int LDB = kFrLDB, PLANE = kFrPlane;
   extern __shared__ __attribute__((aligned(16))) char smem_fr[];
   char* ring = smem_fr;
   float* KT = (float*)(smem_fr + 2 * SLOT);  // [64 d][TL]: Kᵀ of the block's 256 keys
@@ -387,7 +396,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* s
     const int Nk = kv_keys(p, b);  // keys >= Nk are padding: zero gradients
     const int kval = min(N, Nk);
     Frag<T> bk[KS], bv[KS];
-    {
+    {  // (X3: split per use; held split, the three pieces took 32 more VGPRs and spilled)
       const int kr = min(my_k, N - 1);
       row_frags(bk, Kg + (int64_t)kr * p.sk[2], d, hf);
       row_frags(bv, Vg + (int64_t)kr * p.sv[2], d, hf);
@@ -435,9 +444,26 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* s
       T* sQ = (T*)(ring + s * SLOT);
       T* sO = sQ + BQ * kLD;
       const int r = tid / kCPR, cc = (tid % kCPR) * EPC;
-      *(uint4*)(sQ + r * kLD + cc) = pq;
-      *(uint4*)(sO + r * kLD + cc) = po;
-      float* sRow = (float*)(sO + BQ * kLD);
+      float* sRow;
+      if constexpr (X3) {  // Q planes h, m, l then dO's: 8 B of each per 16-B chunk
+        bf16* pl3 = (bf16*)(ring + s * SLOT);
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+          const float4 f = __builtin_bit_cast(float4, t2 ? po : pq);
+          unsigned h0, m0, l0, h1, m1, l1;
+          x3_split2(f.x, f.y, h0, m0, l0);
+          x3_split2(f.z, f.w, h1, m1, l1);
+          bf16* q3 = pl3 + 3 * t2 * PLANE + r * LDB + cc;
+          *(uint2*)(q3) = make_uint2(h0, h1);
+          *(uint2*)(q3 + PLANE) = make_uint2(m0, m1);
+          *(uint2*)(q3 + 2 * PLANE) = make_uint2(l0, l1);
+        }
+        sRow = (float*)(pl3 + 6 * PLANE);
+      } else {
+        *(uint4*)(sQ + r * kLD + cc) = pq;
+        *(uint4*)(sO + r * kLD + cc) = po;
+        sRow = (float*)(sO + BQ * kLD);
+      }
       if (PREP) {
         const float4 x = __builtin_bit_cast(float4, pa), y = __builtin_bit_cast(float4, po);
         float a = 0.f;
@@ -466,15 +492,32 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* s
       const int qt = qstart + t * BQ;
       const T* sQ = (const T*)(ring + (t & 1) * SLOT);
       const T* sO = sQ + BQ * kLD;
-      const float* sLse = (const float*)(sO + BQ * kLD);
+      const bf16* sQ3 = (const bf16*)(ring + (t & 1) * SLOT);  // X3: Q planes, then dO's
+      const bf16* sO3 = sQ3 + 3 * PLANE;
+      const float* sLse = X3 ? (const float*)(sQ3 + 6 * PLANE) : (const float*)(sO + BQ * kLD);
       const float* sDel = sLse + BQ;
       if (!(CAUSAL && qt + BQ - 1 < wave_kmin)) {
         f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int col = ks * 16 + 8 * hf;
-          mma(S, row_frag<T>(sQ + c32 * kLD + col), bk[ks]);
-          mma(dP, row_frag<T>(sO + c32 * kLD + col), bv[ks]);
+          if constexpr (X3) {
+            const int o = c32 * LDB + col;
+            X3Frag aq, ao;
+            aq.h = *(const bf16x8*)(sQ3 + o);
+            aq.m = *(const bf16x8*)(sQ3 + PLANE + o);
+            aq.l = *(const bf16x8*)(sQ3 + 2 * PLANE + o);
+            ao.h = *(const bf16x8*)(sO3 + o);
+            ao.m = *(const bf16x8*)(sO3 + PLANE + o);
+            ao.l = *(const bf16x8*)(sO3 + 2 * PLANE + o);
+            // (an opaque use per tile keeps hipcc from hoisting the loop-invariant splits)
+            asm volatile("" : "+v"(bk[ks]), "+v"(bv[ks]));
+            mma_x3(S, aq, x3_split(bk[ks]));
+            mma_x3(dP, ao, x3_split(bv[ks]));
+          } else {
+            mma(S, row_frag<T>(sQ + c32 * kLD + col), bk[ks]);
+            mma(dP, row_frag<T>(sO + c32 * kLD + col), bv[ks]);
+          }
         }
         const bool msk = qt + BQ > N || k0 + BKV > Nk || (CAUSAL && qt < wave_kmin + 31);
 #pragma unroll
@@ -489,11 +532,28 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_fused_ring(AttnArgs p, float* s
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const Frag<T> bp = acc_frag<T>(S, s), bs = acc_frag<T>(dP, s);
+          if constexpr (X3) {
+            const X3Frag bp = x3_split(acc_frag<float>(S, s)), bs = x3_split(acc_frag<float>(dP, s));
 #pragma unroll
-          for (int db = 0; db < NDB; ++db) {
-            mma(dV[db], col_frag<T>(sO, kLD, 16 * s + 4 * hf, db * 32, lane), bp);
-            mma(dK[db], col_frag<T>(sQ, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+            for (int db = 0; db < NDB; ++db) {
+              const int kq = 16 * s + 4 * hf;
+              X3Frag ao, aq;
+              ao.h = col_frag<bf16>(sO3, LDB, kq, db * 32, lane);
+              ao.m = col_frag<bf16>(sO3 + PLANE, LDB, kq, db * 32, lane);
+              ao.l = col_frag<bf16>(sO3 + 2 * PLANE, LDB, kq, db * 32, lane);
+              mma_x3(dV[db], ao, bp);
+              aq.h = col_frag<bf16>(sQ3, LDB, kq, db * 32, lane);
+              aq.m = col_frag<bf16>(sQ3 + PLANE, LDB, kq, db * 32, lane);
+              aq.l = col_frag<bf16>(sQ3 + 2 * PLANE, LDB, kq, db * 32, lane);
+              mma_x3(dK[db], aq, bs);
+            }
+          } else {
+            const Frag<T> bp = acc_frag<T>(S, s), bs = acc_frag<T>(dP, s);
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) {
+              mma(dV[db], col_frag<T>(sO, kLD, 16 * s + 4 * hf, db * 32, lane), bp);
+              mma(dK[db], col_frag<T>(sQ, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+            }
           }
         }
       } else {
@@ -591,15 +651,25 @@ hipError_t launch_bwd_ring_fused(const AttnArgs& a, bool causal, bool pair, int6
   const int64_t grp = std::min<int64_t>(BH, slab_bytes / per);
   if (grp < 1 || a.N < 1) return hipErrorInvalidValue;
   const int nkb = (a.N + kFrBKV - 1) / kFrBKV;
-  auto kfn = prep ? (causal ? (pair ? fa_bwd_fused_ring<true, true> : fa_bwd_fused_ring<true, false>)
-                            : fa_bwd_fused_ring<false, false>)
-                  : (causal ? (pair ? fa_bwd_fused_ring<true, true, false> : fa_bwd_fused_ring<true, false, false>)
-                            : fa_bwd_fused_ring<false, false, false>);
-  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, kFrSmem);
+  bool x3 = true;
+#ifdef MT_DIAGNOSTICS
+  if (a.knob == 65) x3 = false;  // A/B: every product on the fp32 MFMA
+#endif
+  void (*kfn)(AttnArgs, float*, int) =
+      x3 ? (prep ? (causal ? (pair ? fa_bwd_fused_ring<true, true> : fa_bwd_fused_ring<true, false>)
+                           : fa_bwd_fused_ring<false, false>)
+                 : (causal ? (pair ? fa_bwd_fused_ring<true, true, false> : fa_bwd_fused_ring<true, false, false>)
+                           : fa_bwd_fused_ring<false, false, false>))
+         : (prep ? (causal ? (pair ? fa_bwd_fused_ring<true, true, true, false> : fa_bwd_fused_ring<true, false, true, false>)
+                           : fa_bwd_fused_ring<false, false, true, false>)
+                 : (causal ? (pair ? fa_bwd_fused_ring<true, true, false, false> : fa_bwd_fused_ring<true, false, false, false>)
+                           : fa_bwd_fused_ring<false, false, false, false>));
+  const int smem = x3 ? kFrSmemX3 : kFrSmem;
+  hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
   if (e != hipSuccess) return e;
   for (int64_t bh0 = 0; bh0 < BH; bh0 += grp) {
     const int64_t ng = std::min<int64_t>(grp, BH - bh0);
-    hipLaunchKernelGGL(kfn, dim3((unsigned)(pair ? (nkb + 1) / 2 : nkb), (unsigned)ng), dim3(512), kFrSmem, st, a,
+    hipLaunchKernelGGL(kfn, dim3((unsigned)(pair ? (nkb + 1) / 2 : nkb), (unsigned)ng), dim3(512), smem, st, a,
                        (float*)a.slab, (int)bh0);
     e = hipGetLastError();
     if (e != hipSuccess) return e;

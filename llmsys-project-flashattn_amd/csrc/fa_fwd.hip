@@ -215,14 +215,23 @@ __global__ __launch_bounds__(256, 3) void fa_fwd_generic(AttnArgs p) {
 // half the workgroups, each filling the ring for its second block while it drains the first).
 // (32-key slots at four workgroups per CU, 128 VGPRs with 9 spilled, measured 4.8 % slower
 // non-causal and 22 % slower causal: profiles/r2m_ab_fp32_fwd_ring32.txt; not kept.)
-template <typename T, int DT, int KB, bool CAUSAL, bool PAIR>
+// X3 (fp32 only): both products on the bf16 MFMA with every fp32 operand in three bf16 pieces
+// (fa_common.h mma_x3: six 32x32x16 bf16 MFMAs per 16-deep k step, fp32 accuracy, 2.67x the
+// v_mfma_f32_32x32x2_f32 rate). Q is split once into registers; each K / V tile is split once
+// when it is written to the ring, into three bf16 planes ([BK][DT + 8] each, read like the bf16
+// kernel's tiles); P is split per tile in registers.
+template <typename T, int DT, int KB, bool CAUSAL, bool PAIR, bool X3 = false>
 __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
+  static_assert(!X3 || std::is_same<T, float>::value, "x3: fp32 inputs");
   constexpr int BQ = 128, BK = 32 * KB;
   constexpr int PAD = 16 / sizeof(T);
   constexpr int LD = DT + PAD;
   constexpr int SLOT = 2 * BK * LD;  // K then V
+  constexpr int LDB = DT + 8;        // X3: a bf16 plane's row (elements)
+  constexpr int PLANE = BK * LDB;    // X3: one bf16 plane (elements); a slot is K h, m, l, V h, m, l
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* ring = (T*)smem;
+  bf16* ring3 = (bf16*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
@@ -248,7 +257,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
 
   // Q row my_q (clamped; rows past N are computed but not stored), k-step ks: elements
   // 16 ks + 8 hf .. +7, zero past d (d is a multiple of 16 B here)
-  Frag<T> bq[DT / 16];
+  Frag<T> bq[X3 ? 1 : DT / 16];
+  X3Frag bq3[X3 ? DT / 16 : 1];
   {
     const T* qrow = Qg + (int64_t)min(my_q, N - 1) * p.sq[2];
 #pragma unroll
@@ -259,7 +269,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
         const int col = 16 * ks + 8 * hf + j * EPC;
         ch[j] = col < d ? *(const uint4*)(qrow + col) : make_uint4(0, 0, 0, 0);
       }
-      bq[ks] = __builtin_bit_cast(Frag<T>, ch);
+      if constexpr (X3)
+        bq3[ks] = x3_split(__builtin_bit_cast(f32x8, ch));
+      else
+        bq[ks] = __builtin_bit_cast(Frag<T>, ch);
     }
   }
 
@@ -284,6 +297,25 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
     }
   };
   auto pre_store = [&](int s) __attribute__((always_inline)) {
+    if constexpr (X3) {  // three bf16 planes per tensor: 8 B of each per 16-B chunk
+      bf16* sl = ring3 + s * 6 * PLANE;
+#pragma unroll
+      for (int i = 0; i < NCK; ++i) {
+        const int ch = tid + 256 * i, r = ch / CPR, cc = (ch % CPR) * EPC;
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+          const float4 f = __builtin_bit_cast(float4, t2 ? pv[i] : pk[i]);
+          unsigned h0, m0, l0, h1, m1, l1;
+          x3_split2(f.x, f.y, h0, m0, l0);
+          x3_split2(f.z, f.w, h1, m1, l1);
+          bf16* pl = sl + 3 * t2 * PLANE + r * LDB + cc;
+          *(uint2*)(pl) = make_uint2(h0, h1);
+          *(uint2*)(pl + PLANE) = make_uint2(m0, m1);
+          *(uint2*)(pl + 2 * PLANE) = make_uint2(l0, l1);
+        }
+      }
+      return;
+    }
     T* sK = ring + s * SLOT;
     T* sV = sK + BK * LD;
 #pragma unroll
@@ -304,6 +336,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
     const int k0 = t * BK;
     const T* sK = ring + (t & 1) * SLOT;
     const T* sV = sK + BK * LD;
+    const bf16* sK3 = ring3 + (t & 1) * 6 * PLANE;  // X3: K h, m, l planes, then V's
+    const bf16* sV3 = sK3 + 3 * PLANE;
     if (!(CAUSAL && k0 > wave_qmax)) {
       f32x16 S[KB];
 #pragma unroll
@@ -315,8 +349,17 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
       for (int ks = 0; ks < DT / 16; ++ks) {
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-          Frag<T> ak = row_frag<T>(sK + (kb * 32 + c32) * LD + ks * 16 + 8 * hf);
-          mma(S[kb], ak, bq[ks]);
+          if constexpr (X3) {
+            const int o = (kb * 32 + c32) * LDB + ks * 16 + 8 * hf;
+            X3Frag ak;
+            ak.h = *(const bf16x8*)(sK3 + o);
+            ak.m = *(const bf16x8*)(sK3 + PLANE + o);
+            ak.l = *(const bf16x8*)(sK3 + 2 * PLANE + o);
+            mma_x3(S[kb], ak, bq3[ks]);
+          } else {
+            Frag<T> ak = row_frag<T>(sK + (kb * 32 + c32) * LD + ks * 16 + 8 * hf);
+            mma(S[kb], ak, bq[ks]);
+          }
         }
       }
       // masks only on the ragged last tile and on tiles that reach past the wave's first
@@ -352,12 +395,35 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
         }
       l_run = l_run * alpha + rs;
       m_run = m_new;
+      // X3: the tile's PV in its own accumulator, added to the running O by a VALU fma: the
+      // bf16 MFMA's accumulation is not a round-to-nearest fp32 add chain, and over thousands
+      // of keys its error compounds into a bias (1.2e-5 relative in a dW_out at N = 4096, where
+      // the fp32 MFMA's chain stayed within 1e-6); within one 32-key tile it stays below 1e-6
+      f32x16 Ot[X3 ? DT / 32 : 1];
+      if constexpr (X3) {
 #pragma unroll
-      for (int i = 0; i < DT / 32; ++i) O[i] *= alpha;
+        for (int i = 0; i < DT / 32; ++i) Ot[i] = f32x16{};
+      } else {
+#pragma unroll
+        for (int i = 0; i < DT / 32; ++i) O[i] *= alpha;
+      }
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
+          if constexpr (X3) {
+            const X3Frag bp = x3_split(acc_frag<float>(S[kb], s));
+#pragma unroll
+            for (int db = 0; db < DT / 32; ++db) {
+              const int k0v = kb * 32 + 16 * s + 4 * hf;
+              X3Frag av;
+              av.h = col_frag<bf16>(sV3, LDB, k0v, db * 32, lane);
+              av.m = col_frag<bf16>(sV3 + PLANE, LDB, k0v, db * 32, lane);
+              av.l = col_frag<bf16>(sV3 + 2 * PLANE, LDB, k0v, db * 32, lane);
+              mma_x3(Ot[db], av, bp);
+            }
+            continue;
+          }
           Frag<T> bp = acc_frag<T>(S[kb], s);
 #pragma unroll
           for (int db = 0; db < DT / 32; ++db) {
@@ -365,6 +431,12 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
             mma(O[db], av, bp);
           }
         }
+      if constexpr (X3) {
+#pragma unroll
+        for (int i = 0; i < DT / 32; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) O[i][r] = __builtin_fmaf(O[i][r], alpha, Ot[i][r]);
+      }
     }
     if (t + 1 < ntiles) {
       pre_store((t + 1) & 1);
@@ -401,10 +473,12 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_generic_ring(AttnArgs p) {
   }  // pass
 }
 
-template <typename T, int DT, int KB, bool CAUSAL, bool PAIR>
+template <typename T, int DT, int KB, bool CAUSAL, bool PAIR, bool X3 = false>
 static hipError_t launch_fwd_ring_t(const AttnArgs& a, hipStream_t st) {
-  const size_t smem = sizeof(T) * (size_t)(DT + 16 / sizeof(T)) * 4 * 32 * KB;
-  auto kfn = fa_fwd_generic_ring<T, DT, KB, CAUSAL, PAIR>;
+  // two slots of K and V: fp32 / bf16 rows, or (X3) three bf16 planes each
+  const size_t smem = X3 ? (size_t)2 * 6 * 32 * KB * (DT + 8) * 2
+                         : sizeof(T) * (size_t)(DT + 16 / sizeof(T)) * 4 * 32 * KB;
+  auto kfn = fa_fwd_generic_ring<T, DT, KB, CAUSAL, PAIR, X3>;
   hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)smem);
   if (e != hipSuccess) return e;
@@ -463,6 +537,31 @@ hipError_t launch_fwd_generic(const AttnArgs& a, bool bf16_io, bool vec, bool ca
   }
   if (ring && vec && !bf16_io && a.d <= 64) {
     const bool pair = ring == 2 || (ring == 3 && (int64_t)((a.N + 255) / 256) * a.B * a.H >= 512);
+    // round 6: the products on the bf16 MFMA, every fp32 operand in three bf16 pieces (X3,
+    // fp32 accuracy: C2 0.277 -> 0.184 ms, causal 0.163 -> 0.108 ms, O within 6.9e-7 of the C
+    // oracle on every head against 8.0e-7 for the fp32 MFMA; profiles/r6_ab_fp32_fwd_x3.txt),
+    // 32-key slots (three planes per tensor: the 64-key form leaves one workgroup per CU and ran
+    // 0.246 ms)
+    bool x3 = true;
+#ifdef MT_DIAGNOSTICS
+    if (a.knob == 65) x3 = false;  // A/B: the v_mfma_f32_32x32x2_f32 ring
+    if (a.knob == 64)  // A/B: X3 with 64-key slots (one workgroup per CU)
+      return causal ? (pair ? launch_fwd_ring_t<float, 64, 2, true, true, true>(a, st)
+                            : launch_fwd_ring_t<float, 64, 2, true, false, true>(a, st))
+                    : (pair ? launch_fwd_ring_t<float, 64, 2, false, true, true>(a, st)
+                            : launch_fwd_ring_t<float, 64, 2, false, false, true>(a, st));
+#endif
+    if (x3) {
+      if (a.d <= 32)
+        return causal ? (pair ? launch_fwd_ring_t<float, 32, 1, true, true, true>(a, st)
+                              : launch_fwd_ring_t<float, 32, 1, true, false, true>(a, st))
+                      : (pair ? launch_fwd_ring_t<float, 32, 1, false, true, true>(a, st)
+                              : launch_fwd_ring_t<float, 32, 1, false, false, true>(a, st));
+      return causal ? (pair ? launch_fwd_ring_t<float, 64, 1, true, true, true>(a, st)
+                            : launch_fwd_ring_t<float, 64, 1, true, false, true>(a, st))
+                    : (pair ? launch_fwd_ring_t<float, 64, 1, false, true, true>(a, st)
+                            : launch_fwd_ring_t<float, 64, 1, false, false, true>(a, st));
+    }
     if (a.d <= 32)  // 32-column tiles: no zero-padded half of the QKᵀ and PV work (minitorch's
                     // MHA at config 5 has d = 256 / 8 = 32)
       return causal ? (pair ? launch_fwd_ring_t<float, 32, 2, true, true>(a, st)

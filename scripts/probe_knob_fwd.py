@@ -1,6 +1,6 @@
 """Probe (GPU box, diagnostics library): forward outputs under MT_KNOB values against knob 0
 (same kernel family, another schedule) and, on one head, against the C oracle.
-usage: MT_KNOBS=0,4 python scripts/probe_knob_fwd.py B,H,N,d [causal] [iters]"""
+usage: MT_KNOBS=0,4 python scripts/probe_knob_fwd.py B,H,N,d [causal] [iters]   (DTYPE=fp32: fp32 I/O)"""
 import os
 import sys
 
@@ -17,7 +17,8 @@ B, H, N, d = (int(x) for x in sys.argv[1].split(","))
 causal = "causal" in sys.argv[2:]
 iters = int(sys.argv[-1]) if sys.argv[-1].isdigit() else 0
 g = torch.Generator(device="cuda").manual_seed(5)
-q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
+dt = torch.float32 if os.environ.get("DTYPE") == "fp32" else torch.bfloat16
+q, k, v = (torch.randn((B, H, N, d), device="cuda", generator=g).to(dt) for _ in range(3))
 outs = {}
 for kn in os.environ.get("MT_KNOBS", "0").split(","):
     os.environ["MT_KNOB"] = kn
@@ -37,3 +38,9 @@ if not iters:
         o_ref = cref.attn_fwd(qs[None], ks[None], vs[None], causal)[0][0]
         for kn, (o, _) in outs.items():
             print(f"head ({b},{h}) knob {kn}: max |O - oracle| {np.abs(o[b, h].cpu().numpy() - o_ref).max():.3e}")
+    for kn, (o, lse) in outs.items():  # every head (DTYPE=fp32: the fp32 bound is 1e-5)
+        qs, ks, vs = (t.float().cpu().numpy().reshape(B * H, N, d) for t in (q, k, v))
+        o_ref, m_ref, l_ref = cref.attn_fwd(qs, ks, vs, causal)
+        err = np.abs(o.cpu().numpy().reshape(B * H, N, d) - o_ref).max()
+        lerr = np.abs(lse.cpu().numpy().reshape(B * H, N) - (m_ref + np.log(l_ref))).max()
+        print(f"all heads knob {kn}: max |O - oracle| {err:.3e}, max |lse - oracle| {lerr:.3e}")
