@@ -496,6 +496,11 @@ def extra_legs(torch, _hip, time_fn):
     extra["c2_fp32_fwd_ms"] = round(c2_ms, 4)
     extra["c2_fp32_fwd_tflops"] = round(fwd_flops(*c2) / (c2_ms * 1e-3) / 1e12, 2)
     extra["c2_fp32_frac_of_f32_peak"] = round(extra["c2_fp32_fwd_tflops"] / PEAK_F32_TFLOPS, 4)
+    # since round 6 the fp32 products run on the bf16 MFMA, every operand in three bf16 pieces
+    # (six bf16 products per fp32 product, fp32 accuracy), so the fp32-peak fraction can pass 1;
+    # the bf16 pipe's own fraction is 6 x the flops over the dense bf16 peak
+    extra["c2_fp32_method"] = "x3: fp32 products as six bf16 MFMA products (DESIGN.md §3)"
+    extra["c2_fp32_bf16_pipe_frac"] = round(6 * extra["c2_fp32_fwd_tflops"] / PEAK_BF16_TFLOPS, 4)
     ws2 = torch.empty(_hip.lib().mt_flash_attn_bwd_workspace_bytes(*c2) // 4, dtype=torch.float32,
                       device="cuda")
     g2 = [torch.empty_like(q2) for _ in range(3)]
