@@ -652,6 +652,155 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
   }
 }
 
+// Batched fp32 GEMM C[b] = A[b]·B[b] on the bf16 MFMA with every operand in three bf16 pieces
+// (fa_common.h mma_x3: six v_mfma_f32_32x32x16_bf16 per 16-deep k step, fp32 accuracy, 2.67x
+// the v_mfma_f32_32x32x2_f32 rate; the flash kernels' fp32 path uses the same split). A 64x64
+// tile per 256-thread workgroup (2 x 2 waves of 32x32), K staged 32 at a time: every thread
+// loads two 16-B chunks of A and of B along each operand's unit-stride dimension into
+// registers one stage ahead, splits them and writes 8 B per chunk to each of the three bf16
+// planes of a two-stage LDS ring. An operand contiguous along k (AK / BK) keeps planes
+// [row][k] and its MFMA fragment is two 8-B row reads; one contiguous along m (A) or n (B) keeps
+// planes [k][row] read by ds_read_b64_tr_b16 (the flash kernels' transposed V reads). Both take
+// the k order of that transposed read (element j of lane half h: k = 8 (j >> 2) + 4 h + (j & 3)),
+// so A and B agree. The MFMA accumulator is flushed into an fp32 register sum every 256 k (a
+// VALU add), so no single MFMA accumulation chain grows with K. Split-K: slice z % S covers k in
+// [slice·ks, (slice+1)·ks) and writes C (S = 1) or its own [S][M][N] partial (gemm_slice_sum).
+struct GemmX3Args {
+  const float* a; const float* b; float* c;
+  int64_t M, N, K, ks;  // ks: k per slice
+  int64_t sab, sam, sak, sbb, sbk, sbn, scb, scm, scn;
+  int S;
+};
+constexpr int kGxLDK = 40;                 // [row][k] plane row: 32 k + 8
+constexpr int kGxLDR = 72;                 // [k][row] plane row: 64 rows + 8
+constexpr int kGxPlane = 64 * kGxLDK;      // one plane (bf16 elements; 32 x 72 = 2304 fits too)
+constexpr int kGxStage = 6 * kGxPlane;     // A h, m, l then B h, m, l
+static_assert(32 * kGxLDR <= kGxPlane, "plane size");
+template <bool AK, bool BK, bool VEC>
+__global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmX3Args g) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[2 * kGxStage];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t bz = blockIdx.z / g.S, slice = blockIdx.z % g.S;
+  const int64_t m0 = (int64_t)blockIdx.y * 64, n0 = (int64_t)blockIdx.x * 64;
+  const float* A = g.a + bz * g.sab;
+  const float* B = g.b + bz * g.sbb;
+  const int64_t kbeg = slice * g.ks, kend = min(g.K, kbeg + g.ks);
+  // 16-B chunk c of an operand tile: along k (KC): row c / 8, k 4 (c % 8); along the rows:
+  // k c / 16, rows 4 (c % 16)
+  auto chunk = [&](const float* base, int64_t rs, int64_t rlim, int64_t r, int64_t k, bool kc) -> float4 {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t lim = kc ? kend : rlim;  // the contiguous dimension's end
+    const int64_t i0 = kc ? k : r;         // its index
+    if ((kc ? r >= rlim : k >= kend)) return v;
+    const float* p = base + (kc ? r * rs + k : k * rs + r);
+    if (VEC && i0 + 3 < lim) return *(const float4*)p;
+    if (i0 < lim) v.x = p[0];
+    if (i0 + 1 < lim) v.y = p[1];
+    if (i0 + 2 < lim) v.z = p[2];
+    if (i0 + 3 < lim) v.w = p[3];
+    return v;
+  };
+  float4 ra[2], rb[2];
+  auto load = [&](int64_t k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      ra[i] = AK ? chunk(A, g.sam, g.M, m0 + c / 8, k0 + 4 * (c % 8), true)
+                 : chunk(A, g.sak, g.M, m0 + 4 * (c % 16), k0 + c / 16, false);
+      rb[i] = BK ? chunk(B, g.sbn, g.N, n0 + c / 8, k0 + 4 * (c % 8), true)
+                 : chunk(B, g.sbk, g.N, n0 + 4 * (c % 16), k0 + c / 16, false);
+    }
+  };
+  auto store = [&](int st) __attribute__((always_inline)) {
+    bf16* base = sm + st * kGxStage;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+#pragma unroll
+      for (int op = 0; op < 2; ++op) {
+        const float4 v = op ? rb[i] : ra[i];
+        const bool kc = op ? BK : AK;
+        unsigned h0, m0_, l0, h1, m1, l1;
+        x3_split2(v.x, v.y, h0, m0_, l0);
+        x3_split2(v.z, v.w, h1, m1, l1);
+        bf16* pl = base + 3 * op * kGxPlane + (kc ? (c / 8) * kGxLDK + 4 * (c % 8) : (c / 16) * kGxLDR + 4 * (c % 16));
+        *(uint2*)(pl) = make_uint2(h0, h1);
+        *(uint2*)(pl + kGxPlane) = make_uint2(m0_, m1);
+        *(uint2*)(pl + 2 * kGxPlane) = make_uint2(l0, l1);
+      }
+    }
+  };
+  // the fragment of k step ks for row `row` (m or n) of a plane: row reads or transposed reads
+  typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+  auto frag = [&](const bf16* pl, int row, int ks, bool kc) -> bf16x8 {
+    if (kc) {
+      const bf16* q = pl + row * kGxLDK + 16 * ks + 4 * hf;
+      const u32x2 lo = *(const u32x2*)q, hi = *(const u32x2*)(q + 8);
+      const unsigned u[4] = {lo[0], lo[1], hi[0], hi[1]};
+      return __builtin_bit_cast(bf16x8, u);
+    }
+    return col_frag<bf16>(pl, kGxLDR, 16 * ks + 4 * hf, row - c32, lane);
+  };
+  f32x16 tot = f32x16{}, acc = f32x16{};
+  const int nst = (int)((kend - kbeg + 31) / 32);
+  if (nst > 0) {
+    load(kbeg);
+    store(0);
+    if (nst > 1) load(kbeg + 32);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const bf16* base = sm + (st & 1) * kGxStage;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ra_ = wm * 32 + c32, rb_ = wn * 32 + c32;
+      X3Frag fa, fb;
+      fa.h = frag(base, ra_, ks, AK);
+      fa.m = frag(base + kGxPlane, ra_, ks, AK);
+      fa.l = frag(base + 2 * kGxPlane, ra_, ks, AK);
+      fb.h = frag(base + 3 * kGxPlane, rb_, ks, BK);
+      fb.m = frag(base + 4 * kGxPlane, rb_, ks, BK);
+      fb.l = frag(base + 5 * kGxPlane, rb_, ks, BK);
+      // C[m][n] += A[m][k]·B[k][n]: A's row m as the A operand, B's column n as the B operand
+      mma_x3(acc, fa, fb);
+    }
+    if ((st & 7) == 7 || st + 1 == nst) {  // flush every 256 k
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tot[r] += acc[r];
+      acc = f32x16{};
+    }
+    if (st + 1 < nst) {
+      store((st + 1) & 1);
+      if (st + 2 < nst) load(kbeg + 32 * (st + 2));
+    }
+    __syncthreads();
+  }
+  // tot: column n0 + 32 wn + c32 on the lane, rows m0 + 32 wm + acc_row(r, hf)
+  const int64_t gn = n0 + wn * 32 + c32;
+  if (gn >= g.N) return;
+  float* C = g.c + (g.S > 1 ? slice * g.M * g.N : bz * g.scb);
+  const int64_t scm = g.S > 1 ? g.N : g.scm, scn = g.S > 1 ? 1 : g.scn;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t gm = m0 + wm * 32 + acc_row(r, hf);
+    if (gm < g.M) C[gm * scm + gn * scn] = tot[r];
+  }
+}
+
+// C = Σ_s part[s] (slice order: deterministic), C at row stride scm, column stride scn
+__global__ __launch_bounds__(256) void gemm_slice_sum(float* __restrict__ c, const float* __restrict__ part,
+                                                      int64_t M, int64_t N, int S, int64_t scm, int64_t scn) {
+  const int64_t n = M * N, step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += step) {
+    float a = part[t];
+    for (int s = 1; s < S; ++s) a += part[s * n + t];
+    const int64_t m = t / N, j = t - m * N;
+    c[m * scm + j * scn] = a;
+  }
+}
+
 static Layout make_layout(const int64_t* shape, const int64_t* strides, int dims) {
   Layout l;
   memset(&l, 0, sizeof(l));
@@ -1163,7 +1312,7 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   return check_hip(hipGetLastError(), "mt_tensor_reduce");
 }
 
-static int g_gemm_backend = 0;  // 0: rocBLAS where the layout allows, 1: own kernel only
+static int g_gemm_backend = 0;  // 0: rocBLAS where the layout allows, 1: own kernel only, 2: own X3 kernel
 
 void mt_set_gemm_backend(int backend) { g_gemm_backend = backend; }
 
@@ -1268,12 +1417,69 @@ static bool gemm_rocblas(float* c, const float* a, const float* b, int64_t batch
   return true;
 }
 
+// The X3 GEMM (gemm_x3_kernel): false when a layout has no unit stride (the caller falls back).
+// Split-K when one matrix has fewer than 256 output tiles and K >= 512 (config 5's 256 x 256
+// weight gradients over K = 4992: 16 tiles -> 16 slices).
+static bool gemm_x3(float* c, const float* a, const float* b, int64_t batch, int64_t M, int64_t N,
+                    int64_t K, const int64_t* sa, const int64_t* sb, const int64_t* sc, hipStream_t st) {
+  int64_t sam = sa[1], sak = sa[2], sbk = sb[1], sbn = sb[2];
+  if (K == 1) { sak = 1; sbk = 1; }
+  if (M == 1) sam = 1;
+  if (N == 1) sbn = 1;
+  const bool ak = sak == 1, bk = sbk == 1;
+  if ((!ak && sam != 1) || (!bk && sbn != 1)) return false;
+  if (batch > 65535) return false;
+  const int64_t tm = (M + 63) / 64, tn = (N + 63) / 64;
+  if (tm > 65535) return false;
+  int S = 1;
+  if (batch == 1 && tm * tn < 256 && K >= 512) {
+    S = (int)std::min<int64_t>(16, std::max<int64_t>(1, 256 / (tm * tn)));
+    S = (int)std::min<int64_t>(S, K / 256);
+  }
+  int64_t ks = K;
+  float* part = nullptr;
+  if (S > 1) {
+    ks = ((K + S - 1) / S + 31) / 32 * 32;
+    S = (int)((K + ks - 1) / ks);
+    if (S > 1) part = (float*)reduce_scratch((size_t)S * M * N * 4, st);
+    if (!part) { S = 1; ks = K; }
+  }
+  GemmX3Args g;
+  g.a = a; g.b = b; g.c = S > 1 ? part : c;
+  g.M = M; g.N = N; g.K = K; g.ks = ks; g.S = S;
+  g.sab = sa[0]; g.sam = sam; g.sak = sak;
+  g.sbb = sb[0]; g.sbk = sbk; g.sbn = sbn;
+  g.scb = sc[0]; g.scm = sc[1]; g.scn = sc[2];
+  const dim3 grid((unsigned)tn, (unsigned)tm, (unsigned)(batch * S));
+  // 16-B chunks: the bases and every stride but the unit one multiples of 4 floats
+  const int64_t oa = ak ? sam : sak, ob = bk ? sbn : sbk;
+  const bool vec = (((uintptr_t)a | (uintptr_t)b) & 15) == 0 && oa % 4 == 0 && ob % 4 == 0 &&
+                   (batch == 1 || (sa[0] % 4 == 0 && sb[0] % 4 == 0));
+#define MT_GX(AKV, BKV)                                                                            \
+  {                                                                                                \
+    if (vec) hipLaunchKernelGGL((gemm_x3_kernel<AKV, BKV, true>), grid, dim3(256), 0, st, g);      \
+    else hipLaunchKernelGGL((gemm_x3_kernel<AKV, BKV, false>), grid, dim3(256), 0, st, g);         \
+  }
+  if (ak && bk) MT_GX(true, true)
+  else if (ak) MT_GX(true, false)
+  else if (bk) MT_GX(false, true)
+  else MT_GX(false, false)
+#undef MT_GX
+  if (S > 1)
+    hipLaunchKernelGGL(gemm_slice_sum, dim3(grid_for(M * N)), dim3(256), 0, st, c, (const float*)part, M, N, S,
+                       sc[1], sc[2]);
+  return true;
+}
+
 int mt_matmul_f32(float* c, const float* a, const float* b, int64_t batch, int64_t M, int64_t N,
                   int64_t K, const int64_t* a_strides, const int64_t* b_strides,
                   const int64_t* c_strides, void* stream) {
   if (batch <= 0 || M <= 0 || N <= 0 || K <= 0)
     return set_error("mt_matmul_f32: bad sizes %lld %lld %lld %lld", (long long)batch,
                      (long long)M, (long long)N, (long long)K);
+  if (g_gemm_backend == 2 &&
+      gemm_x3(c, a, b, batch, M, N, K, a_strides, b_strides, c_strides, (hipStream_t)stream))
+    return check_hip(hipGetLastError(), "mt_matmul_f32(x3)");
   if (g_gemm_backend == 0) {
     rocblas_status rs = rocblas_status_success;
     if (gemm_rocblas(c, a, b, batch, M, N, K, a_strides, b_strides, c_strides, (hipStream_t)stream, &rs)) {

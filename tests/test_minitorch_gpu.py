@@ -243,10 +243,12 @@ def test_device_rand_and_dropout(mt):
 @pytest.mark.parametrize("shapes", [((5, 7), (7, 3)), ((4, 33, 65), (4, 65, 70)),
                                     ((2, 3, 17, 8), (2, 3, 8, 40)), ((1, 64, 96), (3, 96, 5)),
                                     ((4992, 256), (256, 256))])
-@pytest.mark.parametrize("gemm_backend", [0, 1])
+@pytest.mark.parametrize("gemm_backend", [0, 1, 2])
 def test_matmul(mt, shapes, gemm_backend):
-    """Batched matmul on both GEMM back ends (0: rocBLAS for plain layouts with the own
-    kernel for the rest, 1: own kernel only), plain, transposed and fully strided operands."""
+    """Batched matmul on the GEMM back ends (0: rocBLAS for plain layouts with the own
+    kernel for the rest, 1: own fp32-MFMA kernel only, 2: own X3 kernel (bf16 MFMA, three
+    pieces per operand) where an operand dimension has unit stride, else 1), plain,
+    transposed and fully strided operands."""
     from minitorch import _hip
     _hip.lib().mt_set_gemm_backend(gemm_backend)
     try:
@@ -255,13 +257,24 @@ def test_matmul(mt, shapes, gemm_backend):
         _hip.lib().mt_set_gemm_backend(0)
 
 
+@pytest.mark.parametrize("gemm_backend", [0, 2])
 @pytest.mark.parametrize("transposed", [False, True])
 @pytest.mark.parametrize("M,K,N", [(300, 8192, 64), (256, 4992, 256)])
-def test_matmul_split_k(mt, transposed, M, K, N):
+def test_matmul_split_k(mt, transposed, M, K, N, gemm_backend):
     """A long reduction into a small output (K >= 8192 under 128 output tiles: config 5's
     LM-head dX; K >= 4096 under 17 tiles: the linears' dW) runs as batched K slices plus an
-    ordered sum of the partials (combine.hip gemm_rocblas); against NumPy in fp64, plain and
-    with a transposed right operand, and bitwise repeatable."""
+    ordered sum of the partials (combine.hip gemm_rocblas; backend 2: the X3 kernel's own
+    slices and gemm_slice_sum); against NumPy in fp64, plain and with a transposed right
+    operand, and bitwise repeatable."""
+    from minitorch import _hip
+    _hip.lib().mt_set_gemm_backend(gemm_backend)
+    try:
+        _split_k_case(mt, transposed, M, K, N)
+    finally:
+        _hip.lib().mt_set_gemm_backend(0)
+
+
+def _split_k_case(mt, transposed, M, K, N):
     minitorch, B = mt
     rng = np.random.default_rng(7)
     x = rng.standard_normal((M, K)).astype(np.float32)
