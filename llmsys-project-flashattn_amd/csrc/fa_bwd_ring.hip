@@ -40,13 +40,21 @@ __device__ __forceinline__ void row_frags(Frag<T> (&f)[KS], const T* row, int d,
 
 // dK, dV: grid (nkb or ceil(nkb / 2) when PAIR, B*H); 4 waves x 32 keys; Q/dO tiles of 32
 // queries (with their lse2 / delta) streamed through the ring.
-template <typename T, int DT, bool CAUSAL, bool PAIR>
+// X3 (fp32): the four products on the bf16 MFMA in three pieces per operand (fa_common.h
+// mma_x3): the Q / dO tiles split once when written to the ring (three bf16 planes each), the
+// register K / V rows per use, P and dS per tile; dK and dV take each k-step's products in a
+// fresh sum added with a VALU fp32 add (x3_tile_sum). 1.28-1.43x the fp32-MFMA form, closer to
+// float64 on the MHA test's inputs (profiles/r6_x3_split_ring.txt).
+template <typename T, int DT, bool CAUSAL, bool PAIR, bool X3 = false>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
   // DT = 64, or 32 for d <= 32; rows padded by 16 B; NCK 16-B chunks per thread per 32-row tile
   constexpr int EPC = 16 / sizeof(T), kLD = DT + EPC, kCPR = DT / EPC;
   constexpr int NCK = (32 * kCPR + 255) / 256, KS = DT / 16, NDB = DT / 32;
   constexpr int BKV = 128, BQ = 32;
-  constexpr int SLOT = 2 * BQ * kLD * (int)sizeof(T) + 2 * BQ * 4;  // Q, dO, lse2, delta (bytes)
+  // Q, dO, lse2, delta (bytes); X3: Q and dO as three bf16 planes each ([32][DT + 8])
+  constexpr int LDB = DT + 8, PLANE = BQ * LDB;
+  constexpr int SLOT = X3 ? 6 * PLANE * 2 + 2 * BQ * 4 : 2 * BQ * kLD * (int)sizeof(T) + 2 * BQ * 4;
+  static_assert(!X3 || sizeof(T) == 4, "X3 splits fp32 operands");
   extern __shared__ __attribute__((aligned(16))) char ring[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, c32 = lane & 31;
@@ -73,6 +81,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
     const int k0 = kblk * BKV;
     const int my_k = k0 + wave * 32 + c32;
     const int wave_kmin = k0 + wave * 32;
+    // the causal skip bound; X3 non-causal: -1 behind an opaque copy, so the tile body stays a
+    // branch (as a branch-free body, hipcc 7.2 scheduled it into 200 spilled VGPRs at d = 64)
+    int skip_lim = CAUSAL ? wave_kmin : -1;
+    if (X3 && !CAUSAL) asm volatile("" : "+s"(skip_lim));
     const int Nk = kv_keys(p, b);  // keys >= Nk are padding: zero gradients
     Frag<T> bk[KS], bv[KS];
     {
@@ -111,12 +123,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
       for (int i = 0; i < NCK; ++i) {
         const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * EPC;
         if (ch < 32 * kCPR) {
-          *(uint4*)(sQ + r * kLD + cc) = pq[i];
-          *(uint4*)(sO + r * kLD + cc) = po[i];
+          if constexpr (X3) {
+            bf16* q3 = (bf16*)(ring + s * SLOT) + r * LDB + cc;
+            x3_store4(q3, PLANE, pq[i]);
+            x3_store4(q3 + 3 * PLANE, PLANE, po[i]);
+          } else {
+            *(uint4*)(sQ + r * kLD + cc) = pq[i];
+            *(uint4*)(sO + r * kLD + cc) = po[i];
+          }
         }
       }
       if (tid < BQ) {
-        float* sRow = (float*)(sO + BQ * kLD);
+        float* sRow = X3 ? (float*)((bf16*)(ring + s * SLOT) + 6 * PLANE) : (float*)(sO + BQ * kLD);
         sRow[tid] = pl;
         sRow[BQ + tid] = pd;
       }
@@ -128,20 +146,30 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
     }
     __syncthreads();
 
+#pragma nounroll
     for (int t = 0; t < ntile; ++t) {
       const int qt = qstart + t * BQ;
       const T* sQ = (const T*)(ring + (t & 1) * SLOT);
       const T* sO = sQ + BQ * kLD;
-      const float* sLse = (const float*)(sO + BQ * kLD);
+      const bf16* sQ3 = (const bf16*)(ring + (t & 1) * SLOT);  // X3: Q planes, then dO's
+      const bf16* sO3 = sQ3 + 3 * PLANE;
+      const float* sLse = X3 ? (const float*)(sQ3 + 6 * PLANE) : (const float*)(sO + BQ * kLD);
       const float* sDel = sLse + BQ;
-      if (!(CAUSAL && qt + BQ - 1 < wave_kmin)) {
+      if (!((CAUSAL || X3) && qt + BQ - 1 < skip_lim)) {
         // Sᵀ and dPᵀ: the lane's column is key my_k, rows are queries qt + acc_row(r, hf)
         f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int col = ks * 16 + 8 * hf;
-          mma(S, row_frag<T>(sQ + c32 * kLD + col), bk[ks]);
-          mma(dP, row_frag<T>(sO + c32 * kLD + col), bv[ks]);
+          if constexpr (X3) {
+            // (an opaque use per tile keeps hipcc from hoisting the loop-invariant splits)
+            asm volatile("" : "+v"(bk[ks]), "+v"(bv[ks]));
+            mma_x3(S, x3_rows(sQ3 + c32 * LDB + col, PLANE), x3_split(bk[ks]));
+            mma_x3(dP, x3_rows(sO3 + c32 * LDB + col, PLANE), x3_split(bv[ks]));
+          } else {
+            mma(S, row_frag<T>(sQ + c32 * kLD + col), bk[ks]);
+            mma(dP, row_frag<T>(sO + c32 * kLD + col), bv[ks]);
+          }
         }
         const bool msk = qt + BQ > N || k0 + BKV > Nk || (CAUSAL && qt < wave_kmin + 31);
 #pragma unroll
@@ -153,13 +181,29 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
           S[r] = pv;
           dP[r] = pv * (dP[r] - sDel[ql]);
         }
+        if constexpr (X3) {  // each k-step's products in a fresh sum (x3_tile_sum)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const Frag<T> bp = acc_frag<T>(S, s), bs = acc_frag<T>(dP, s);
+          for (int s = 0; s < 2; ++s) {
+            const X3Frag bp = x3_split(acc_frag<float>(S, s)), bs = x3_split(acc_frag<float>(dP, s));
 #pragma unroll
-          for (int db = 0; db < NDB; ++db) {
-            mma(dV[db], col_frag<T>(sO, kLD, 16 * s + 4 * hf, db * 32, lane), bp);
-            mma(dK[db], col_frag<T>(sQ, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+            for (int db = 0; db < NDB; ++db) {
+              f32x16 t = f32x16{};
+              mma_x3(t, x3_cols(sO3, PLANE, LDB, 16 * s + 4 * hf, db * 32, lane), bp);
+              dV[db] += t;
+              t = f32x16{};
+              mma_x3(t, x3_cols(sQ3, PLANE, LDB, 16 * s + 4 * hf, db * 32, lane), bs);
+              dK[db] += t;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const Frag<T> bp = acc_frag<T>(S, s), bs = acc_frag<T>(dP, s);
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) {
+              mma(dV[db], col_frag<T>(sO, kLD, 16 * s + 4 * hf, db * 32, lane), bp);
+              mma(dK[db], col_frag<T>(sQ, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+            }
           }
         }
       }
@@ -191,14 +235,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_ring(AttnArgs p) {
 }
 
 // dQ: grid (nqb or ceil(nqb / 2) when PAIR, B*H); 4 waves x 32 queries; K/V tiles of 32
-// keys streamed through the ring.
-template <typename T, int DT, bool CAUSAL, bool PAIR>
+// keys streamed through the ring. X3 (fp32): K / V tiles as three bf16 planes each, the register
+// Q / dO rows split per use, dS per tile, dQ's k-step sums fresh (as fa_bwd_dkv_ring).
+template <typename T, int DT, bool CAUSAL, bool PAIR, bool X3 = false>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
   // DT = 64, or 32 for d <= 32; rows padded by 16 B; NCK 16-B chunks per thread per 32-row tile
   constexpr int EPC = 16 / sizeof(T), kLD = DT + EPC, kCPR = DT / EPC;
   constexpr int NCK = (32 * kCPR + 255) / 256, KS = DT / 16, NDB = DT / 32;
   constexpr int BQ = 128, BK = 32;
-  constexpr int SLOT = 2 * BK * kLD;  // K, V (elements)
+  // K, V (elements of T); X3: K and V as three bf16 planes each ([32][DT + 8])
+  constexpr int LDB = DT + 8, PLANE = BK * LDB;
+  constexpr int SLOT = X3 ? 6 * PLANE * 2 / (int)sizeof(T) : 2 * BK * kLD;
+  static_assert(!X3 || sizeof(T) == 4, "X3 splits fp32 operands");
   extern __shared__ __attribute__((aligned(16))) char ring_raw[];
   T* ring = (T*)ring_raw;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -259,8 +307,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
       for (int i = 0; i < NCK; ++i) {
         const int ch = tid + 256 * i, r = ch / kCPR, cc = (ch % kCPR) * EPC;
         if (ch < 32 * kCPR) {
-          *(uint4*)(sK + r * kLD + cc) = pk[i];
-          *(uint4*)(sV + r * kLD + cc) = pv[i];
+          if constexpr (X3) {
+            bf16* k3 = (bf16*)sK + r * LDB + cc;
+            x3_store4(k3, PLANE, pk[i]);
+            x3_store4(k3 + 3 * PLANE, PLANE, pv[i]);
+          } else {
+            *(uint4*)(sK + r * kLD + cc) = pk[i];
+            *(uint4*)(sV + r * kLD + cc) = pv[i];
+          }
         }
       }
     };
@@ -271,18 +325,27 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
     }
     __syncthreads();
 
+#pragma nounroll
     for (int t = 0; t < ntile; ++t) {
       const int k0 = t * BK;
       const T* sK = ring + (t & 1) * SLOT;
       const T* sV = sK + BK * kLD;
+      const bf16* sK3 = (const bf16*)sK;  // X3: K planes, then V's
+      const bf16* sV3 = sK3 + 3 * PLANE;
       if (!(CAUSAL && k0 > wave_qmax)) {
         // S and dP with the query on the lane: rows are keys k0 + acc_row(r, hf)
         f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int col = ks * 16 + 8 * hf;
-          mma(S, row_frag<T>(sK + c32 * kLD + col), bq[ks]);
-          mma(dP, row_frag<T>(sV + c32 * kLD + col), bo[ks]);
+          if constexpr (X3) {
+            asm volatile("" : "+v"(bq[ks]), "+v"(bo[ks]));  // split per use (see fa_bwd_dkv_ring)
+            mma_x3(S, x3_rows(sK3 + c32 * LDB + col, PLANE), x3_split(bq[ks]));
+            mma_x3(dP, x3_rows(sV3 + c32 * LDB + col, PLANE), x3_split(bo[ks]));
+          } else {
+            mma(S, row_frag<T>(sK + c32 * kLD + col), bq[ks]);
+            mma(dP, row_frag<T>(sV + c32 * kLD + col), bo[ks]);
+          }
         }
         const bool msk = k0 + BK > Nk || (CAUSAL && k0 + BK - 1 > q0 + wave * 32);
 #pragma unroll
@@ -292,12 +355,23 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_ring(AttnArgs p) {
           if (msk && (key >= Nk || (CAUSAL && key > my_q))) pvv = 0.f;
           dP[r] = pvv * (dP[r] - del_q);
         }
+        if constexpr (X3) {  // the tile's products in a fresh sum (x3_tile_sum)
+          const X3Frag bs0 = x3_split(acc_frag<float>(dP, 0)), bs1 = x3_split(acc_frag<float>(dP, 1));
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const Frag<T> bs = acc_frag<T>(dP, s);
+          for (int db = 0; db < NDB; ++db) {
+            f32x16 t = f32x16{};
+            mma_x3(t, x3_cols(sK3, PLANE, LDB, 4 * hf, db * 32, lane), bs0);
+            mma_x3(t, x3_cols(sK3, PLANE, LDB, 16 + 4 * hf, db * 32, lane), bs1);
+            dQ[db] += t;
+          }
+        } else {
 #pragma unroll
-          for (int db = 0; db < NDB; ++db)
-            mma(dQ[db], col_frag<T>(sK, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+          for (int s = 0; s < 2; ++s) {
+            const Frag<T> bs = acc_frag<T>(dP, s);
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+              mma(dQ[db], col_frag<T>(sK, kLD, 16 * s + 4 * hf, db * 32, lane), bs);
+          }
         }
       }
       if (t + 1 < ntile) {
@@ -682,14 +756,21 @@ hipError_t launch_bwd_ring_fused(const AttnArgs& a, bool causal, bool pair, int6
   return hipSuccess;
 }
 
-template <typename T, int DT, bool CAUSAL, bool PAIR>
+template <typename T, int DT, bool CAUSAL, bool PAIR, bool X3 = false>
 static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
   constexpr int kLD = DT + 16 / (int)sizeof(T);
+  constexpr size_t kTile = X3 ? 6 * 32 * (DT + 8) * 2 : 2 * 32 * kLD * sizeof(T);  // bytes per ring slot
+  constexpr size_t kTileF = 2 * 32 * kLD * sizeof(T);
   const unsigned bhn = (unsigned)(a.B * a.H);
+  bool x3kv = X3, x3q = X3;
+#ifdef MT_DIAGNOSTICS
+  if (a.knob == 66) x3q = false;   // A/B: X3 in the dK/dV pass only
+  if (a.knob == 67) x3kv = false;  // A/B: X3 in the dQ pass only
+#endif
   {
     const int nkb = (a.N + 127) / 128;
-    const size_t smem = 2 * (2 * 32 * kLD * sizeof(T) + 2 * 32 * sizeof(float));
-    auto kfn = fa_bwd_dkv_ring<T, DT, CAUSAL, PAIR>;
+    const size_t smem = 2 * ((x3kv ? kTile : kTileF) + 2 * 32 * sizeof(float));
+    auto kfn = x3kv ? fa_bwd_dkv_ring<T, DT, CAUSAL, PAIR, X3> : fa_bwd_dkv_ring<T, DT, CAUSAL, PAIR, false>;
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)smem);
     if (e != hipSuccess) return e;
@@ -699,8 +780,8 @@ static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
   }
   {
     const int nqb = (a.N + 127) / 128;
-    const size_t smem = 2 * 2 * 32 * kLD * sizeof(T);
-    auto kfn = fa_bwd_dq_ring<T, DT, CAUSAL, PAIR>;
+    const size_t smem = 2 * (x3q ? kTile : kTileF);
+    auto kfn = x3q ? fa_bwd_dq_ring<T, DT, CAUSAL, PAIR, X3> : fa_bwd_dq_ring<T, DT, CAUSAL, PAIR, false>;
     hipError_t e = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)smem);
     if (e != hipSuccess) return e;
@@ -709,11 +790,11 @@ static hipError_t launch_bwd_ring_t(const AttnArgs& a, hipStream_t st) {
   }
 }
 
-template <typename T, int DT>
+template <typename T, int DT, bool X3 = false>
 static hipError_t launch_bwd_ring_d(const AttnArgs& a, bool causal, bool pair, hipStream_t st) {
   if (causal)
-    return pair ? launch_bwd_ring_t<T, DT, true, true>(a, st) : launch_bwd_ring_t<T, DT, true, false>(a, st);
-  return pair ? launch_bwd_ring_t<T, DT, false, true>(a, st) : launch_bwd_ring_t<T, DT, false, false>(a, st);
+    return pair ? launch_bwd_ring_t<T, DT, true, true, X3>(a, st) : launch_bwd_ring_t<T, DT, true, false, X3>(a, st);
+  return pair ? launch_bwd_ring_t<T, DT, false, true, X3>(a, st) : launch_bwd_ring_t<T, DT, false, false, X3>(a, st);
 }
 
 // 16-B rows, d <= 64 (fp32) or d < 64 (bf16, which the d = 64 MFMA backward does not take);
@@ -723,8 +804,14 @@ hipError_t launch_bwd_ring(const AttnArgs& a, bool bf16_io, bool causal, bool pa
   if (bf16_io)
     return a.d <= 32 ? launch_bwd_ring_d<bf16, 32>(a, causal, pair, st)
                      : launch_bwd_ring_d<bf16, 64>(a, causal, pair, st);
-  return a.d <= 32 ? launch_bwd_ring_d<float, 32>(a, causal, pair, st)
-                   : launch_bwd_ring_d<float, 64>(a, causal, pair, st);
+#ifdef MT_DIAGNOSTICS
+  if (a.knob == 65)  // A/B: every product on the fp32 MFMA
+    return a.d <= 32 ? launch_bwd_ring_d<float, 32>(a, causal, pair, st)
+                     : launch_bwd_ring_d<float, 64>(a, causal, pair, st);
+#endif
+  // fp32: the four products on the bf16 MFMA in three pieces per operand (fa_common.h mma_x3)
+  return a.d <= 32 ? launch_bwd_ring_d<float, 32, true>(a, causal, pair, st)
+                   : launch_bwd_ring_d<float, 64, true>(a, causal, pair, st);
 }
 
 }  // namespace mt

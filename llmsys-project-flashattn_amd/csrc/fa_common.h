@@ -138,6 +138,37 @@ __device__ __forceinline__ void mma_x3(f32x16& acc, const X3Frag& a, const X3Fra
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, acc, 0, 0, 0);
 }
+// x3_tile_sum: the bf16 MFMA's accumulation rounds toward -inf and loses more than an fp32
+// rounding when a small product meets a large running sum (measured, round 6: a dV row summed
+// over 32 tiles in one register sum drifted by about -7e-8 of its mean magnitude and erred 4x
+// the fp32-MFMA form on the MHA test's inputs; scripts/probe_x3_ring2.py). A kernel that
+// accumulates X3 products across tiles therefore takes each tile's products in a fresh
+// accumulator and adds it to the running sum with a VALU fp32 add (round to nearest).
+// LDS tiles held as three bf16 planes `plane` elements apart (h, m, l): a 16-B chunk of four
+// fp32 values goes in as 8 B per plane; fragments come out as row_frag / col_frag of each plane
+__device__ __forceinline__ void x3_store4(bf16* dst, int plane, const uint4& v) {
+  const float4 f = __builtin_bit_cast(float4, v);
+  unsigned h0, m0, l0, h1, m1, l1;
+  x3_split2(f.x, f.y, h0, m0, l0);
+  x3_split2(f.z, f.w, h1, m1, l1);
+  *(uint2*)(dst) = make_uint2(h0, h1);
+  *(uint2*)(dst + plane) = make_uint2(m0, m1);
+  *(uint2*)(dst + 2 * plane) = make_uint2(l0, l1);
+}
+__device__ __forceinline__ X3Frag x3_rows(const bf16* p, int plane) {
+  X3Frag f;
+  f.h = *(const bf16x8*)p;
+  f.m = *(const bf16x8*)(p + plane);
+  f.l = *(const bf16x8*)(p + 2 * plane);
+  return f;
+}
+__device__ __forceinline__ X3Frag x3_cols(const bf16* tile, int plane, int ld, int k0, int cbase, int lane) {
+  X3Frag f;
+  f.h = col_frag(tile, ld, k0, cbase, lane, (bf16x8*)nullptr);
+  f.m = col_frag(tile + plane, ld, k0, cbase, lane, (bf16x8*)nullptr);
+  f.l = col_frag(tile + 2 * plane, ld, k0, cbase, lane, (bf16x8*)nullptr);
+  return f;
+}
 
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
