@@ -174,7 +174,10 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
 int mt_matmul_f32(float* c, const float* a, const float* b, int64_t batch, int64_t M, int64_t N,
                   int64_t K, const int64_t* a_strides, const int64_t* b_strides,
                   const int64_t* c_strides, void* stream);
-/* 0 (default): rocBLAS for plain layouts; 1: the library's own GEMM kernel only (A/B). */
+/* 0 (default): rocBLAS for plain layouts; 1: the library's own fp32-MFMA GEMM kernel only;
+ * 2: the library's own fp32-accurate GEMM on the bf16 MFMA (three bf16 pieces per operand:
+ * 128x128 tiles where they fill the chip, else 64x64 with split-K); 3: that GEMM on 64x64
+ * tiles only (A/B). The environment variable MT_GEMM_BACKEND sets the initial value. */
 void mt_set_gemm_backend(int backend);
 
 /* out[0..n) <- U[0,1) from a stateless counter-based hash of (seed, index). Replaces the

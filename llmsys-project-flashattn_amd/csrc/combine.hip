@@ -789,6 +789,137 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmX3Args g) {
   }
 }
 
+// The same GEMM on a 128x128 tile (gemm_x3 takes it where those tiles alone fill the chip):
+// 2 x 2 waves of 64x64 (2 x 2 MFMA tiles of 32x32 each), K staged 16 at a time through a
+// two-stage ring of six planes (72 KiB: two workgroups per CU, two waves per SIMD). Each loaded
+// element is split once and feeds 128 outputs (64 in gemm_x3_kernel), and every barrier covers
+// 24 MFMAs per wave (12 there). Each k-step's six products go to a fresh sum added to the
+// running fp32 sum with a VALU add (fa_common.h x3_tile_sum). Split-K as gemm_x3_kernel.
+constexpr int kGbLDK = 24;                 // [row][k] plane row: 16 k + 8
+constexpr int kGbLDR = 136;                // [k][row] plane row: 128 rows + 8
+constexpr int kGbPlane = 128 * kGbLDK;     // 3072 elements (16 x 136 = 2176 fits too)
+constexpr int kGbStage = 6 * kGbPlane;
+static_assert(16 * kGbLDR <= kGbPlane, "plane size");
+template <bool AK, bool BK, bool VEC>
+__global__ __launch_bounds__(256, 2) void gemm_x3_big(GemmX3Args g) {
+  extern __shared__ __attribute__((aligned(16))) bf16 smb[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, c32 = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t bz = blockIdx.z / g.S, slice = blockIdx.z % g.S;
+  const int64_t m0 = (int64_t)blockIdx.y * 128, n0 = (int64_t)blockIdx.x * 128;
+  const float* A = g.a + bz * g.sab;
+  const float* B = g.b + bz * g.sbb;
+  const int64_t kbeg = slice * g.ks, kend = min(g.K, kbeg + g.ks);
+  auto chunk = [&](const float* base, int64_t rs, int64_t rlim, int64_t r, int64_t k, bool kc) -> float4 {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t lim = kc ? kend : rlim;
+    const int64_t i0 = kc ? k : r;
+    if ((kc ? r >= rlim : k >= kend)) return v;
+    const float* p = base + (kc ? r * rs + k : k * rs + r);
+    if (VEC && i0 + 3 < lim) return *(const float4*)p;
+    if (i0 < lim) v.x = p[0];
+    if (i0 + 1 < lim) v.y = p[1];
+    if (i0 + 2 < lim) v.z = p[2];
+    if (i0 + 3 < lim) v.w = p[3];
+    return v;
+  };
+  // 16-B chunk c (0..511) of a 128 x 16 operand tile: along k: row c / 4, k 4 (c % 4); along
+  // the rows: k c / 32, rows 4 (c % 32)
+  float4 ra[2], rb[2];
+  auto load = [&](int64_t k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      ra[i] = AK ? chunk(A, g.sam, g.M, m0 + c / 4, k0 + 4 * (c % 4), true)
+                 : chunk(A, g.sak, g.M, m0 + 4 * (c % 32), k0 + c / 32, false);
+      rb[i] = BK ? chunk(B, g.sbn, g.N, n0 + c / 4, k0 + 4 * (c % 4), true)
+                 : chunk(B, g.sbk, g.N, n0 + 4 * (c % 32), k0 + c / 32, false);
+    }
+  };
+  auto store = [&](int st) __attribute__((always_inline)) {
+    bf16* base = smb + st * kGbStage;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      x3_store4(base + (AK ? (c / 4) * kGbLDK + 4 * (c % 4) : (c / 32) * kGbLDR + 4 * (c % 32)), kGbPlane,
+                __builtin_bit_cast(uint4, ra[i]));
+      x3_store4(base + 3 * kGbPlane + (BK ? (c / 4) * kGbLDK + 4 * (c % 4) : (c / 32) * kGbLDR + 4 * (c % 32)),
+                kGbPlane, __builtin_bit_cast(uint4, rb[i]));
+    }
+  };
+  typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+  auto frag = [&](const bf16* pl, int row, int ks, bool kc) -> bf16x8 {
+    if (kc) {
+      const bf16* q = pl + row * kGbLDK + 16 * ks + 4 * hf;
+      const u32x2 lo = *(const u32x2*)q, hi = *(const u32x2*)(q + 8);
+      const unsigned u[4] = {lo[0], lo[1], hi[0], hi[1]};
+      return __builtin_bit_cast(bf16x8, u);
+    }
+    return col_frag<bf16>(pl, kGbLDR, 16 * ks + 4 * hf, row - c32, lane);
+  };
+  f32x16 tot[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) tot[i][j] = f32x16{};
+  const int nst = (int)((kend - kbeg + 15) / 16);
+  if (nst > 0) {
+    load(kbeg);
+    store(0);
+    if (nst > 1) load(kbeg + 16);
+  }
+  __syncthreads();
+#pragma nounroll
+  for (int st = 0; st < nst; ++st) {
+    const bf16* base = smb + (st & 1) * kGbStage;
+    {
+      constexpr int ks = 0;
+      X3Frag fb[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rb_ = wn * 64 + 32 * j + c32;
+        fb[j].h = frag(base + 3 * kGbPlane, rb_, ks, BK);
+        fb[j].m = frag(base + 4 * kGbPlane, rb_, ks, BK);
+        fb[j].l = frag(base + 5 * kGbPlane, rb_, ks, BK);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ra_ = wm * 64 + 32 * i + c32;
+        X3Frag fa;
+        fa.h = frag(base, ra_, ks, AK);
+        fa.m = frag(base + kGbPlane, ra_, ks, AK);
+        fa.l = frag(base + 2 * kGbPlane, ra_, ks, AK);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x16 t = f32x16{};
+          mma_x3(t, fa, fb[j]);
+          tot[i][j] += t;
+        }
+      }
+    }
+    if (st + 1 < nst) {
+      store((st + 1) & 1);
+      if (st + 2 < nst) load(kbeg + 16 * (st + 2));
+    }
+    __syncthreads();
+  }
+  float* C = g.c + (g.S > 1 ? slice * g.M * g.N : bz * g.scb);
+  const int64_t scm = g.S > 1 ? g.N : g.scm, scn = g.S > 1 ? 1 : g.scn;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t gn = n0 + wn * 64 + 32 * j + c32;
+    if (gn >= g.N) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t gm = m0 + wm * 64 + 32 * i + acc_row(r, hf);
+        if (gm < g.M) C[gm * scm + gn * scn] = tot[i][j][r];
+      }
+  }
+}
+
 // C = Σ_s part[s] (slice order: deterministic), C at row stride scm, column stride scn
 __global__ __launch_bounds__(256) void gemm_slice_sum(float* __restrict__ c, const float* __restrict__ part,
                                                       int64_t M, int64_t N, int S, int64_t scm, int64_t scn) {
@@ -1312,7 +1443,15 @@ int mt_tensor_reduce(int fn, float* out, const int64_t* out_shape, const int64_t
   return check_hip(hipGetLastError(), "mt_tensor_reduce");
 }
 
-static int g_gemm_backend = 0;  // 0: rocBLAS where the layout allows, 1: own kernel only, 2: own X3 kernel
+// 0: rocBLAS where the layout allows; 1: own fp32-MFMA kernel only; 2: own X3 kernels (128x128
+// tiles where they fill the chip, else 64x64); 3: X3 on 64x64 tiles only (A/B). MT_GEMM_BACKEND
+// sets the process default.
+static int initial_gemm_backend() {
+  const char* e = getenv("MT_GEMM_BACKEND");
+  const int v = e ? atoi(e) : 0;
+  return v >= 0 && v <= 3 ? v : 0;
+}
+static int g_gemm_backend = initial_gemm_backend();
 
 void mt_set_gemm_backend(int backend) { g_gemm_backend = backend; }
 
@@ -1420,8 +1559,10 @@ static bool gemm_rocblas(float* c, const float* a, const float* b, int64_t batch
 // The X3 GEMM (gemm_x3_kernel): false when a layout has no unit stride (the caller falls back).
 // Split-K when one matrix has fewer than 256 output tiles and K >= 512 (config 5's 256 x 256
 // weight gradients over K = 4992: 16 tiles -> 16 slices).
+// big: 128x128 tiles where they fill the chip (alone or as k-slices), else 64x64.
 static bool gemm_x3(float* c, const float* a, const float* b, int64_t batch, int64_t M, int64_t N,
-                    int64_t K, const int64_t* sa, const int64_t* sb, const int64_t* sc, hipStream_t st) {
+                    int64_t K, const int64_t* sa, const int64_t* sb, const int64_t* sc, hipStream_t st,
+                    bool big) {
   int64_t sam = sa[1], sak = sa[2], sbk = sb[1], sbn = sb[2];
   if (K == 1) { sak = 1; sbk = 1; }
   if (M == 1) sam = 1;
@@ -1429,6 +1570,55 @@ static bool gemm_x3(float* c, const float* a, const float* b, int64_t batch, int
   const bool ak = sak == 1, bk = sbk == 1;
   if ((!ak && sam != 1) || (!bk && sbn != 1)) return false;
   if (batch > 65535) return false;
+  // 16-B chunks: the bases and every stride but the unit one multiples of 4 floats
+  const int64_t oa = ak ? sam : sak, ob = bk ? sbn : sbk;
+  const bool vec = (((uintptr_t)a | (uintptr_t)b) & 15) == 0 && oa % 4 == 0 && ob % 4 == 0 &&
+                   (batch == 1 || (sa[0] % 4 == 0 && sb[0] % 4 == 0));
+  const int64_t tm2 = (M + 127) / 128, tn2 = (N + 127) / 128;
+  // 128x128 tiles where they fill the chip, alone or as up to 8 k-slices of >= 1024
+  int S2 = 1;
+  if (batch == 1 && tm2 * tn2 < 256) S2 = (int)std::min<int64_t>((256 + tm2 * tn2 - 1) / (tm2 * tn2), K / 1024);
+  int64_t ks2 = K;
+  if (S2 > 8) S2 = 1;
+  if (S2 > 1) {
+    ks2 = ((K + S2 - 1) / S2 + 15) / 16 * 16;
+    S2 = (int)((K + ks2 - 1) / ks2);
+  }
+  float* part2 = nullptr;
+  if (big && batch * tm2 * tn2 * S2 >= 256 && tm2 <= 65535 &&
+      (S2 == 1 || (part2 = (float*)reduce_scratch((size_t)S2 * M * N * 4, st)) != nullptr)) {
+    GemmX3Args g;
+    g.a = a; g.b = b; g.c = S2 > 1 ? part2 : c;
+    g.M = M; g.N = N; g.K = K; g.ks = ks2; g.S = S2;
+    g.sab = sa[0]; g.sam = sam; g.sak = sak;
+    g.sbb = sb[0]; g.sbk = sbk; g.sbn = sbn;
+    g.scb = sc[0]; g.scm = sc[1]; g.scn = sc[2];
+    const dim3 grid((unsigned)tn2, (unsigned)tm2, (unsigned)(batch * S2));
+    constexpr int smem = 2 * kGbStage * 2;
+#define MT_GB(AKV, BKV, VV)                                                                          \
+  {                                                                                                \
+    static const hipError_t attr = hipFuncSetAttribute(                                            \
+        (const void*)gemm_x3_big<AKV, BKV, VV>, hipFuncAttributeMaxDynamicSharedMemorySize, smem); \
+    if (attr != hipSuccess) return false;                                                          \
+    hipLaunchKernelGGL((gemm_x3_big<AKV, BKV, VV>), grid, dim3(256), smem, st, g);                 \
+  }
+    if (vec) {
+      if (ak && bk) MT_GB(true, true, true)
+      else if (ak) MT_GB(true, false, true)
+      else if (bk) MT_GB(false, true, true)
+      else MT_GB(false, false, true)
+    } else {
+      if (ak && bk) MT_GB(true, true, false)
+      else if (ak) MT_GB(true, false, false)
+      else if (bk) MT_GB(false, true, false)
+      else MT_GB(false, false, false)
+    }
+#undef MT_GB
+    if (S2 > 1)
+      hipLaunchKernelGGL(gemm_slice_sum, dim3(grid_for(M * N)), dim3(256), 0, st, c, (const float*)part2, M, N, S2,
+                         sc[1], sc[2]);
+    return true;
+  }
   const int64_t tm = (M + 63) / 64, tn = (N + 63) / 64;
   if (tm > 65535) return false;
   int S = 1;
@@ -1451,10 +1641,6 @@ static bool gemm_x3(float* c, const float* a, const float* b, int64_t batch, int
   g.sbb = sb[0]; g.sbk = sbk; g.sbn = sbn;
   g.scb = sc[0]; g.scm = sc[1]; g.scn = sc[2];
   const dim3 grid((unsigned)tn, (unsigned)tm, (unsigned)(batch * S));
-  // 16-B chunks: the bases and every stride but the unit one multiples of 4 floats
-  const int64_t oa = ak ? sam : sak, ob = bk ? sbn : sbk;
-  const bool vec = (((uintptr_t)a | (uintptr_t)b) & 15) == 0 && oa % 4 == 0 && ob % 4 == 0 &&
-                   (batch == 1 || (sa[0] % 4 == 0 && sb[0] % 4 == 0));
 #define MT_GX(AKV, BKV)                                                                            \
   {                                                                                                \
     if (vec) hipLaunchKernelGGL((gemm_x3_kernel<AKV, BKV, true>), grid, dim3(256), 0, st, g);      \
@@ -1477,8 +1663,9 @@ int mt_matmul_f32(float* c, const float* a, const float* b, int64_t batch, int64
   if (batch <= 0 || M <= 0 || N <= 0 || K <= 0)
     return set_error("mt_matmul_f32: bad sizes %lld %lld %lld %lld", (long long)batch,
                      (long long)M, (long long)N, (long long)K);
-  if (g_gemm_backend == 2 &&
-      gemm_x3(c, a, b, batch, M, N, K, a_strides, b_strides, c_strides, (hipStream_t)stream))
+  if ((g_gemm_backend == 2 || g_gemm_backend == 3) &&
+      gemm_x3(c, a, b, batch, M, N, K, a_strides, b_strides, c_strides, (hipStream_t)stream,
+              g_gemm_backend == 2))
     return check_hip(hipGetLastError(), "mt_matmul_f32(x3)");
   if (g_gemm_backend == 0) {
     rocblas_status rs = rocblas_status_success;

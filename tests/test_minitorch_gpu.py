@@ -275,6 +275,43 @@ def test_matmul_split_k(mt, transposed, M, K, N, gemm_backend):
         _hip.lib().mt_set_gemm_backend(0)
 
 
+@pytest.mark.parametrize("case", ["fwd", "dx", "dw"])
+def test_matmul_x3_128_tiles(mt, case):
+    """Backend 2's 128x128 X3 GEMM (combine.hip gemm_x3_big) on config 5's LM-head shapes in the
+    layouts minitorch hands over: the forward [4992, 256] x [256, 10000] (3081 tiles, one pass),
+    dX = dC·Wᵀ (K = 10000, 78 tiles: four K slices plus gemm_slice_sum, right operand
+    transposed) and dW = Xᵀ·dC (K = 4992, left operand transposed, two slices). Against fp64:
+    error over max|ref| at most 1e-6 (measured 2.1-4.1e-7; rocBLAS sgemm 0.8-3.4e-6 on the same
+    products, profiles/r6_gemm_x3.txt); bitwise repeatable."""
+    import torch
+    from minitorch import _hip
+    g = torch.Generator(device="cuda").manual_seed(3)
+    T, E, V = 4992, 256, 10000
+    x = torch.randn(T, E, device="cuda", generator=g)
+    wl = torch.randn(E, V, device="cuda", generator=g) * 0.05
+    dc = torch.randn(T, V, device="cuda", generator=g) * 0.01
+    a, b = {"fwd": (x, wl), "dx": (dc, wl.t()), "dw": (x.t(), dc)}[case]
+    lib = _hip.lib()
+    s3 = lambda t: (ctypes.c_int64 * 3)(0, t.stride(0), t.stride(1))  # noqa: E731
+
+    def run():
+        c = torch.empty(a.shape[0], b.shape[1], device="cuda")
+        _hip.check(lib.mt_matmul_f32(c.data_ptr(), a.data_ptr(), b.data_ptr(), 1, a.shape[0], b.shape[1],
+                                     a.shape[1], s3(a), s3(b), s3(c), _hip.stream_ptr()), "mt_matmul_f32")
+        torch.cuda.synchronize()
+        return c
+
+    lib.mt_set_gemm_backend(2)
+    try:
+        c1, c2 = run(), run()
+    finally:
+        lib.mt_set_gemm_backend(0)
+    ref = a.double() @ b.double()
+    err = float((c1.double() - ref).abs().max() / ref.abs().max())
+    assert err <= 1e-6, err
+    assert torch.equal(c1, c2)
+
+
 def _split_k_case(mt, transposed, M, K, N):
     minitorch, B = mt
     rng = np.random.default_rng(7)
